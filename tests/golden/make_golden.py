@@ -1,0 +1,363 @@
+"""Generate the golden parity fixtures from the reference implementation.
+
+Runs ONLY in the build container, where the read-only reference checkout lives at
+/root/reference. It imports the reference's own Python modules (the reference is
+never copied into this repository and never travels to the GPU box) and records
+small input/output vectors as .npz files next to this script. Those .npz files are
+the pins for both the CPU oracle (oracle/) and the HIP product path.
+
+Offline stand-ins: `gym` is not installed, so a minimal module
+providing the names the reference imports is registered in sys.modules; the
+orbital-simulator dependencies (astropy, poliastro, h3, shapely) are only needed for
+import-time side effects of envs/__init__.py and are satisfied with MagicMock.
+
+Usage:  python tests/golden/make_golden.py          (rewrites every fixture)
+
+Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
+  mt19937_words.npz   raw legacy-MT19937 32-bit words after np.random.seed(s)
+  mock_reset.npz      construct + reset of MockConstellationEnv for several seeds/shapes
+  mock_step.npz       per-step rewards / obs / beta / done for injected tables
+  lsa.npz             scipy.optimize.linear_sum_assignment input/output pairs
+  runner_dumps.npz    EpisodeRunner / ParallelRunner EpisodeBatch dumps (layout + quirks)
+"""
+import os
+import sys
+import types
+from types import SimpleNamespace
+from unittest import mock
+
+import numpy as np
+
+REF_SRC = "/root/reference/src"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------------
+# offline stand-ins
+# ----------------------------------------------------------------------------------
+class _GymEnv:  # the reference only subclasses gym.Env
+    pass
+
+
+class _GymObservationWrapper:
+    def __init__(self, env=None):
+        self.env = env
+
+
+class _Space:
+    def __init__(self, *a, **k):
+        self.args, self.kwargs = a, k
+
+
+class _Tuple(_Space):
+    pass
+
+
+class _Discrete(_Space):
+    pass
+
+
+class _Box(_Space):
+    pass
+
+
+def _flatdim(space):
+    return 0
+
+
+def _np_random(seed=None):
+    # gym's helper builds a private generator; it never touches the global stream
+    return np.random.RandomState(), seed
+
+
+class _TimeLimit:
+    def __init__(self, env, max_episode_steps=None):
+        self.env = env
+
+
+def _install_stubs():
+    # module-level classes so that envs stay picklable across the ParallelRunner pipes
+    gym = types.ModuleType("gym")
+    Env, ObservationWrapper = _GymEnv, _GymObservationWrapper
+    spaces = types.ModuleType("gym.spaces")
+    spaces.Tuple, spaces.Discrete, spaces.Box, spaces.flatdim = _Tuple, _Discrete, _Box, _flatdim
+    utils = types.ModuleType("gym.utils")
+    seeding = types.ModuleType("gym.utils.seeding")
+    np_random = _np_random
+    seeding.np_random = np_random
+    utils.seeding = seeding
+    envs_mod = types.ModuleType("gym.envs")
+    envs_mod.registry = {}
+    wrappers = types.ModuleType("gym.wrappers")
+    wrappers.TimeLimit = _TimeLimit
+    gym.Env, gym.ObservationWrapper, gym.spaces = Env, ObservationWrapper, spaces
+    gym.utils, gym.envs, gym.wrappers = utils, envs_mod, wrappers
+    for name, mod in {"gym": gym, "gym.spaces": spaces, "gym.utils": utils,
+                      "gym.utils.seeding": seeding, "gym.envs": envs_mod,
+                      "gym.wrappers": wrappers}.items():
+        sys.modules[name] = mod
+    for name in ["astropy", "astropy.units", "poliastro", "poliastro.bodies",
+                 "poliastro.twobody", "poliastro.spheroid_location", "poliastro.core",
+                 "poliastro.core.events", "h3", "shapely", "shapely.geometry"]:
+        sys.modules[name] = mock.MagicMock()
+    sys.path.insert(0, REF_SRC)
+
+
+# ----------------------------------------------------------------------------------
+def gen_mt_words():
+    seeds = np.array([0, 1, 7, 42, 12345, 2**32 - 1], dtype=np.uint64)
+    words = np.stack([np.random.RandomState(int(s)).randint(0, 2**32, size=1400, dtype=np.uint32)
+                      for s in seeds])
+    # derived draws used by the env (Appendix A): rand / uniform / choice / permutation
+    rs = np.random.RandomState(3)
+    rand = rs.rand(50)
+    rs = np.random.RandomState(3)
+    uni = np.array([rs.uniform(0, 20) for _ in range(25)])
+    perms = []
+    for m in (1, 2, 3, 4, 5, 16, 64, 100, 256):
+        rs = np.random.RandomState(m)
+        perms.append(np.pad(rs.permutation(m), (0, 256 - m), constant_values=-1))
+    np.savez_compressed(os.path.join(OUT, "mt19937_words.npz"), seeds=seeds, words=words,
+                        rand_seed3=rand, uniform0_20_seed3=uni,
+                        perm_sizes=np.array([1, 2, 3, 4, 5, 16, 64, 100, 256]),
+                        perms=np.stack(perms))
+
+
+def gen_mock_reset():
+    from envs.mock_constellation_env import MockConstellationEnv
+    cases = [(4, 4, 5, 3, s) for s in (0, 1, 2, 3, 4)] + \
+            [(16, 16, 20, 3, s) for s in (0, 1, 7)] + \
+            [(8, 12, 6, 4, 5), (3, 10, 4, 6, 11), (64, 64, 20, 3, 0)]
+    out = {}
+    for idx, (n, m, T, L, s) in enumerate(cases):
+        np.random.seed(s)
+        env = MockConstellationEnv(n, m, T, L, 0.5)
+        init_tab = env.sat_prox_mat.copy()
+        env.reset()
+        st = np.random.get_state()
+        out[f"c{idx}_shape"] = np.array([n, m, T, L, s])
+        out[f"c{idx}_init_table"] = init_tab
+        out[f"c{idx}_table"] = env.sat_prox_mat
+        out[f"c{idx}_prev_assigns"] = np.asarray(env.prev_assigns, dtype=np.int64)
+        out[f"c{idx}_obs"] = np.array(env._obs)
+        out[f"c{idx}_beta"] = np.asarray(env.beta)
+        out[f"c{idx}_mt_key_after"] = st[1]
+        out[f"c{idx}_mt_pos_after"] = np.array(st[2])
+    out["n_cases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(OUT, "mock_reset.npz"), **out)
+
+
+def gen_mock_step():
+    """Injected tables + fixed action sequences through reset/step."""
+    from envs.mock_constellation_env import MockConstellationEnv, generate_benefits_over_time
+    rng = np.random.RandomState(1234)
+    out = {}
+    cases = []
+    # (n, m, T, L, lambda, kind)
+    specs = [(4, 4, 5, 3, 0.5, "random"), (4, 4, 5, 3, 0.5, "collide"),
+             (16, 16, 20, 3, 0.5, "random"), (16, 16, 20, 3, 0.5, "collide"),
+             (8, 12, 7, 2, 0.25, "random"), (7, 10, 6, 3, 0.5, "collide"),
+             (16, 16, 8, 3, 0.5, "bids"), (6, 6, 5, 2, 0.5, "bids_int"),
+             (16, 16, 10, 3, 1.5, "dense"), (5, 9, 4, 5, 0.5, "random")]
+    for idx, (n, m, T, L, lam, kind) in enumerate(specs):
+        np.random.seed(100 + idx)
+        if kind == "dense":
+            table = rng.uniform(0.0, 1.0, size=(n, m, T)) + 1e-3
+        else:
+            table = generate_benefits_over_time(n, m, T, 3, 6)
+        # a few exact zeros and tiny values around the 1e-12 mask threshold
+        table[0, 0, :] = 0.0
+        if n > 1 and m > 1:
+            table[1, 1, :] = 1e-13
+            table[0, 1, :] = 2e-12
+        bids = kind.startswith("bids")
+        env = MockConstellationEnv(n, m, T, L, lam, bids_as_actions=bids, sat_prox_mat=table.copy())
+        env.reset()
+        prev0 = np.asarray(env.prev_assigns, dtype=np.int64)
+        obs0 = np.array(env._obs)
+        beta0 = np.asarray(env.beta).copy()
+        acts, rews, obs, betas, dones, prevs = [], [], [], [], [], []
+        for t in range(T):
+            if kind == "collide":
+                a = np.full(n, t % m, dtype=np.int64) if t % 2 == 0 else rng.randint(0, min(2, m), size=n)
+            elif kind == "bids":
+                a = rng.uniform(0, 1, size=(n, m)).astype(np.float32)
+            elif kind == "bids_int":
+                a = rng.randint(0, 3, size=(n, m)).astype(np.float32)
+            else:
+                a = rng.randint(0, m, size=n)
+            r, d, info = env.step(a.copy() if bids else list(a))
+            acts.append(np.asarray(a))
+            rews.append(np.asarray(r, dtype=np.float64))
+            obs.append(np.array(env._obs))
+            betas.append(np.asarray(env.beta).copy())
+            dones.append(bool(d))
+            prevs.append(np.asarray(env.prev_assigns, dtype=np.int64))
+        out[f"c{idx}_spec"] = np.array([n, m, T, L])
+        out[f"c{idx}_lambda"] = np.array(lam)
+        out[f"c{idx}_kind"] = np.array(kind)
+        out[f"c{idx}_table"] = table
+        out[f"c{idx}_prev0"] = prev0
+        out[f"c{idx}_obs0"] = obs0
+        out[f"c{idx}_beta0"] = beta0
+        out[f"c{idx}_actions"] = np.stack(acts)
+        out[f"c{idx}_rewards"] = np.stack(rews)
+        out[f"c{idx}_obs"] = np.stack(obs)
+        out[f"c{idx}_beta"] = np.stack(betas)
+        out[f"c{idx}_done"] = np.array(dones)
+        out[f"c{idx}_prev"] = np.stack(prevs)
+        cases.append(idx)
+    # beta_hat on a time-batched state (HAA call shape) with a custom T_trans
+    np.random.seed(9)
+    n, m = 6, 7
+    T_trans = (rng.uniform(size=(m, m)) > 0.5).astype(np.float64)
+    env = MockConstellationEnv(n, m, 4, 2, 0.7, sat_prox_mat=np.ones((n, m, 4)), T_trans=T_trans)
+    beta = rng.uniform(-0.2, 1.0, size=(3, n, m))
+    beta[beta < 0] = 0.0
+    prev = rng.randint(0, m, size=(3, n))
+    out["bh_T_trans"] = T_trans
+    out["bh_beta"] = beta
+    out["bh_prev"] = prev
+    out["bh_lambda"] = np.array(0.7)
+    out["bh_out"] = env.beta_hat(beta, prev)
+    out["bh_out2d"] = env.beta_hat(beta[0], prev[0])
+    out["n_cases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(OUT, "mock_step.npz"), **out)
+
+
+def gen_lsa():
+    import scipy.optimize as so
+    rng = np.random.RandomState(77)
+    out = {}
+    k = 0
+    shapes = [(1, 1), (1, 5), (5, 1), (2, 3), (3, 2), (4, 4), (5, 8), (8, 5), (16, 16),
+              (7, 7), (10, 13), (13, 10), (64, 64), (33, 64), (64, 40), (100, 100), (3, 0)]
+    for (nr, nc) in shapes:
+        for kind in ("uniform", "int3", "round1", "const", "neg"):
+            for maximize in (False, True):
+                if kind == "uniform":
+                    C = rng.uniform(-1, 1, size=(nr, nc))
+                elif kind == "int3":
+                    C = rng.randint(0, 3, size=(nr, nc)).astype(np.float64)
+                elif kind == "round1":
+                    C = np.round(rng.uniform(0, 1, size=(nr, nc)), 1)
+                elif kind == "const":
+                    C = np.full((nr, nc), 2.5)
+                else:
+                    C = -np.exp(rng.normal(size=(nr, nc)) * 3)
+                r, c = so.linear_sum_assignment(C, maximize=maximize)
+                out[f"k{k}_C"] = C
+                out[f"k{k}_max"] = np.array(maximize)
+                out[f"k{k}_row"] = r.astype(np.int64)
+                out[f"k{k}_col"] = c.astype(np.int64)
+                k += 1
+    # float32 Q-value-like matrices (the SAP selector casts f32 -> f64)
+    for _ in range(20):
+        C = rng.normal(size=(16, 16)).astype(np.float32).astype(np.float64)
+        r, c = so.linear_sum_assignment(C, maximize=True)
+        out[f"k{k}_C"], out[f"k{k}_max"] = C, np.array(True)
+        out[f"k{k}_row"], out[f"k{k}_col"] = r.astype(np.int64), c.astype(np.int64)
+        k += 1
+    # error cases: (C, maximize, expected message fragment)
+    errs = []
+    bad = np.ones((3, 3)); bad[1, 1] = np.nan
+    errs.append((bad, False))
+    bad2 = np.ones((3, 3)); bad2[0, 2] = -np.inf
+    errs.append((bad2, False))
+    bad3 = np.ones((3, 3)); bad3[0, 2] = np.inf
+    errs.append((bad3, True))  # +inf under maximize becomes -inf -> invalid
+    inf = np.full((3, 3), np.inf); inf[0, 0] = 1.0; inf[1, 0] = 1.0
+    errs.append((inf, False))  # infeasible
+    for i, (C, mx) in enumerate(errs):
+        try:
+            so.linear_sum_assignment(C, maximize=mx)
+            msg = "ok"
+        except ValueError as e:
+            msg = str(e)
+        out[f"e{i}_C"], out[f"e{i}_max"], out[f"e{i}_msg"] = C, np.array(mx), np.array(msg)
+    out["n_cases"], out["n_err"] = np.array(k), np.array(len(errs))
+    np.savez_compressed(os.path.join(OUT, "lsa.npz"), **out)
+
+
+class _Logger:
+    def __init__(self):
+        self.stats = []
+
+    def log_stat(self, k, v, t):
+        self.stats.append((k, float(v), int(t)))
+
+
+def _args(**kw):
+    base = dict(batch_size_run=1, env="mock_constellation_env",
+                env_args=dict(n=4, m=4, T=5, L=3, lambda_=0.5, bids_as_actions=False, seed=0),
+                use_mps_action_selection=False, mac="basic_mac", test_nepisode=1,
+                runner_log_interval=10**9, render=False, agent="rnn", hidden_dim=64, use_rnn=True,
+                obs_last_action=False, obs_agent_id=False, agent_output_type="q",
+                action_selector="epsilon_greedy", epsilon_start=0.0, epsilon_finish=0.0,
+                epsilon_anneal_time=1000, evaluation_epsilon=0.0, device="cpu",
+                jumpstart_action_selector="haa_selector", jumpstart_epsilon_start=1.0,
+                jumpstart_epsilon_finish=1.0, jumpstart_epsilon_anneal_time=1000,
+                jumpstart_evaluation_epsilon=1.0)
+    base.update(kw)
+    return SimpleNamespace(**base)
+
+
+def gen_runner_dumps():
+    import torch as th
+    th.set_num_threads(1)
+    from runners.episode_runner import EpisodeRunner
+    from runners.parallel_runner import ParallelRunner
+    from controllers import REGISTRY as mac_REGISTRY
+
+    out = {}
+    runs = [  # (tag, runner, n, m, T, B, selector, mac, use_rnn)
+        ("ep_eg_4", "episode", 4, 4, 5, 1, "epsilon_greedy", "basic_mac", True),
+        ("ep_sap_8", "episode", 8, 8, 6, 1, "sap", "basic_mac", False),
+        ("par_eg_6", "parallel", 6, 6, 5, 3, "epsilon_greedy", "basic_mac", True),
+        ("par_sap_8", "parallel", 8, 8, 6, 3, "sap", "basic_mac", True),
+        ("ep_haa_8", "episode", 8, 8, 6, 1, "sap", "jumpstart_mac", False),
+    ]
+    for ri, (tag, rname, n, m, T, B, sel, macname, use_rnn) in enumerate(runs):
+        seed = 10 + ri
+        np.random.seed(seed)
+        th.manual_seed(seed)
+        args = _args(batch_size_run=B, mac=macname, action_selector=sel, use_rnn=use_rnn,
+                     env_args=dict(n=n, m=m, T=T, L=3, lambda_=0.5, bids_as_actions=False, seed=seed))
+        logger = _Logger()
+        runner = (EpisodeRunner if rname == "episode" else ParallelRunner)(args, logger)
+        env = runner.get_env()
+        args.n, args.m, args.T = env.n, env.m, env.T
+        groups = {"agents": n}
+        mac = mac_REGISTRY[macname](env.scheme, groups, args)
+        # deterministic, non-trivial weights shared by the training and selector copies
+        g = th.Generator().manual_seed(1000 + ri)
+        with th.no_grad():
+            for p in mac.agent.parameters():
+                p.copy_(th.randn(p.shape, generator=g) * 0.3)
+        mac.update_action_selector_agent()
+        runner.setup(scheme=env.scheme, groups=groups, preprocess=env.preprocess, mac=mac)
+        batch = runner.run(test_mode=False)
+        for k, v in batch.data.transition_data.items():
+            out[f"{tag}__{k}"] = v.numpy()
+        sd = mac.agent.state_dict()
+        for k, v in sd.items():
+            out[f"{tag}__w__{k}"] = v.numpy()
+        out[f"{tag}__returns"] = np.asarray(runner.train_returns, dtype=np.float64)
+        out[f"{tag}__t_env"] = np.array(runner.t_env)
+        out[f"{tag}__cfg"] = np.array([n, m, T, B, seed, int(use_rnn)])
+        out[f"{tag}__names"] = np.array([rname, sel, macname])
+        if rname == "parallel":
+            runner.close_env()
+    np.savez_compressed(os.path.join(OUT, "runner_dumps.npz"), **out)
+
+
+if __name__ == "__main__":
+    _install_stubs()
+    gen_mt_words()
+    gen_mock_reset()
+    gen_mock_step()
+    gen_lsa()
+    gen_runner_dumps()
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))
