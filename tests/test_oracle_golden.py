@@ -1,0 +1,97 @@
+"""Pins the CPU oracle (oracle/) against the golden vectors captured from the reference
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+
+def test_mt19937_words(golden, oracle):
+    g = golden("mt19937_words")
+    for s, words in zip(g["seeds"], g["words"]):
+        mt = oracle.MT(int(s))
+        np.testing.assert_array_equal(mt.next32(len(words)), words)
+
+
+def test_mt19937_derived(golden, oracle):
+    g = golden("mt19937_words")
+    mt = oracle.MT(3)
+    np.testing.assert_array_equal(np.array([mt.rand() for _ in range(50)]), g["rand_seed3"])
+    mt = oracle.MT(3)
+    np.testing.assert_array_equal(np.array([mt.uniform(0, 20) for _ in range(25)]),
+                                  g["uniform0_20_seed3"])
+    for m, perm in zip(g["perm_sizes"], g["perms"]):
+        np.testing.assert_array_equal(oracle.MT(int(m)).permutation(int(m)), perm[:m])
+
+
+def _table_close(a, b):
+    """Benefit tables are the same float64 expression of the same MT19937 draws; the
+    only inexact op is exp.  numpy's AVX-512 float64 exp is not correctly rounded (its
+    error grows with |argument|: up to ~1e-13 relative for arguments near -150), while
+    the oracle uses libm's, so float64 values agree to rtol 1e-12; the zero pattern and
+    the float32 values the EpisodeBatch stores are identical."""
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(a == 0, b == 0)
+    np.testing.assert_array_equal(a.astype(np.float32), b.astype(np.float32))
+
+
+def test_mock_construct_reset(golden, oracle):
+    g = golden("mock_reset")
+    for c in range(int(g["n_cases"])):
+        n, m, T, L, s = [int(x) for x in g[f"c{c}_shape"]]
+        mt = oracle.MT(s)
+        env = oracle.OracleMockEnv(n, m, T, L, 0.5, mt=mt)
+        _table_close(env.sat_prox_mat, g[f"c{c}_init_table"])
+        env.reset()
+        _table_close(env.sat_prox_mat, g[f"c{c}_table"])
+        np.testing.assert_array_equal(env.prev_assigns, g[f"c{c}_prev_assigns"])
+        _table_close(env._obs, g[f"c{c}_obs"])
+        _table_close(env.beta, g[f"c{c}_beta"])
+        key, pos = mt.state()
+        assert pos == int(g[f"c{c}_mt_pos_after"])
+        np.testing.assert_array_equal(key, g[f"c{c}_mt_key_after"])
+
+
+def test_mock_steps(golden, oracle):
+    g = golden("mock_step")
+    for c in range(int(g["n_cases"])):
+        n, m, T, L = [int(x) for x in g[f"c{c}_spec"]]
+        lam = float(g[f"c{c}_lambda"])
+        kind = str(g[f"c{c}_kind"])
+        bids = kind.startswith("bids")
+        mt = oracle.MT(100 + c)
+        if kind != "dense":  # the fixture drew its table from the global stream first
+            tab = oracle.generate(mt, n, m, T, 3.0, 6.0)
+            keep = np.ones_like(tab, dtype=bool)
+            keep[0, 0], keep[0, 1], keep[1, 1] = False, False, False
+            np.testing.assert_allclose(tab[keep], g[f"c{c}_table"][keep], rtol=1e-12, atol=0)
+        env = oracle.OracleMockEnv(n, m, T, L, lam, bids_as_actions=bids,
+                                   sat_prox_mat=g[f"c{c}_table"], mt=mt)
+        env.reset()
+        np.testing.assert_array_equal(env.prev_assigns, g[f"c{c}_prev0"])
+        np.testing.assert_array_equal(env._obs, g[f"c{c}_obs0"])
+        for t in range(T):
+            r, d, info = env.step(g[f"c{c}_actions"][t])
+            np.testing.assert_array_equal(np.array(r), g[f"c{c}_rewards"][t], err_msg=f"{c},{t}")
+            np.testing.assert_array_equal(env._obs, g[f"c{c}_obs"][t])
+            np.testing.assert_array_equal(env.beta, g[f"c{c}_beta"][t])
+            np.testing.assert_array_equal(env.prev_assigns, g[f"c{c}_prev"][t])
+            assert d == bool(g[f"c{c}_done"][t])
+
+
+def test_beta_hat(golden, oracle):
+    g = golden("mock_step")
+    out = oracle.beta_hat(g["bh_beta"], g["bh_prev"], float(g["bh_lambda"]), g["bh_T_trans"])
+    np.testing.assert_array_equal(out, g["bh_out"])
+    out2 = oracle.beta_hat(g["bh_beta"][0], g["bh_prev"][0], float(g["bh_lambda"]), g["bh_T_trans"])
+    np.testing.assert_array_equal(out2, g["bh_out2d"])
+
+
+def test_lsa(golden, oracle):
+    g = golden("lsa")
+    for k in range(int(g["n_cases"])):
+        r, c = oracle.lsa(g[f"k{k}_C"], bool(g[f"k{k}_max"]))
+        np.testing.assert_array_equal(r, g[f"k{k}_row"], err_msg=str(k))
+        np.testing.assert_array_equal(c, g[f"k{k}_col"], err_msg=str(k))
+    for e in range(int(g["n_err"])):
+        msg = str(g[f"e{e}_msg"])
+        with pytest.raises(ValueError, match=msg):
+            oracle.lsa(g[f"e{e}_C"], bool(g[f"e{e}_max"]))
