@@ -1,0 +1,183 @@
+/*
+ * asg.h -- C-ABI of the MI355X-native batched sequential-assignment environment.
+ *
+ * One handle = E independent MockConstellationEnv episodes resident on one GPU,
+ * advanced in lockstep by HIP kernels that read actions from, and write observations,
+ * rewards, masks and bookkeeping into, an EpisodeBatch whose tensors the CALLER owns
+ * (PyTorch tensors; zero copies).  Every entry point is stream-ordered and asynchronous
+ * to the host unless stated otherwise, returns 0 on success or a negative ASG_E_* code,
+ * and never throws across the boundary; asg_last_error() explains the last failure.
+ *
+ * Reference interfaces replaced (all paths under /root/reference/src):
+ *   asg_create / asg_destroy   MockConstellationEnv.__init__ / close
+ *                              (envs/mock_constellation_env.py:17-65, :177-178), one
+ *                              instance per env of ParallelRunner.__init__
+ *                              (runners/parallel_runner.py:14-31)
+ *   asg_reset                  MockConstellationEnv.reset + get_pretransition_data
+ *                              (mock_constellation_env.py:94-114, :164-175) and the
+ *                              runner's batch.update(pre_transition_data, ts=0)
+ *                              (episode_runner.py:55-74, parallel_runner.py:94-111)
+ *   asg_step                   MockConstellationEnv.step (mock_constellation_env.py:116-162)
+ *                              + the runner's post-/pre-transition batch.update calls and
+ *                              OneHot preprocess (episode_runner.py:80-95,
+ *                              parallel_runner.py:141-200, components/episode_buffer.py:89-129,
+ *                              components/transforms.py:12-22)
+ *   asg_random_actions         a uniform random policy (BASELINE config 2)
+ *   asg_set_benefits           MockConstellationEnv(sat_prox_mat=...) injection
+ *                              (mock_constellation_env.py:22, :32-37)
+ *   asg_beta_hat               MockConstellationEnv.beta_hat (mock_constellation_env.py:228-274)
+ *   asg_lsa_batched            scipy.optimize.linear_sum_assignment per env, as called by
+ *                              mock_constellation_env.py:122, action_selectors/sap_selectors.py:32,90,
+ *                              action_selectors/non_rl_selectors.py:47
+ *   asg_haa_select             HAASelector.select_action (action_selectors/non_rl_selectors.py:19-50)
+ *   asg_get_returns            the runners' episode_return accumulation
+ *                              (episode_runner.py:84, parallel_runner.py:173-176)
+ */
+#ifndef ASG_H
+#define ASG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ASG_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define ASG_OK 0
+#define ASG_E_INVALID_ARG (-1)   /* maps to ValueError in the Python shim */
+#define ASG_E_HIP (-2)           /* HIP runtime failure -> RuntimeError */
+#define ASG_E_STATE (-3)         /* call out of order (step before reset, step past T) */
+#define ASG_E_LSA_INVALID (-4)   /* "matrix contains invalid numeric entries" */
+#define ASG_E_LSA_INFEASIBLE (-5)/* "cost matrix is infeasible" */
+#define ASG_E_ACTION_RANGE (-6)  /* an action outside [0, m) was stepped */
+
+/* ---- element types of batch fields ------------------------------------------------- */
+enum asg_dtype {
+    ASG_F32 = 0,
+    ASG_F64 = 1,
+    ASG_I64 = 2,
+    ASG_I32 = 3,
+    ASG_BOOL = 4, /* 1 byte, torch.bool */
+};
+
+/* A strided view of one EpisodeBatch field.  ptr addresses element [0, 0, 0, 0] of the
+ * [B, T+1, d2, d3] tensor; strides are in ELEMENTS (torch .stride()), unused trailing
+ * dims have size 1.  ptr == NULL means "field absent, skip the write". */
+typedef struct {
+    void *ptr;
+    int32_t dtype;
+    int32_t pad_;
+    int64_t stride[4];
+} asg_field;
+
+/* The transition_data of an EpisodeBatch (components/episode_buffer.py:30-77) for the
+ * envs of one handle.  Shapes per scheme (mock_constellation_env.py:73-86):
+ *   obs           f32  [B, T+1, n, m*(L+1)]
+ *   actions       i64  [B, T+1, n, 1]      (f32 [B, T+1, n, m] bids when bids_as_actions)
+ *   avail_actions bool [B, T+1, n, m]
+ *   rewards       f32  [B, T+1, n]
+ *   terminated    bool [B, T+1, 1]
+ *   prev_assigns  i64  [B, T+1, n]
+ *   beta          f32  [B, T+1, n, m]
+ *   actions_onehot i64 [B, T+1, n, m]     (OneHot keeps the input dtype, transforms.py:21-22)
+ *   filled        i64  [B, T+1, 1]                                                         */
+typedef struct {
+    asg_field obs, actions, avail_actions, rewards, terminated, prev_assigns, beta,
+        actions_onehot, filled;
+} asg_batch_view;
+
+/* ---- configuration ------------------------------------------------------------------ */
+enum asg_rng_mode {
+    ASG_RNG_PHILOX = 0,   /* native: counter-based Philox4x32-10 keyed (seed, global env, episode) */
+    ASG_RNG_MT19937 = 1,  /* compat: numpy legacy MT19937 stream per env, bit-exact draws */
+};
+
+enum asg_benefit_mode {
+    ASG_BENEFIT_BUMP = 0,     /* generate_benefits_over_time bumps (~25% active pairs) */
+    ASG_BENEFIT_DENSE = 1,    /* every (i, j) pair active (BASELINE config 5) */
+    ASG_BENEFIT_INJECTED = 2, /* constant table from asg_set_benefits (sat_prox_mat=) */
+};
+
+/* reference quirks (SURVEY.md §8(a) "quirks"); 0 = native semantics */
+#define ASG_QUIRK_PREV_ASSIGNS_ZERO 0x1u   /* batch prev_assigns never written (mock :170-174) */
+#define ASG_QUIRK_PARALLEL_TERMINATED 0x2u /* ParallelRunner terminated flag bug (parallel_runner.py:181-187) */
+#define ASG_QUIRK_REPLICATE_STREAM 0x4u    /* every env shares env 0's MT stream (forked workers) */
+
+typedef struct {
+    int64_t num_envs;       /* E: envs owned by this handle (one GPU) */
+    int32_t n, m, T, L;     /* agents, tasks, horizon, lookahead */
+    double lambda_;         /* handover penalty */
+    int32_t bids_as_actions;
+    int32_t rng_mode;       /* asg_rng_mode */
+    int32_t benefit_mode;   /* asg_benefit_mode */
+    uint32_t quirks;        /* ASG_QUIRK_* */
+    uint64_t seed;
+    int64_t env_index_base; /* global index of env 0 (rank * E when sharded) */
+    const double *T_trans;  /* host [m][m] transition-penalty matrix or NULL = 1 - I (mock :40) */
+} asg_config;
+
+typedef struct asg_handle asg_handle;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+int asg_abi_version(void);
+const char *asg_last_error(const asg_handle *h); /* h may be NULL: last global error */
+int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle **out);
+int asg_destroy(asg_handle *h);
+int asg_set_stream(asg_handle *h, void *hip_stream);
+
+/* ---- the hot path --------------------------------------------------------------------- */
+/* New episode: draw benefits (unless injected) and initial prev_assigns, zero returns,
+ * write pre-transition row `ts` (obs, beta, avail_actions, prev_assigns, filled). */
+int asg_reset(asg_handle *h, const asg_batch_view *b, int ts);
+/* One transition of every env: read actions at row ts; write rewards/terminated/
+ * actions_onehot at ts and obs/beta/avail_actions/prev_assigns/filled at ts+1;
+ * accumulate per-env float64 returns.  Actions outside [0, m) set a sticky device
+ * error reported by asg_sync_status. */
+int asg_step(asg_handle *h, const asg_batch_view *b, int ts);
+/* Uniform random actions in [0, m) at row ts (Philox keyed (seed, env, episode, t)). */
+int asg_random_actions(asg_handle *h, const asg_batch_view *b, int ts);
+/* Blocks until the handle's stream drains; returns the first sticky device error. */
+int asg_sync_status(asg_handle *h);
+
+/* ---- state in / out ------------------------------------------------------------------- */
+/* Constant benefit table, reference layout [E][n][m][T] float64 (host or device ptr). */
+int asg_set_benefits(asg_handle *h, const double *table, int64_t count, int on_device);
+/* The current episode's benefit table [E][n][m][T] float64 into a device buffer
+ * (materialises Philox/bump draws; a debugging and parity aid). */
+int asg_export_benefits(asg_handle *h, double *out_dev);
+/* Current internal prev_assigns [E][n] (int64, device buffer). */
+int asg_export_prev_assigns(asg_handle *h, int64_t *out_dev);
+/* Per-env float64 returns accumulated since the last reset [E] (device buffer). */
+int asg_get_returns(asg_handle *h, double *out_dev);
+/* Current step counter k of the handle (host value; 0 after reset). */
+int asg_get_step(const asg_handle *h, int *k_out);
+/* Advance every env's MT19937 stream by `words` 32-bit draws (compat mode): models
+ * other consumers of numpy's global stream between resets (jumpstart_controller.py:33). */
+int asg_advance_stream(asg_handle *h, int64_t words);
+
+/* ---- batched kernels for the action selectors ----------------------------------------- */
+/* beta_hat for a batch of states: beta [B][n][m] (f32 or f64, strides in elements),
+ * prev [B][n] int64 -> out [B][n][m] float64.  T_trans: device [m][m] f64 or NULL. */
+int asg_beta_hat(const void *beta, int beta_dtype, const int64_t beta_strides[3],
+                 const int64_t *prev, const int64_t prev_strides[2], int64_t B, int n, int m,
+                 const double *T_trans_dev, double lambda_, double *out, void *hip_stream);
+/* scipy-exact linear_sum_assignment on B cost matrices C[b] = [nr][nc] (f32 or f64,
+ * element strides {batch, row, col}).  row_out/col_out: [B][min(nr, nc)] int64 device
+ * buffers; status_out [B] int32 device buffer (0, ASG_E_LSA_INVALID, ASG_E_LSA_INFEASIBLE).
+ * Either of row_out / status_out may be NULL. */
+int asg_lsa_batched(const void *C, int dtype, const int64_t strides[3], int64_t B, int nr,
+                    int nc, int maximize, int64_t *row_out, int64_t *col_out,
+                    int32_t *status_out, void *hip_stream);
+/* HAASelector: per env LSA(maximize) of beta_hat(beta[b], prev[b]) -> col_out [B][n]
+ * float32 (the selector returns float tensors holding task ids, non_rl_selectors.py:30). */
+int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64_t *prev,
+                   const int64_t prev_strides[2], int64_t B, int n, int m,
+                   const double *T_trans_dev, double lambda_, float *col_out,
+                   int32_t *status_out, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ASG_H */

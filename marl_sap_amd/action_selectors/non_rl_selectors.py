@@ -1,0 +1,56 @@
+"""Non-RL selectors (reference: action_selectors/non_rl_selectors.py:10-50).
+
+HAASelector: per env, LSA(maximize) of beta_hat(beta, prev_assigns) taken from the
+batch's part_of_state fields -- fused into one HIP kernel over all envs
+(asg_haa_select: beta_hat formed on the fly, scipy-exact LSA per wave)."""
+import ctypes
+
+import torch
+
+from .. import _lib
+from .lsa import DeferredStatus
+
+REGISTRY = {}
+
+
+class HAASelector:
+    def __init__(self, args):
+        self.args = args
+        self.envs = None
+        self.status = DeferredStatus()
+
+    def _env_params(self):
+        env = self.envs[0] if self.envs is not None else None
+        lam = env.lambda_ if env is not None else self.args.env_args["lambda_"]
+        tt = getattr(env, "T_trans", None)
+        m = self.args.m
+        if tt is not None and not (torch.is_tensor(tt) and tt.numel() == 0):
+            tt = torch.as_tensor(tt, dtype=torch.float64)
+            eye = torch.ones((m, m), dtype=torch.float64) - torch.eye(m, dtype=torch.float64)
+            if tt.shape == (m, m) and torch.equal(tt, eye):
+                tt = None  # the default 1 - I is computed in-kernel
+        return float(lam), tt
+
+    def select_action(self, batch):
+        beta = batch["beta"][:, 0]
+        prev = batch["prev_assigns"][:, 0]
+        if beta.dim() == 4:  # L-deep beta of the real env: use the current step only
+            beta = beta[..., 0]
+        B, n, m = beta.shape
+        if beta.dtype != torch.float32:
+            beta = beta.float()
+        lam, tt = self._env_params()
+        tt_dev = None if tt is None else tt.to(beta.device).contiguous()
+        out = torch.empty((B, n), dtype=torch.float32, device=beta.device)
+        status = torch.empty((B,), dtype=torch.int32, device=beta.device)
+        with torch.cuda.device(beta.device):
+            _lib.check(_lib.lib().asg_haa_select(
+                ctypes.c_void_p(beta.data_ptr()), _lib.i64arr(beta.stride()), ctypes.c_void_p(prev.data_ptr()),
+                _lib.i64arr(prev.stride()), B, n, m,
+                ctypes.c_void_p(tt_dev.data_ptr()) if tt_dev is not None else None, lam,
+                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(beta.device)))
+        self.status.add(status)
+        return out
+
+
+REGISTRY["haa_selector"] = HAASelector

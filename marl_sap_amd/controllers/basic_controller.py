@@ -1,0 +1,97 @@
+"""Shared-parameter multi-agent controller (reference: controllers/basic_controller.py:7-101).
+
+The reference keeps a CPU copy (`selector_agent`) for action selection.  Here the agent
+lives on the GPU next to the batched env, so by default selection uses the agent itself
+(`selector_agent` is the same module); with args.separate_selector_agent=True a distinct
+copy is kept and `update_action_selector_agent` syncs it, as in the reference.
+"""
+import torch
+
+from ..action_selectors import REGISTRY as action_REGISTRY
+from ..modules.agents import REGISTRY as agent_REGISTRY
+
+
+class BasicMAC:
+    def __init__(self, scheme, groups, args):
+        self.n = args.n
+        self.args = args
+        input_shape = self._get_input_shape(scheme)
+        self._build_agents(input_shape)
+        self.agent_output_type = args.agent_output_type
+        self.action_selector = action_REGISTRY[args.action_selector](args)
+        self.hidden_states = None
+
+    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False):
+        avail_actions = ep_batch["avail_actions"][:, t_ep]
+        agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode, action_selection_mode=True)
+        return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env,
+                                                  test_mode=test_mode, beta=ep_batch["beta"][bs, t_ep])
+
+    def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
+        agent_inputs = self._build_inputs(ep_batch, t)
+        net = self.selector_agent if action_selection_mode else self.agent
+        agent_outs, self.hidden_states = net(agent_inputs, self.hidden_states)
+        if self.agent_output_type == "pi_logits":
+            agent_outs = torch.nn.functional.softmax(agent_outs, dim=-1)
+        return agent_outs.view(ep_batch.batch_size, self.n, -1)
+
+    def init_hidden(self, batch_size):
+        self.hidden_states = self.agent.init_hidden().unsqueeze(0).expand(batch_size, self.n, -1)
+
+    def parameters(self):
+        return self.agent.parameters()
+
+    def load_state(self, other_mac):
+        self.agent.load_state_dict(other_mac.agent.state_dict())
+
+    def cuda(self):
+        self.agent.cuda()
+        if self.selector_agent is not self.agent:
+            self.selector_agent.cuda()
+
+    def to(self, device):
+        self.agent.to(device)
+        if self.selector_agent is not self.agent:
+            self.selector_agent.to(device)
+        return self
+
+    def save_models(self, path):
+        torch.save(self.agent.state_dict(), "{}/agent.th".format(path))
+
+    def load_models(self, path):
+        self.agent.load_state_dict(torch.load("{}/agent.th".format(path), map_location=lambda s, loc: s,
+                                              weights_only=True))
+        self.update_action_selector_agent()
+
+    def _build_agents(self, input_shape):
+        self.agent = agent_REGISTRY[self.args.agent](input_shape, self.args)
+        if getattr(self.args, "separate_selector_agent", False):
+            self.selector_agent = agent_REGISTRY[self.args.agent](input_shape, self.args)
+        else:
+            self.selector_agent = self.agent
+
+    def update_action_selector_agent(self):
+        if self.selector_agent is not self.agent:
+            self.selector_agent.load_state_dict(self.agent.state_dict())
+
+    def _build_inputs(self, batch, t):
+        bs = batch.batch_size
+        inputs = [batch["obs"][:, t].float()]
+        if self.args.obs_last_action:
+            if t == 0:
+                inputs.append(torch.zeros_like(batch["actions_onehot"][:, t]))
+            else:
+                inputs.append(batch["actions_onehot"][:, t - 1])
+        if self.args.obs_agent_id:
+            inputs.append(torch.eye(self.n, device=batch.device).unsqueeze(0).expand(bs, -1, -1))
+        if len(inputs) == 1:
+            return inputs[0].reshape(bs * self.n, -1)
+        return torch.cat([x.reshape(bs * self.n, -1).to(torch.float32) for x in inputs], dim=1)
+
+    def _get_input_shape(self, scheme):
+        input_shape = scheme["obs"]["vshape"]
+        if self.args.obs_last_action:
+            input_shape += scheme["actions_onehot"]["vshape"][0]
+        if self.args.obs_agent_id:
+            input_shape += self.n
+        return input_shape

@@ -1,0 +1,338 @@
+// asg_abi.hip -- the extern "C" boundary (include/asg.h): handle lifecycle, argument
+// validation, error strings, and dispatch to the kernels.  No exception crosses it.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/asg.h"
+#include "asg_internal.h"
+
+using asg::EnvState;
+
+struct asg_handle {
+    EnvState st{};
+    hipStream_t stream = nullptr;
+    int device = 0;
+    int k = 0;                 // steps taken in the current episode
+    bool has_reset = false;
+    bool constructed = false;  // MT19937: first reset also replays __init__'s draw
+    bool table_ready = false;  // injected table uploaded
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(asg_handle *h, int code, const std::string &msg) {
+    g_err = msg;
+    if (h) h->err = msg;
+    return code;
+}
+
+int hip_fail(asg_handle *h, hipError_t e, const char *what) {
+    return fail(h, ASG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// keeps the caller's current device (PyTorch tracks its own) around every entry point
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+bool field_ok(const asg_field &f, int want_dtype) { return f.ptr == nullptr || f.dtype == want_dtype; }
+
+int check_view(asg_handle *h, const asg_batch_view *b, int ts, bool step) {
+    if (!b) return fail(h, ASG_E_INVALID_ARG, "batch view is NULL");
+    const EnvState &st = h->st;
+    if (ts < 0 || (step && ts + 1 > st.T + 64 * 1024)) return fail(h, ASG_E_INVALID_ARG, "bad ts");
+    if (!b->obs.ptr) return fail(h, ASG_E_INVALID_ARG, "obs field is required");
+    if (!field_ok(b->obs, ASG_F32) || !field_ok(b->beta, ASG_F32) || !field_ok(b->rewards, ASG_F32) ||
+        !field_ok(b->avail_actions, ASG_BOOL) || !field_ok(b->terminated, ASG_BOOL) ||
+        !field_ok(b->prev_assigns, ASG_I64) || !field_ok(b->actions_onehot, ASG_I64) ||
+        !field_ok(b->filled, ASG_I64))
+        return fail(h, ASG_E_INVALID_ARG, "batch field dtype does not match the env scheme");
+    if (step) {
+        if (!b->actions.ptr) return fail(h, ASG_E_INVALID_ARG, "actions field is required for step");
+        if (!field_ok(b->actions, st.bids ? ASG_F32 : ASG_I64))
+            return fail(h, ASG_E_INVALID_ARG,
+                        st.bids ? "bids_as_actions expects float32 actions" : "actions must be int64");
+    }
+    return ASG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int asg_abi_version(void) { return ASG_ABI_VERSION; }
+
+const char *asg_last_error(const asg_handle *h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle **out) {
+    if (!cfg || !out) return fail(nullptr, ASG_E_INVALID_ARG, "cfg and out must be non-NULL");
+    *out = nullptr;
+    if (cfg->num_envs <= 0 || cfg->n <= 0 || cfg->m <= 0 || cfg->T <= 0 || cfg->L < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "num_envs, n, m, T must be positive and L >= 0");
+    if (cfg->n > cfg->m)
+        return fail(nullptr, ASG_E_INVALID_ARG,
+                    "Cannot take a larger sample than population when 'replace=False' (reset draws "
+                    "choice(m, n, replace=False): needs n <= m)");
+    if (cfg->n > 4096 || cfg->m > 1024)
+        return fail(nullptr, ASG_E_INVALID_ARG, "n <= 4096 and m <= 1024 are supported");
+    if (cfg->rng_mode != ASG_RNG_PHILOX && cfg->rng_mode != ASG_RNG_MT19937)
+        return fail(nullptr, ASG_E_INVALID_ARG, "unknown rng_mode");
+    if (cfg->benefit_mode < ASG_BENEFIT_BUMP || cfg->benefit_mode > ASG_BENEFIT_INJECTED)
+        return fail(nullptr, ASG_E_INVALID_ARG, "unknown benefit_mode");
+    if (cfg->rng_mode == ASG_RNG_MT19937 && cfg->benefit_mode == ASG_BENEFIT_DENSE)
+        return fail(nullptr, ASG_E_INVALID_ARG, "dense benefits are a Philox-mode workload");
+    asg_handle *h = new (std::nothrow) asg_handle();
+    if (!h) return fail(nullptr, ASG_E_HIP, "out of host memory");
+    DeviceGuard g(device);
+    h->device = device;
+    h->stream = static_cast<hipStream_t>(hip_stream);
+    EnvState &st = h->st;
+    st.E = cfg->num_envs;
+    st.n = cfg->n;
+    st.m = cfg->m;
+    st.T = cfg->T;
+    st.L = cfg->L;
+    st.lambda_ = cfg->lambda_;
+    st.bids = cfg->bids_as_actions ? 1 : 0;
+    st.rng_mode = cfg->rng_mode;
+    st.benefit_mode = cfg->benefit_mode;
+    st.quirks = cfg->quirks;
+    st.seed = cfg->seed;
+    st.env_base = cfg->env_index_base;
+    st.episode = 0;
+    st.wmin_init = 5.0;
+    st.wmax_init = 8.0;
+    st.wmin = 3.0;
+    st.wmax = 6.0;
+    const size_t E = (size_t)st.E, n = st.n, m = st.m, T = st.T;
+    hipError_t e;
+    if ((e = hipMalloc(&st.prev, sizeof(int) * E * n)) != hipSuccess) goto oom;
+    if ((e = hipMalloc(&st.returns, sizeof(double) * E)) != hipSuccess) goto oom;
+    if ((e = hipMalloc(&st.err, sizeof(int))) != hipSuccess) goto oom;
+    if ((e = hipMemsetAsync(st.err, 0, sizeof(int), h->stream)) != hipSuccess) goto oom;
+    if ((e = hipMemsetAsync(st.returns, 0, sizeof(double) * E, h->stream)) != hipSuccess) goto oom;
+    if ((e = hipMemsetAsync(st.prev, 0, sizeof(int) * E * n, h->stream)) != hipSuccess) goto oom;
+    if (cfg->T_trans) {
+        double *tt = nullptr;
+        if ((e = hipMalloc(&tt, sizeof(double) * m * m)) != hipSuccess) goto oom;
+        if ((e = hipMemcpy(tt, cfg->T_trans, sizeof(double) * m * m, hipMemcpyHostToDevice)) != hipSuccess) goto oom;
+        st.T_trans = tt;
+    }
+    if (st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED) {
+        if ((e = hipMalloc(&st.table, sizeof(double) * E * T * n * m)) != hipSuccess) goto oom;
+        if ((e = hipMemsetAsync(st.table, 0, sizeof(double) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
+    }
+    if (st.rng_mode == ASG_RNG_MT19937) {
+        if ((e = hipMalloc(&st.mt, sizeof(uint32_t) * E * 625)) != hipSuccess) goto oom;
+        if ((e = asg::launch_mt_seed(st, h->stream)) != hipSuccess) goto oom;
+    }
+    *out = h;
+    return ASG_OK;
+oom:
+    {
+        const int rc = hip_fail(nullptr, e, "asg_create");
+        asg_destroy(h);
+        return rc;
+    }
+}
+
+int asg_destroy(asg_handle *h) {
+    if (!h) return ASG_OK;
+    DeviceGuard g(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    else (void)hipDeviceSynchronize();
+    EnvState &st = h->st;
+    (void)hipFree(st.prev);
+    (void)hipFree(st.returns);
+    (void)hipFree(st.err);
+    (void)hipFree(const_cast<double *>(st.T_trans));
+    (void)hipFree(st.table);
+    (void)hipFree(st.mt);
+    delete h;
+    return ASG_OK;
+}
+
+int asg_set_stream(asg_handle *h, void *hip_stream) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    h->stream = static_cast<hipStream_t>(hip_stream);
+    return ASG_OK;
+}
+
+int asg_reset(asg_handle *h, const asg_batch_view *b, int ts) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (int rc = check_view(h, b, ts, false)) return rc;
+    if (h->st.benefit_mode == ASG_BENEFIT_INJECTED && !h->table_ready)
+        return fail(h, ASG_E_STATE, "benefit_mode=injected needs asg_set_benefits before reset");
+    DeviceGuard g(h->device);
+    if (h->has_reset) h->st.episode += 1;  // Philox: a fresh key per episode (first = 0)
+    hipError_t e = asg::launch_reset(*b, h->st, ts, !h->constructed, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_reset");
+    h->constructed = true;
+    h->has_reset = true;
+    h->k = 0;
+    return ASG_OK;
+}
+
+int asg_step(asg_handle *h, const asg_batch_view *b, int ts) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (int rc = check_view(h, b, ts, true)) return rc;
+    if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
+    if (h->k >= h->st.T) return fail(h, ASG_E_STATE, "episode already terminated (k >= T); reset first");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_step(*b, h->st, ts, h->k, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_step");
+    h->k += 1;
+    return ASG_OK;
+}
+
+int asg_random_actions(asg_handle *h, const asg_batch_view *b, int ts) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (!b || !b->actions.ptr || b->actions.dtype != ASG_I64)
+        return fail(h, ASG_E_INVALID_ARG, "random actions need an int64 actions field");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_random_actions(*b, h->st, ts, h->k, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_random_actions");
+    return ASG_OK;
+}
+
+int asg_sync_status(asg_handle *h) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    DeviceGuard g(h->device);
+    int code = 0;
+    hipError_t e = hipMemcpyAsync(&code, h->st.err, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_sync_status");
+    if (code != 0) {
+        (void)hipMemsetAsync(h->st.err, 0, sizeof(int), h->stream);
+        if (code == ASG_E_ACTION_RANGE)
+            return fail(h, code, "an action outside [0, m) was passed to step (OneHot / task index out of range)");
+        if (code == ASG_E_LSA_INVALID) return fail(h, code, "matrix contains invalid numeric entries");
+        if (code == ASG_E_LSA_INFEASIBLE) return fail(h, code, "cost matrix is infeasible");
+        return fail(h, code, "device error " + std::to_string(code));
+    }
+    return ASG_OK;
+}
+
+int asg_set_benefits(asg_handle *h, const double *table, int64_t count, int on_device) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    EnvState &st = h->st;
+    const int64_t per = (int64_t)st.n * st.m * st.T;
+    if (!table || (count != per && count != per * st.E))
+        return fail(h, ASG_E_INVALID_ARG, "benefit table must hold n*m*T (broadcast) or E*n*m*T doubles");
+    if (st.benefit_mode != ASG_BENEFIT_INJECTED)
+        return fail(h, ASG_E_STATE, "handle was not created with benefit_mode=injected");
+    DeviceGuard g(h->device);
+    const double *src = table;
+    double *tmp = nullptr;
+    hipError_t e = hipSuccess;
+    if (!on_device) {
+        if ((e = hipMalloc(&tmp, sizeof(double) * count)) != hipSuccess) return hip_fail(h, e, "asg_set_benefits");
+        if ((e = hipMemcpyAsync(tmp, table, sizeof(double) * count, hipMemcpyHostToDevice, h->stream)) != hipSuccess) {
+            (void)hipFree(tmp);
+            return hip_fail(h, e, "asg_set_benefits");
+        }
+        src = tmp;
+    }
+    e = asg::launch_import_table(src, count == per ? 1 : st.E, st, h->stream);
+    if (tmp) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipFree(tmp);
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "asg_set_benefits");
+    h->table_ready = true;
+    return ASG_OK;
+}
+
+int asg_export_benefits(asg_handle *h, double *out_dev) {
+    if (!h || !out_dev) return fail(h, ASG_E_INVALID_ARG, "NULL argument");
+    if (!h->has_reset) return fail(h, ASG_E_STATE, "no episode yet: reset first");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_export_table(h->st, out_dev, h->stream);
+    return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_export_benefits");
+}
+
+int asg_export_prev_assigns(asg_handle *h, int64_t *out_dev) {
+    if (!h || !out_dev) return fail(h, ASG_E_INVALID_ARG, "NULL argument");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_export_prev(h->st, out_dev, h->stream);
+    return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_export_prev_assigns");
+}
+
+int asg_get_returns(asg_handle *h, double *out_dev) {
+    if (!h || !out_dev) return fail(h, ASG_E_INVALID_ARG, "NULL argument");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpyAsync(out_dev, h->st.returns, sizeof(double) * h->st.E, hipMemcpyDeviceToDevice,
+                                  h->stream);
+    return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_get_returns");
+}
+
+int asg_get_step(const asg_handle *h, int *k_out) {
+    if (!h || !k_out) return fail(nullptr, ASG_E_INVALID_ARG, "NULL argument");
+    *k_out = h->k;
+    return ASG_OK;
+}
+
+int asg_advance_stream(asg_handle *h, int64_t words) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (h->st.rng_mode != ASG_RNG_MT19937) return fail(h, ASG_E_STATE, "only MT19937 streams can be advanced");
+    if (words < 0) return fail(h, ASG_E_INVALID_ARG, "words must be >= 0");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_mt_advance(h->st, words, h->stream);
+    return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_advance_stream");
+}
+
+int asg_beta_hat(const void *beta, int beta_dtype, const int64_t beta_strides[3], const int64_t *prev,
+                 const int64_t prev_strides[2], int64_t B, int n, int m, const double *T_trans_dev, double lambda_,
+                 double *out, void *hip_stream) {
+    if (!beta || !beta_strides || !prev || !prev_strides || !out || B < 0 || n <= 0 || m <= 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_beta_hat: bad arguments");
+    if (beta_dtype != ASG_F32 && beta_dtype != ASG_F64)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_beta_hat: beta must be float32 or float64");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_beta_hat(beta, beta_dtype, beta_strides, prev, prev_strides, B, n, m, T_trans_dev,
+                                        lambda_, out, static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_beta_hat");
+}
+
+int asg_lsa_batched(const void *C, int dtype, const int64_t strides[3], int64_t B, int nr, int nc, int maximize,
+                    int64_t *row_out, int64_t *col_out, int32_t *status_out, void *hip_stream) {
+    if (B < 0 || nr < 0 || nc < 0 || !strides) return fail(nullptr, ASG_E_INVALID_ARG, "asg_lsa_batched: bad shape");
+    if (dtype != ASG_F32 && dtype != ASG_F64)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_lsa_batched: cost must be float32 or float64");
+    if ((nr > nc ? nr : nc) > 1024) return fail(nullptr, ASG_E_INVALID_ARG, "asg_lsa_batched: max(nr, nc) <= 1024");
+    if (B == 0 || nr == 0 || nc == 0) return ASG_OK;
+    if (!C) return fail(nullptr, ASG_E_INVALID_ARG, "asg_lsa_batched: NULL cost");
+    hipError_t e = asg::launch_lsa_batched(C, dtype, strides, B, nr, nc, maximize, row_out, col_out, status_out,
+                                           static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_lsa_batched");
+}
+
+int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64_t *prev,
+                   const int64_t prev_strides[2], int64_t B, int n, int m, const double *T_trans_dev, double lambda_,
+                   float *col_out, int32_t *status_out, void *hip_stream) {
+    if (!beta || !beta_strides || !prev || !prev_strides || !col_out || B < 0 || n <= 0 || m <= 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_haa_select: bad arguments");
+    if (n > m) return fail(nullptr, ASG_E_INVALID_ARG, "asg_haa_select: needs n <= m");
+    if (m > 1024) return fail(nullptr, ASG_E_INVALID_ARG, "asg_haa_select: m <= 1024");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_haa_select(beta, beta_strides, prev, prev_strides, B, n, m, T_trans_dev, lambda_,
+                                          col_out, status_out, static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_haa_select");
+}
+
+}  // extern "C"

@@ -1,0 +1,562 @@
+// asg_env.hip -- batched MockConstellationEnv kernels for gfx950.
+//
+// One workgroup advances one env.  The EpisodeBatch tensors (PyTorch-owned, any
+// strides) are written in place: the next pre-transition row (obs, beta, avail_actions,
+// prev_assigns, filled) and this step's post-transition row (rewards, terminated,
+// actions_onehot).  Benefits come from one of two sources:
+//   * BumpSrc  (Philox, native throughput mode): bump parameters are regenerated on the
+//     fly from a counter-based key each step -- no benefit table in HBM at all;
+//   * TableSrc (MT19937 compat / injected / exported): float64 table [E][T][n][m].
+// Reference: envs/mock_constellation_env.py:94-175 (reset / step / pre-transition data),
+// runners/episode_runner.py:60-100 and runners/parallel_runner.py:113-200 (which rows
+// get which fields), components/transforms.py:12-22 (OneHot, int64).
+#include "asg_device.h"
+#include "asg_internal.h"
+#include "lsa_wave.h"
+
+namespace asg {
+
+// ------------------------------------------------------------------------------------
+// benefit sources
+// ------------------------------------------------------------------------------------
+struct BumpSrc {
+    uint64_t seed;
+    int64_t env_base;
+    uint32_t episode;
+    int n, m, T;
+    double wmin, wmax;
+    bool dense;
+
+    struct Pair {
+        Bump b;
+        __device__ double at(int t) const { return bump_at(b, t); }
+    };
+    __device__ Pair pair(int64_t e, int i, int j) const {
+        return Pair{philox_bump(env_key(seed, env_base + e), episode, i, j, m, T, wmin, wmax, dense)};
+    }
+};
+
+struct TableSrc {
+    const double *tab;  // [E][T][n][m]
+    int n, m, T;
+
+    struct Pair {
+        const double *p;  // &tab[e][0][i][j]
+        int64_t tstride;
+        __device__ double at(int t) const { return p[t * tstride]; }
+    };
+    __device__ Pair pair(int64_t e, int i, int j) const {
+        const int64_t nm = (int64_t)n * m;
+        return Pair{tab + e * (int64_t)T * nm + (int64_t)i * m + j, nm};
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// pre-transition row writer: obs = [onehot(assign) | B(k) .. B(k+L-1)] (zeros past T),
+// beta = B(k) (zeros when k >= T), avail_actions = 1; optionally actions_onehot of the
+// post-transition row `ts_onehot`.  VEC consecutive tasks per work item.
+// ------------------------------------------------------------------------------------
+template <int VEC, class Src>
+__device__ void write_pre_row(const Src &src, const asg_batch_view &bv, int64_t e, int ts, int k,
+                              int n, int m, int T, int L, const int *s_assign, int ts_onehot) {
+    const int groups = m / VEC;
+    for (int idx = threadIdx.x; idx < n * groups; idx += blockDim.x) {
+        const int i = idx / groups;
+        const int j0 = (idx - i * groups) * VEC;
+        const int a = s_assign ? s_assign[i] : -1;
+        float oh[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
+        // benefits for lookahead blocks l = 0..L-1 at time k + l
+        typename Src::Pair P[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) P[q] = src.pair(e, i, j0 + q);
+        float *ob = fptr<float>(bv.obs, e, ts, i, j0);
+        const int64_t os = bv.obs.stride[3];
+        if (VEC == 4) {
+            *reinterpret_cast<float4 *>(ob) = make_float4(oh[0], oh[1], oh[2], oh[3]);
+        } else {
+            for (int q = 0; q < VEC; ++q) ob[q * os] = oh[q];
+        }
+        float b0[VEC];
+        for (int l = 0; l < L; ++l) {
+            const int t = k + l;
+            float val[VEC];
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) val[q] = (t < T) ? (float)P[q].at(t) : 0.0f;
+            if (l == 0) {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) b0[q] = val[q];
+            }
+            float *o = ob + (int64_t)m * (l + 1) * os;
+            if (VEC == 4) {
+                *reinterpret_cast<float4 *>(o) = make_float4(val[0], val[1], val[2], val[3]);
+            } else {
+                for (int q = 0; q < VEC; ++q) o[q * os] = val[q];
+            }
+        }
+        if (L == 0) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) b0[q] = (k < T) ? (float)P[q].at(k) : 0.0f;
+        }
+        if (bv.beta.ptr) {
+            float *bp = fptr<float>(bv.beta, e, ts, i, j0);
+            if (VEC == 4) {
+                *reinterpret_cast<float4 *>(bp) = make_float4(b0[0], b0[1], b0[2], b0[3]);
+            } else {
+                for (int q = 0; q < VEC; ++q) bp[q * bv.beta.stride[3]] = b0[q];
+            }
+        }
+        if (bv.avail_actions.ptr) {
+            uint8_t *ap = fptr<uint8_t>(bv.avail_actions, e, ts, i, j0);
+            if (VEC == 4) {
+                *reinterpret_cast<uint32_t *>(ap) = 0x01010101u;
+            } else {
+                for (int q = 0; q < VEC; ++q) ap[q * bv.avail_actions.stride[3]] = 1;
+            }
+        }
+        if (ts_onehot >= 0 && bv.actions_onehot.ptr) {
+            int64_t *hp = fptr<int64_t>(bv.actions_onehot, e, ts_onehot, i, j0);
+            if (VEC == 4) {
+                reinterpret_cast<longlong2 *>(hp)[0] = make_longlong2(oh[0] != 0.f, oh[1] != 0.f);
+                reinterpret_cast<longlong2 *>(hp)[1] = make_longlong2(oh[2] != 0.f, oh[3] != 0.f);
+            } else {
+                for (int q = 0; q < VEC; ++q) hp[q * bv.actions_onehot.stride[3]] = (oh[q] != 0.f);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// reset: prev_assigns = first n of a random permutation of m; row ts pre-transition data
+// ------------------------------------------------------------------------------------
+template <int VEC, class Src>
+__global__ void __launch_bounds__(256) reset_kernel(Src src, asg_batch_view bv, EnvState st, int ts,
+                                                    bool philox_perm) {
+    extern __shared__ int s_dyn[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m;
+    if (philox_perm) {
+        // Fisher-Yates from the top, Philox-drawn (distribution of choice(m, n, False))
+        int *perm = s_dyn;
+        for (int j = threadIdx.x; j < m; j += blockDim.x) perm[j] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const EnvKey key = env_key(st.seed, st.env_base + e);
+            for (int i = m - 1; i >= 1; --i) {
+                const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, 0u, kCtrPerm, st.episode}, key.k0, key.k1);
+                const int jj = (int)(((uint64_t)r.x * (uint64_t)(i + 1)) >> 32);
+                const int t = perm[i];
+                perm[i] = perm[jj];
+                perm[jj] = t;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) st.prev[e * n + i] = perm[i];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (bv.prev_assigns.ptr)
+            *fptr<int64_t>(bv.prev_assigns, e, ts, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : st.prev[e * n + i];
+    }
+    if (threadIdx.x == 0) {
+        st.returns[e] = 0.0;
+        if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts, 0, 0) = 1;
+    }
+    write_pre_row<VEC>(src, bv, e, ts, 0, n, m, st.T, st.L, nullptr, -1);
+}
+
+// ------------------------------------------------------------------------------------
+// step (mock_constellation_env.py:116-162 plus the runner's batch updates)
+// ------------------------------------------------------------------------------------
+template <int VEC, class Src>
+__global__ void __launch_bounds__(256) step_kernel(Src src, asg_batch_view bv, EnvState st, int ts, int k) {
+    extern __shared__ int s_dyn[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, T = st.T, L = st.L;
+    int *s_act = s_dyn;                                    // [n]
+    int *s_cnt = s_act + n;                                // [m]
+    double *s_rew = reinterpret_cast<double *>(s_cnt + m + ((n + m) & 1));  // [n], 8-aligned
+    __shared__ int s_err;
+
+    if (threadIdx.x == 0) s_err = 0;
+    for (int j = threadIdx.x; j < m; j += blockDim.x) s_cnt[j] = 0;
+    __syncthreads();
+    if (st.bids) {
+        // bids_as_actions: assignments = LSA(bids, maximize)[1]  (mock :121-122), wave 0
+        if (threadIdx.x < kWave) {
+            float *cost = reinterpret_cast<float *>(s_rew + n);          // [n][m]
+            double *u = reinterpret_cast<double *>(cost + n * m + ((n * m) & 1));
+            int *c4r = reinterpret_cast<int *>(u + n);
+            int *r4c = c4r + n;
+            int *path = r4c + m;
+            const float *bids = fptr<float>(bv.actions, e, ts, 0, 0);
+            int status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3],
+                                                      n, m, true, cost);
+            if (status == ASG_OK) {
+                LsaScratch sc{u, c4r, r4c, path};
+                const DenseCost<float> acc{cost, m};
+                if (m <= 64) status = lsa_solve_wave<1>(acc, n, m, sc);
+                else if (m <= 128) status = lsa_solve_wave<2>(acc, n, m, sc);
+                else if (m <= 256) status = lsa_solve_wave<4>(acc, n, m, sc);
+                else status = lsa_solve_wave<16>(acc, n, m, sc);
+            }
+            const int lane = threadIdx.x;
+            for (int i = lane; i < n; i += kWave) s_act[i] = status == ASG_OK ? c4r[i] : 0;
+            if (lane == 0 && status != ASG_OK) s_err = status;
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int64_t a = *fptr<int64_t>(bv.actions, e, ts, i, 0);
+            const bool ok = a >= 0 && a < m;
+            s_act[i] = ok ? (int)a : 0;
+            if (!ok) s_err = ASG_E_ACTION_RANGE;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&s_cnt[s_act[i]], 1);
+    __syncthreads();
+    // rewards (mock :126-138): only the chosen task's beta_hat is needed per agent
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int j = s_act[i];
+        const int p = st.prev[e * n + i];
+        const double beta = src.pair(e, i, j).at(k);
+        const double tt = st.T_trans ? st.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+        const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+        const double bh = beta - st.lambda_ * pen;
+        const double r = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+        s_rew[i] = r;
+        if (bv.rewards.ptr) *fptr<float>(bv.rewards, e, ts, i, 0) = (float)r;
+        st.prev[e * n + i] = j;
+        if (bv.prev_assigns.ptr)
+            *fptr<int64_t>(bv.prev_assigns, e, ts + 1, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+    }
+    const bool done = k + 1 >= T;
+    // next pre-transition row (mock :141-160) + this row's OneHot of the actions
+    write_pre_row<VEC>(src, bv, e, ts + 1, k + 1, n, m, T, L, s_act, st.bids ? -1 : ts);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // episode_return += sum(rewards): Python sums the float64 list left to right
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += s_rew[i];
+        st.returns[e] += s;
+        bool term = done;  // terminated = done != info.get("T", False)
+        if (st.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
+        if (bv.terminated.ptr) *fptr<uint8_t>(bv.terminated, e, ts, 0, 0) = term;
+        if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts + 1, 0, 0) = 1;
+        if (s_err) atomicCAS(st.err, 0, s_err);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// uniform random actions (BASELINE config 2 random policy)
+// ------------------------------------------------------------------------------------
+__global__ void random_actions_kernel(asg_batch_view bv, EnvState st, int ts, int k) {
+    const int64_t e = blockIdx.x;
+    const EnvKey key = env_key(st.seed, st.env_base + e);
+    for (int i = threadIdx.x; i < st.n; i += blockDim.x) {
+        const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, (uint32_t)k, kCtrAction, st.episode}, key.k0, key.k1);
+        *fptr<int64_t>(bv.actions, e, ts, i, 0) = (int64_t)(((uint64_t)r.x * (uint64_t)st.m) >> 32);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// table export (Philox bumps -> [E][n][m][T] float64, the reference layout)
+// ------------------------------------------------------------------------------------
+template <class Src>
+__global__ void export_table_kernel(Src src, EnvState st, double *out) {
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, T = st.T;
+    for (int p = threadIdx.x; p < n * m; p += blockDim.x) {
+        const int i = p / m, j = p - i * m;
+        const auto P = src.pair(e, i, j);
+        for (int t = 0; t < T; ++t) out[((e * n + i) * (int64_t)m + j) * T + t] = P.at(t);
+    }
+}
+
+// [E][n][m][T] (reference layout) -> [E][T][n][m] (kernel layout)
+__global__ void import_table_kernel(const double *in, EnvState st, double *tab, int64_t src_envs) {
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, T = st.T;
+    const int64_t se = src_envs == 1 ? 0 : e;
+    for (int64_t p = threadIdx.x; p < (int64_t)n * m * T; p += blockDim.x) {
+        const int t = (int)(p % T);
+        const int64_t ij = p / T;
+        tab[(e * T + t) * (int64_t)n * m + ij] = in[se * (int64_t)n * m * T + p];
+    }
+}
+
+__global__ void export_prev_kernel(EnvState st, int64_t *out) {
+    const int64_t e = blockIdx.x;
+    for (int i = threadIdx.x; i < st.n; i += blockDim.x) out[e * st.n + i] = st.prev[e * st.n + i];
+}
+
+// ------------------------------------------------------------------------------------
+// legacy MT19937 compat mode: one wave per env, stream state [E][625] in HBM
+// ------------------------------------------------------------------------------------
+constexpr int kMtN = 624, kMtM = 397;
+
+__global__ void mt_seed_kernel(uint32_t *mt, int64_t E, uint64_t seed, int64_t base, bool replicate) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    uint32_t *key = mt + e * (kMtN + 1);
+    uint32_t s = (uint32_t)(replicate ? seed : seed + (uint64_t)(base + e));
+    key[0] = s;
+    for (int i = 1; i < kMtN; ++i) {
+        s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
+        key[i] = s;
+    }
+    key[kMtN] = kMtN;  // pos
+}
+
+// A wave-cooperative view of one MT19937 stream in LDS with pre-tempered output words.
+struct MtWave {
+    uint32_t *key;  // [624] raw state (LDS)
+    uint32_t *out;  // [624] tempered words (LDS)
+    int pos;        // wave-uniform
+
+    __device__ void twist() {
+        const int lane = threadIdx.x & (kWave - 1);
+        // scipy-free restatement of the MT recurrence in 4 dependency phases
+        auto gen = [&](int i, uint32_t ki, uint32_t ki1, uint32_t kim) {
+            const uint32_t y = (ki & 0x80000000u) | (ki1 & 0x7fffffffu);
+            return kim ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        };
+        const int phase_lo[3] = {0, kMtN - kMtM, 2 * (kMtN - kMtM)};
+        const int phase_hi[3] = {kMtN - kMtM, 2 * (kMtN - kMtM), kMtN - 1};
+        for (int ph = 0; ph < 3; ++ph) {
+            uint32_t nv[4];
+            int cnt = 0;
+            for (int i = phase_lo[ph] + lane; i < phase_hi[ph]; i += kWave, ++cnt)
+                nv[cnt] = gen(i, key[i], key[i + 1], key[(i + kMtM) % kMtN]);
+            wave_sync();
+            cnt = 0;
+            for (int i = phase_lo[ph] + lane; i < phase_hi[ph]; i += kWave, ++cnt) key[i] = nv[cnt];
+            wave_sync();
+        }
+        if (lane == 0) key[kMtN - 1] = gen(kMtN - 1, key[kMtN - 1], key[0], key[kMtM - 1]);
+        wave_sync();
+        temper_all();
+        pos = 0;
+    }
+    __device__ void temper_all() {
+        const int lane = threadIdx.x & (kWave - 1);
+        for (int i = lane; i < kMtN; i += kWave) {
+            uint32_t y = key[i];
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= (y >> 18);
+            out[i] = y;
+        }
+        wave_sync();
+    }
+    __device__ uint32_t next() {
+        if (pos >= kMtN) twist();
+        return out[pos++];
+    }
+    __device__ double next_double() {
+        const uint32_t a = next() >> 5, b = next() >> 6;
+        return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    }
+    __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * next_double(); }
+    __device__ uint32_t interval(uint32_t max) {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+        uint32_t v;
+        while ((v = (next() & mask)) > max) {}
+        return v;
+    }
+};
+
+// generate_benefits_over_time + permutation in MT compat mode.  construct: also replay
+// the throwaway __init__ table draw (mock :34) first.  tab: [E][T][n][m].
+__global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvState st, double *tab, bool construct,
+                                                       bool generate) {
+    const bool write_table = generate;
+    extern __shared__ uint32_t s_mt[];
+    uint32_t *key = s_mt;
+    uint32_t *out = s_mt + kMtN;
+    int *perm = reinterpret_cast<int *>(out + kMtN);
+    const int64_t e = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int n = st.n, m = st.m, T = st.T;
+    uint32_t *g = mtstate + e * (kMtN + 1);
+    for (int i = lane; i < kMtN; i += kWave) key[i] = g[i];
+    wave_sync();
+    MtWave mt{key, out, (int)g[kMtN]};
+    mt.temper_all();
+    const int64_t nm = (int64_t)n * m;
+    double *te = tab + e * T * nm;
+    if (write_table)
+        for (int64_t p = lane; p < T * nm; p += kWave) te[p] = 0.0;
+    wave_sync();
+    for (int pass = construct ? 0 : 1; generate && pass < 2; ++pass) {
+        const double wmin = pass == 0 ? st.wmin_init : st.wmin;
+        const double wmax = pass == 0 ? st.wmax_init : st.wmax;
+        for (int j = 0; j < m; ++j) {
+            const double scale = (mt.next() & 3u) == 3u ? 10.0 : 1.0;
+            for (int i = 0; i < n; ++i) {
+                const double r = mt.next_double();
+                if (!(r > 0.75)) continue;
+                const double center = mt.uniform(0.0, (double)T);
+                const double spread = mt.uniform(wmin, wmax);
+                if (pass == 1 && write_table) {
+                    const double s2 = bump_s2(spread);
+                    for (int t = lane; t < T; t += kWave)
+                        te[(int64_t)t * nm + (int64_t)i * m + j] = bump_value(scale, center, s2, t);
+                }
+            }
+        }
+    }
+    // prev_assigns = choice(m, n, replace=False) = permutation(m)[:n]  (mock :105)
+    for (int j = lane; j < m; j += kWave) perm[j] = j;
+    wave_sync();
+    for (int i = m - 1; i >= 1; --i) {
+        const int jj = (int)mt.interval((uint32_t)i);
+        if (lane == 0) {
+            const int t = perm[i];
+            perm[i] = perm[jj];
+            perm[jj] = t;
+        }
+        wave_sync();
+    }
+    for (int i = lane; i < n; i += kWave) st.prev[e * n + i] = perm[i];
+    for (int i = lane; i < kMtN; i += kWave) g[i] = key[i];
+    if (lane == 0) g[kMtN] = (uint32_t)mt.pos;
+}
+
+// skip `words` draws of every stream (other consumers of numpy's global stream)
+__global__ void __launch_bounds__(64) mt_advance_kernel(uint32_t *mtstate, int64_t words) {
+    extern __shared__ uint32_t s_mt[];
+    uint32_t *key = s_mt, *out = s_mt + kMtN;
+    const int64_t e = blockIdx.x;
+    uint32_t *g = mtstate + e * (kMtN + 1);
+    for (int i = threadIdx.x; i < kMtN; i += kWave) key[i] = g[i];
+    wave_sync();
+    MtWave mt{key, out, (int)g[kMtN]};
+    int64_t left = words;
+    while (left > 0) {
+        if (mt.pos >= kMtN) mt.twist();
+        const int64_t take = min<int64_t>(left, kMtN - mt.pos);
+        mt.pos += (int)take;
+        left -= take;
+    }
+    for (int i = threadIdx.x; i < kMtN; i += kWave) g[i] = key[i];
+    if (threadIdx.x == 0) g[kMtN] = (uint32_t)mt.pos;
+}
+
+// ------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------
+// float4 / uchar4 / 2x longlong2 row stores need unit inner stride, 4-element aligned
+// outer strides and aligned base pointers
+static bool vec4_ok(const asg_batch_view &b, int m) {
+    auto al = [](const asg_field &f, uintptr_t bytes) {
+        if (!f.ptr) return true;
+        if (f.stride[3] != 1 || reinterpret_cast<uintptr_t>(f.ptr) % bytes) return false;
+        return f.stride[0] % 4 == 0 && f.stride[1] % 4 == 0 && f.stride[2] % 4 == 0;
+    };
+    return m % 4 == 0 && al(b.obs, 16) && al(b.beta, 16) && al(b.avail_actions, 4) &&
+           al(b.actions_onehot, 16);
+}
+
+static size_t step_lds_bytes(const EnvState &st) {
+    size_t b = sizeof(int) * (st.n + st.m + ((st.n + st.m) & 1)) + sizeof(double) * st.n;
+    if (st.bids) {
+        b += sizeof(float) * ((size_t)st.n * st.m + ((st.n * st.m) & 1)) + sizeof(double) * st.n +
+             sizeof(int) * (st.n + 2 * st.m);
+    }
+    return b + 16;
+}
+
+template <class Src>
+static hipError_t launch_step_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts, int k,
+                                  hipStream_t s) {
+    const size_t lds = step_lds_bytes(st);
+    if (vec4_ok(bv, st.m))
+        hipLaunchKernelGGL((step_kernel<4, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
+    else
+        hipLaunchKernelGGL((step_kernel<1, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
+    return hipGetLastError();
+}
+
+template <class Src>
+static hipError_t launch_reset_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts,
+                                   bool philox_perm, hipStream_t s) {
+    const size_t lds = sizeof(int) * st.m + 16;
+    if (vec4_ok(bv, st.m))
+        hipLaunchKernelGGL((reset_kernel<4, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, philox_perm);
+    else
+        hipLaunchKernelGGL((reset_kernel<1, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, philox_perm);
+    return hipGetLastError();
+}
+
+static BumpSrc bump_src(const EnvState &st) {
+    return BumpSrc{st.seed, st.env_base, st.episode, st.n, st.m, st.T, st.wmin, st.wmax,
+                   st.benefit_mode == ASG_BENEFIT_DENSE};
+}
+static TableSrc table_src(const EnvState &st) { return TableSrc{st.table, st.n, st.m, st.T}; }
+
+static bool uses_table(const EnvState &st) {
+    return st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
+}
+
+hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s) {
+    if (st.rng_mode == ASG_RNG_MT19937) {
+        const size_t lds = sizeof(uint32_t) * 2 * kMtN + sizeof(int) * st.m + 16;
+        const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
+        // with an injected table (sat_prox_mat=) neither __init__ nor reset draw a
+        // table: only the permutation consumes the stream (mock :32-37, :99-105)
+        hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.table, construct && gen,
+                           gen);
+        hipError_t err = hipGetLastError();
+        if (err != hipSuccess) return err;
+        return launch_reset_src(table_src(st), bv, st, ts, false, s);
+    }
+    if (uses_table(st)) return launch_reset_src(table_src(st), bv, st, ts, true, s);
+    return launch_reset_src(bump_src(st), bv, st, ts, true, s);
+}
+
+hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
+    if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s);
+    return launch_step_src(bump_src(st), bv, st, ts, k, s);
+}
+
+hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
+    hipLaunchKernelGGL(random_actions_kernel, dim3(st.E), dim3(64), 0, s, bv, st, ts, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s) {
+    if (uses_table(st))
+        hipLaunchKernelGGL((export_table_kernel<TableSrc>), dim3(st.E), dim3(256), 0, s, table_src(st), st, out);
+    else
+        hipLaunchKernelGGL((export_table_kernel<BumpSrc>), dim3(st.E), dim3(256), 0, s, bump_src(st), st, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_import_table(const double *in, int64_t src_envs, const EnvState &st, hipStream_t s) {
+    hipLaunchKernelGGL(import_table_kernel, dim3(st.E), dim3(256), 0, s, in, st, st.table, src_envs);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_prev(const EnvState &st, int64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(export_prev_kernel, dim3(st.E), dim3(64), 0, s, st, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_seed(const EnvState &st, hipStream_t s) {
+    const int64_t blocks = (st.E + 63) / 64;
+    hipLaunchKernelGGL(mt_seed_kernel, dim3(blocks), dim3(64), 0, s, st.mt, st.E, st.seed, st.env_base,
+                       (st.quirks & ASG_QUIRK_REPLICATE_STREAM) != 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_mt_advance(const EnvState &st, int64_t words, hipStream_t s) {
+    hipLaunchKernelGGL(mt_advance_kernel, dim3(st.E), dim3(64), sizeof(uint32_t) * 2 * kMtN, s, st.mt, words);
+    return hipGetLastError();
+}
+
+}  // namespace asg

@@ -1,0 +1,51 @@
+// asg_internal.h -- device-resident state of one handle, shared by the kernels and the
+// C-ABI layer (passed to kernels by value: a few scalars plus device pointers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/asg.h"
+
+namespace asg {
+
+struct EnvState {
+    int64_t E;             // envs in this handle
+    int n, m, T, L;
+    double lambda_;
+    int bids;              // bids_as_actions
+    int rng_mode;          // asg_rng_mode
+    int benefit_mode;      // asg_benefit_mode
+    uint32_t quirks;       // ASG_QUIRK_*
+    uint64_t seed;
+    int64_t env_base;      // global index of env 0
+    uint32_t episode;      // Philox counter: episodes reset so far (this handle)
+    double wmin_init, wmax_init;  // throwaway __init__ draw widths (mock :34)
+    double wmin, wmax;            // reset draw widths (mock :100)
+    const double *T_trans; // device [m][m] or nullptr (= 1 - I)
+    int *prev;             // [E][n] previous assignment (state for beta_hat)
+    double *returns;       // [E] float64 episode returns
+    double *table;         // [E][T][n][m] float64 (MT19937 / injected modes)
+    uint32_t *mt;          // [E][625] MT19937 key + pos (compat mode)
+    int *err;              // sticky device error code
+};
+
+hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s);
+hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
+hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
+hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s);
+hipError_t launch_import_table(const double *in, int64_t src_envs, const EnvState &st, hipStream_t s);
+hipError_t launch_export_prev(const EnvState &st, int64_t *out, hipStream_t s);
+hipError_t launch_mt_seed(const EnvState &st, hipStream_t s);
+hipError_t launch_mt_advance(const EnvState &st, int64_t words, hipStream_t s);
+
+hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3], int64_t B, int nr, int nc,
+                              int maximize, int64_t *row_out, int64_t *col_out, int32_t *status_out,
+                              hipStream_t s);
+hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], const int64_t *prev,
+                           const int64_t ps[2], int64_t B, int n, int m, const double *T_trans, double lambda_,
+                           double *out, hipStream_t s);
+hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
+                             int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
+                             int32_t *status_out, hipStream_t s);
+
+}  // namespace asg

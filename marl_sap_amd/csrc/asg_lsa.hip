@@ -1,0 +1,240 @@
+// asg_lsa.hip -- batched scipy-exact linear sum assignment, beta_hat and the fused HAA
+// selector (gfx950).  One wave64 per problem; the working cost matrix sits in LDS when
+// it fits (48 KiB budget per wave), otherwise it is read in place from global memory
+// (L2-resident for the row sweeps).
+// Reference call sites: sap_selectors.py:32,90 (SAP selectors on Q-values),
+// non_rl_selectors.py:36-47 (HAA: beta_hat + LSA), mock_constellation_env.py:228-274.
+#include "asg_device.h"
+#include "asg_internal.h"
+#include "lsa_wave.h"
+
+namespace asg {
+
+constexpr size_t kLdsCostBudget = 48 * 1024;
+
+// working matrix read in place: transposed when nr0 > nc0, negated for maximize
+template <typename IT>
+struct GlobalCost {
+    const IT *C;
+    int64_t rs, cs;
+    bool tr, neg;
+    __device__ double operator()(int i, int j) const {
+        const double x = (double)(tr ? C[(int64_t)j * rs + (int64_t)i * cs] : C[(int64_t)i * rs + (int64_t)j * cs]);
+        return neg ? -x : x;
+    }
+};
+
+template <typename IT>
+__device__ int lsa_check_wave(const IT *C, int64_t rs, int64_t cs, int nr0, int nc0, bool maximize) {
+    const int lane = threadIdx.x & (kWave - 1);
+    int bad = 0;
+    for (int idx = lane; idx < nr0 * nc0; idx += kWave) {
+        const int r = idx / nc0, c = idx - r * nc0;
+        double x = (double)C[r * rs + c * cs];
+        if (maximize) x = -x;
+        bad |= (x != x) || (x == -__builtin_inf());
+    }
+    return wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
+}
+
+template <int CPL, class Acc>
+__device__ int solve_cpl(const Acc &acc, int nr, int nc, LsaScratch s) {
+    return lsa_solve_wave<CPL>(acc, nr, nc, s);
+}
+
+template <class Acc>
+__device__ int solve_any(const Acc &acc, int nr, int nc, LsaScratch s) {
+    if (nc <= 64) return solve_cpl<1>(acc, nr, nc, s);
+    if (nc <= 128) return solve_cpl<2>(acc, nr, nc, s);
+    if (nc <= 256) return solve_cpl<4>(acc, nr, nc, s);
+    if (nc <= 512) return solve_cpl<8>(acc, nr, nc, s);
+    return solve_cpl<16>(acc, nr, nc, s);
+}
+
+// LDS carve: [cost (optional)][u: nr f64][col4row: nr][row4col: nc][path: nc][mark: nr0]
+template <typename IT, typename CT, bool LDS_COST>
+__global__ void __launch_bounds__(64) lsa_batched_kernel(const IT *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
+                                                         int nc0, int maximize, int64_t *row_out, int64_t *col_out,
+                                                         int32_t *status_out) {
+    extern __shared__ double s_lsa[];
+    const int64_t b = blockIdx.x;
+    const IT *Cb = C + b * s0;
+    const bool tr = nc0 < nr0;
+    const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;
+    const int k = nr;
+    char *p = reinterpret_cast<char *>(s_lsa);
+    CT *cost = reinterpret_cast<CT *>(p);
+    if (LDS_COST) p += ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
+    LsaScratch sc;
+    sc.u = reinterpret_cast<double *>(p);
+    p += sizeof(double) * nr;
+    sc.col4row = reinterpret_cast<int *>(p);
+    p += sizeof(int) * nr;
+    sc.row4col = reinterpret_cast<int *>(p);
+    p += sizeof(int) * nc;
+    sc.path = reinterpret_cast<int *>(p);
+    p += sizeof(int) * nc;
+    int *mark = reinterpret_cast<int *>(p);
+
+    int status;
+    if (LDS_COST) {
+        status = lsa_stage_wave<IT, CT>(Cb, s1, s2, nr0, nc0, maximize != 0, cost);
+        if (status == ASG_OK) status = solve_any(DenseCost<CT>{cost, nc}, nr, nc, sc);
+    } else {
+        status = lsa_check_wave<IT>(Cb, s1, s2, nr0, nc0, maximize != 0);
+        if (status == ASG_OK) status = solve_any(GlobalCost<IT>{Cb, s1, s2, tr, maximize != 0}, nr, nc, sc);
+    }
+    const int lane = threadIdx.x;
+    if (status == ASG_OK) {
+        lsa_emit_wave(sc.col4row, nr0, nc0, mark, row_out ? row_out + b * k : nullptr,
+                      col_out ? col_out + b * k : nullptr, nullptr);
+    } else {
+        for (int r = lane; r < k; r += kWave) {
+            if (row_out) row_out[b * k + r] = -1;
+            if (col_out) col_out[b * k + r] = -1;
+        }
+    }
+    if (lane == 0 && status_out) status_out[b] = status;
+}
+
+static size_t lsa_scratch_bytes(int nr, int nc, int nr0) {
+    return sizeof(double) * nr + sizeof(int) * (nr + 2 * nc + nr0) + 64;
+}
+
+template <typename IT, typename CT>
+static hipError_t launch_lsa_t(const IT *C, const int64_t st[3], int64_t B, int nr0, int nc0, int maximize,
+                               int64_t *row_out, int64_t *col_out, int32_t *status_out, hipStream_t s) {
+    const int nr = nc0 < nr0 ? nc0 : nr0, nc = nc0 < nr0 ? nr0 : nc0;
+    const size_t cost_bytes = ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
+    const size_t scratch = lsa_scratch_bytes(nr, nc, nr0);
+    if (cost_bytes <= kLdsCostBudget) {
+        hipLaunchKernelGGL((lsa_batched_kernel<IT, CT, true>), dim3(B), dim3(64), cost_bytes + scratch, s, C, st[0],
+                           st[1], st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+    } else {
+        hipLaunchKernelGGL((lsa_batched_kernel<IT, CT, false>), dim3(B), dim3(64), scratch, s, C, st[0], st[1],
+                           st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3], int64_t B, int nr, int nc,
+                              int maximize, int64_t *row_out, int64_t *col_out, int32_t *status_out,
+                              hipStream_t s) {
+    if (dtype == ASG_F32)
+        return launch_lsa_t<float, float>(static_cast<const float *>(C), strides, B, nr, nc, maximize, row_out,
+                                          col_out, status_out, s);
+    return launch_lsa_t<double, double>(static_cast<const double *>(C), strides, B, nr, nc, maximize, row_out,
+                                        col_out, status_out, s);
+}
+
+// ------------------------------------------------------------------------------------
+// beta_hat = beta - lambda * T_trans[prev_i, j] * (beta > 1e-12)   (mock :250-270)
+// ------------------------------------------------------------------------------------
+template <typename BT>
+__global__ void beta_hat_kernel(const BT *beta, int64_t b0, int64_t b1, int64_t b2, const int64_t *prev, int64_t p0,
+                                int64_t p1, int64_t B, int n, int m, const double *T_trans, double lambda_,
+                                double *out) {
+    const int64_t total = B * n * m;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(idx % m);
+        const int64_t bi = idx / m;
+        const int i = (int)(bi % n);
+        const int64_t b = bi / n;
+        const double x = (double)beta[b * b0 + i * b1 + j * b2];
+        const int64_t p = prev[b * p0 + i * p1];
+        const double tt = T_trans ? T_trans[p * m + j] : (j == p ? 0.0 : 1.0);
+        out[idx] = x - lambda_ * (tt * (x > 1e-12 ? 1.0 : 0.0));
+    }
+}
+
+hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], const int64_t *prev,
+                           const int64_t ps[2], int64_t B, int n, int m, const double *T_trans, double lambda_,
+                           double *out, hipStream_t s) {
+    const int64_t total = B * n * m;
+    const int64_t blocks = total == 0 ? 1 : (total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192;
+    if (dtype == ASG_F32)
+        hipLaunchKernelGGL(beta_hat_kernel<float>, dim3(blocks), dim3(256), 0, s, static_cast<const float *>(beta),
+                           bs[0], bs[1], bs[2], prev, ps[0], ps[1], B, n, m, T_trans, lambda_, out);
+    else
+        hipLaunchKernelGGL(beta_hat_kernel<double>, dim3(blocks), dim3(256), 0, s,
+                           static_cast<const double *>(beta), bs[0], bs[1], bs[2], prev, ps[0], ps[1], B, n, m,
+                           T_trans, lambda_, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// HAASelector (non_rl_selectors.py:19-50): col = LSA(beta_hat(beta, prev), maximize)[1]
+// The working matrix -beta_hat is formed on the fly from the f32 beta staged in LDS, so
+// a 64x64 problem needs 16 KiB of LDS instead of 32.
+// ------------------------------------------------------------------------------------
+struct HaaCost {
+    const float *beta;  // [n][m] in LDS (rs = m, cs = 1) or in place in global memory
+    int64_t rs, cs;
+    const int *prev;    // LDS [n]
+    const double *T_trans;
+    double lambda_;
+    int m;
+    __device__ double operator()(int i, int j) const {
+        const double x = (double)beta[i * rs + j * cs];
+        const int p = prev[i];
+        const double tt = T_trans ? T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+        return -(x - lambda_ * (tt * (x > 1e-12 ? 1.0 : 0.0)));
+    }
+};
+
+template <bool STAGE>
+__global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
+                                                        const int64_t *prev, int64_t p0, int64_t p1, int n, int m,
+                                                        const double *T_trans, double lambda_, float *col_out,
+                                                        int32_t *status_out) {
+    extern __shared__ double s_lsa[];
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    char *p = reinterpret_cast<char *>(s_lsa);
+    float *sb = reinterpret_cast<float *>(p);
+    if (STAGE) p += ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
+    int *sp = reinterpret_cast<int *>(p);
+    p += ((sizeof(int) * n + 15) / 16) * 16;
+    LsaScratch sc;
+    sc.u = reinterpret_cast<double *>(p);
+    p += sizeof(double) * n;
+    sc.col4row = reinterpret_cast<int *>(p);
+    p += sizeof(int) * n;
+    sc.row4col = reinterpret_cast<int *>(p);
+    p += sizeof(int) * m;
+    sc.path = reinterpret_cast<int *>(p);
+    int bad = 0;
+    for (int idx = lane; idx < n * m; idx += kWave) {
+        const int i = idx / m, j = idx - i * m;
+        const float x = beta[b * b0 + i * b1 + j * b2];
+        if (STAGE) sb[idx] = x;
+        bad |= (x != x) || (x == __builtin_inff());  // -(+inf) = -inf is invalid
+    }
+    for (int i = lane; i < n; i += kWave) sp[i] = (int)prev[b * p0 + i * p1];
+    wave_sync();
+    int status = wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
+    if (status == ASG_OK) {
+        const HaaCost acc = STAGE ? HaaCost{sb, m, 1, sp, T_trans, lambda_, m}
+                                  : HaaCost{beta + b * b0, b1, b2, sp, T_trans, lambda_, m};
+        status = solve_any(acc, n, m, sc);
+    }
+    for (int i = lane; i < n; i += kWave) col_out[b * n + i] = status == ASG_OK ? (float)sc.col4row[i] : -1.0f;
+    if (lane == 0 && status_out) status_out[b] = status;
+}
+
+hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
+                             int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
+                             int32_t *status_out, hipStream_t s) {
+    const size_t cost = ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
+    const size_t rest = ((sizeof(int) * n + 15) / 16) * 16 + sizeof(double) * n + sizeof(int) * (n + 2 * m) + 64;
+    if (cost <= kLdsCostBudget)
+        hipLaunchKernelGGL(haa_select_kernel<true>, dim3(B), dim3(64), cost + rest, s, beta, bs[0], bs[1], bs[2],
+                           prev, ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out);
+    else
+        hipLaunchKernelGGL(haa_select_kernel<false>, dim3(B), dim3(64), rest, s, beta, bs[0], bs[1], bs[2], prev,
+                           ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out);
+    return hipGetLastError();
+}
+
+}  // namespace asg

@@ -1,0 +1,144 @@
+"""GPU vectorised rollout runner: drop-in for EpisodeRunner / ParallelRunner
+(reference: runners/episode_runner.py:8-137, runners/parallel_runner.py:12-243).
+
+Constructed as GpuVecRunner(args, logger) and used exactly like the reference runners
+(get_env / setup / run / t_env / close_env / save_replay).  Instead of one OS process and
+one pickled Pipe round-trip per env per step, all `batch_size_run` envs of this rank live
+in HBM behind one C-ABI handle and every step is:
+
+    mac.select_actions (PyTorch-ROCm)  ->  actions row write  ->  asg_step (one HIP kernel)
+
+with the EpisodeBatch kept resident on the GPU in time-major storage.  Under
+torch.distributed (one process per GPU, RCCL) each rank owns envs
+[rank*E, (rank+1)*E); the only collective is once per episode: an all-gather of the
+float64 episode returns and an all-reduce of the env-step counter.
+
+Protocols (args.runner_protocol):
+  "episode"  EpisodeRunner semantics per env: T selection passes, true terminated flag,
+             row T actions left 0.
+  "parallel" ParallelRunner semantics: one extra selection pass at t = T writing row T
+             actions (+ one-hot), and its terminated-flag quirk when args.env_quirks
+             contains "parallel_terminated".
+"""
+
+import numpy as np
+import torch
+
+from .. import dist as asg_dist
+from ..components.episode_buffer import EpisodeBatch
+from ..envs import BATCHED_REGISTRY
+
+
+class GpuVecRunner:
+    def __init__(self, args, logger):
+        self.args = args
+        self.logger = logger
+        self.batch_size = args.batch_size_run
+        self.rank, self.world = asg_dist.rank_world()
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        env_args = dict(args.env_args)
+        env_args.pop("seed", None)
+        self.env = BATCHED_REGISTRY[args.env](
+            **env_args, seed=args.env_args.get("seed", 0) or 0, num_envs=self.batch_size,
+            env_index_base=self.rank * self.batch_size, device=self.device,
+            rng=getattr(args, "env_rng", "philox"), quirks=tuple(getattr(args, "env_quirks", ())))
+        self.T = self.env.T
+        self.protocol = getattr(args, "runner_protocol", "episode")
+        self.reuse_batch = getattr(args, "reuse_batch", True)
+        self.t = 0
+        self.t_env = 0
+        self.train_returns, self.test_returns = [], []
+        self.train_stats, self.test_stats = {}, {}
+        self.log_train_stats_t = -1000000
+        self.last_returns = None  # device tensor of the last episode's (gathered) returns
+        self.batch = None
+
+    # ------------------------------------------------------------------ plugin surface
+    def setup(self, scheme, groups, preprocess, mac):
+        self.scheme, self.groups, self.preprocess = scheme, groups, preprocess
+        self.mac = mac
+        self.mac.action_selector.envs = self.env
+        if hasattr(self.mac, "jumpstart_action_selector"):
+            self.mac.jumpstart_action_selector.envs = self.env
+
+    def new_batch(self):
+        return EpisodeBatch(self.scheme, self.groups, self.batch_size, self.T + 1, preprocess=self.preprocess,
+                            device=self.device, time_major=True)
+
+    def get_env_info(self):
+        return self.env.get_env_info()
+
+    def get_env(self):
+        return self.env
+
+    def save_replay(self):
+        self.env.save_replay()
+
+    def close_env(self):
+        self.env.close()
+
+    def reset(self):
+        if self.batch is None or not self.reuse_batch:
+            self.batch = self.new_batch()
+        self.env.reset(self.batch, ts=0)
+        self.t = 0
+
+    # ------------------------------------------------------------------ rollout
+    @torch.no_grad()
+    def rollout(self, test_mode=False):
+        """One episode of every env, fully asynchronous (no host sync)."""
+        self.reset()
+        self.mac.init_hidden(batch_size=self.batch_size)
+        for t in range(self.T):
+            actions = self.mac.select_actions(self.batch, t_ep=t, t_env=self.t_env, test_mode=test_mode)
+            self.batch.update({"actions": actions}, ts=t, mark_filled=False, preprocess=False)
+            self.env.step(self.batch, ts=t)
+        self.t = self.T
+        if self.protocol == "parallel":
+            actions = self.mac.select_actions(self.batch, t_ep=self.T, t_env=self.t_env, test_mode=test_mode)
+            self.batch.update({"actions": actions}, ts=self.T, mark_filled=False)
+        return self.batch
+
+    def finish_episode(self, test_mode=False):
+        """Per-episode host sync: device errors, returns gather, counters, logging."""
+        self.env.sync()
+        for sel in (getattr(self.mac, "action_selector", None), getattr(self.mac, "jumpstart_action_selector", None)):
+            st = getattr(sel, "status", None)
+            if st is not None:
+                st.flush()
+        returns = asg_dist.all_gather_returns(self.env.get_returns())
+        self.last_returns = returns
+        steps = asg_dist.all_reduce_sum(self.batch_size * self.T)
+        cur_stats = self.test_stats if test_mode else self.train_stats
+        cur_returns = self.test_returns if test_mode else self.train_returns
+        log_prefix = "test_" if test_mode else ""
+        n_eps = self.batch_size * self.world
+        cur_stats["n_episodes"] = n_eps + cur_stats.get("n_episodes", 0)
+        cur_stats["ep_length"] = steps + cur_stats.get("ep_length", 0)
+        cur_returns.extend(returns.cpu().tolist())
+        if not test_mode:
+            self.t_env += steps
+        n_test_runs = max(1, self.args.test_nepisode // n_eps) * n_eps
+        if test_mode and len(self.test_returns) == n_test_runs:
+            self._log(cur_returns, cur_stats, log_prefix)
+        elif self.t_env - self.log_train_stats_t >= self.args.runner_log_interval:
+            self._log(cur_returns, cur_stats, log_prefix)
+            if hasattr(self.mac.action_selector, "epsilon"):
+                self.logger.log_stat("epsilon", self.mac.action_selector.epsilon, self.t_env)
+            self.log_train_stats_t = self.t_env
+            self.logger.log_stat("steps", self.t_env, self.t_env)
+
+    def run(self, test_mode=False):
+        batch = self.rollout(test_mode=test_mode)
+        self.finish_episode(test_mode=test_mode)
+        return batch
+
+    def _log(self, returns, stats, prefix):
+        if self.rank == 0 and self.logger is not None:
+            self.logger.log_stat(prefix + "return_mean", np.mean(returns), self.t_env)
+            self.logger.log_stat(prefix + "return_std", np.std(returns), self.t_env)
+            for k, v in stats.items():
+                if k != "n_episodes":
+                    self.logger.log_stat(prefix + k + "_mean", v / stats["n_episodes"], self.t_env)
+        returns.clear()
+        stats.clear()

@@ -38,6 +38,7 @@
 typedef struct {
     uint32_t key[MT_N];
     int pos;
+    uint64_t drawn; /* words consumed since seeding */
 } ora_mt;
 
 /* np.random.seed(s) with an int seed: Knuth init_genrand */
@@ -48,6 +49,7 @@ void ora_mt_seed(ora_mt *st, uint32_t seed) {
         st->key[i] = 1812433253u * (p ^ (p >> 30)) + (uint32_t)i;
     }
     st->pos = MT_N;
+    st->drawn = 0;
 }
 
 static void mt_twist(ora_mt *st) {
@@ -63,6 +65,7 @@ static void mt_twist(ora_mt *st) {
 
 uint32_t ora_mt_next(ora_mt *st) {
     if (st->pos >= MT_N) mt_twist(st);
+    st->drawn++;
     uint32_t y = st->key[st->pos++];
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
@@ -338,3 +341,4 @@ int ora_env_step(int n, int m, int T, int L, double lambda, const double *table,
 }
 
 size_t ora_mt_sizeof(void) { return sizeof(ora_mt); }
+uint64_t ora_mt_drawn(const ora_mt *st) { return st->drawn; }

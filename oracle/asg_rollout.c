@@ -13,7 +13,7 @@
 #include <string.h>
 #include <time.h>
 
-typedef struct { uint32_t key[624]; int pos; } ora_mt;
+typedef struct { uint32_t key[624]; int pos; uint64_t drawn; } ora_mt;
 void ora_mt_seed(ora_mt *st, uint32_t seed);
 uint32_t ora_mt_next(ora_mt *st);
 int ora_env_construct_reset(ora_mt *st, int n, int m, int T, int L, int table_injected,

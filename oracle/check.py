@@ -1,0 +1,56 @@
+"""Parity checker: replays a GPU rollout on the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Given what the HIP env produced for E envs (the benefit table it used, its initial
+prev_assigns, the actions it stepped and the EpisodeBatch rows it wrote), re-run every
+env through OracleMockEnv (mock_constellation_env.py semantics) and compare:
+  integer fields (actions_onehot, avail_actions, filled, terminated, prev_assigns) exact,
+  float32 fields (obs, beta, rewards) exact against float32(oracle float64) -- the GPU
+  computes the same float64 expressions -- and float64 returns within 1e-9 relative.
+"""
+import numpy as np
+
+from . import oracle as ora
+
+
+def replay_and_compare(n, m, T, L, lam, table, prev0, td, returns, T_trans=None, quirks=(),
+                       rtol_reward=0.0, obs_atol=0.0):
+    """table [E,n,m,T] f64, prev0 [E,n] i64, td: dict of numpy arrays [E, T+1, ...] read
+    back from the GPU batch, returns [E] f64.  Raises AssertionError on any mismatch."""
+    E = table.shape[0]
+    for e in range(E):
+        env = ora.OracleMockEnv(n, m, T, L, lam, sat_prox_mat=table[e], T_trans=T_trans, mt=ora.MT(0))
+        env.reset()
+        env.prev_assigns[:] = prev0[e]
+        _cmp(td["obs"][e, 0], env._obs.astype(np.float32), f"env {e} obs row 0", obs_atol)
+        _cmp(td["beta"][e, 0], env.beta.astype(np.float32), f"env {e} beta row 0", obs_atol)
+        ret = 0.0
+        for t in range(T):
+            a = td["actions"][e, t].reshape(n).astype(np.int64)
+            r, done, _ = env.step(a)
+            ret += sum(r)
+            _cmp(td["rewards"][e, t], np.asarray(r).astype(np.float32), f"env {e} rewards t={t}",
+                 rtol=rtol_reward)
+            _cmp(td["obs"][e, t + 1], env._obs.astype(np.float32), f"env {e} obs t={t + 1}", obs_atol)
+            _cmp(td["beta"][e, t + 1], env.beta.astype(np.float32), f"env {e} beta t={t + 1}", obs_atol)
+            onehot = np.zeros((n, m), dtype=np.int64)
+            onehot[np.arange(n), a] = 1
+            if "actions_onehot" in td:
+                _cmp(td["actions_onehot"][e, t], onehot, f"env {e} onehot t={t}")
+            term = bool(done) if "parallel_terminated" not in quirks else (e != 0)
+            assert bool(td["terminated"][e, t, 0]) == term, f"env {e} terminated t={t}"
+            pa = np.zeros(n, np.int64) if "prev_assigns_zero" in quirks else a
+            _cmp(td["prev_assigns"][e, t + 1], pa, f"env {e} prev_assigns t={t + 1}")
+        assert td["avail_actions"][e].all(), f"env {e} avail_actions"
+        assert (td["filled"][e] == 1).all(), f"env {e} filled"
+        assert abs(returns[e] - ret) <= 1e-9 * max(1.0, abs(ret)), f"env {e} return {returns[e]} vs {ret}"
+
+
+def _cmp(got, want, what, atol=0.0, rtol=0.0):
+    got = np.asarray(got).reshape(np.asarray(want).shape)
+    if atol == 0.0 and rtol == 0.0:
+        if not np.array_equal(got, want):
+            bad = np.argwhere(got != want)
+            i = tuple(bad[0])
+            raise AssertionError(f"{what}: {len(bad)} mismatches, first at {i}: {got[i]!r} vs {want[i]!r}")
+    else:
+        np.testing.assert_allclose(got, want, rtol=rtol, atol=atol, err_msg=what)

@@ -43,6 +43,8 @@ def lib():
         L.ora_mt_uniform.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double]
         L.ora_mt_uniform.restype = ctypes.c_double
         L.ora_mt_permutation.argtypes = [ctypes.c_void_p, ctypes.c_int, _i64p]
+        L.ora_mt_drawn.argtypes = [ctypes.c_void_p]
+        L.ora_mt_drawn.restype = ctypes.c_uint64
         L.ora_mt_get_state.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
                                        ctypes.POINTER(ctypes.c_int)]
         L.ora_generate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -94,6 +96,10 @@ class MT:
         out = np.empty(m, dtype=np.int64)
         lib().ora_mt_permutation(self._buf, m, _p(out, _i64p))
         return out
+
+    def drawn(self):
+        """32-bit words consumed since seeding."""
+        return int(lib().ora_mt_drawn(self._buf))
 
     def state(self):
         key = (ctypes.c_uint32 * 624)()
