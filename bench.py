@@ -126,8 +126,7 @@ def main():
             if a.selector == "random":
                 env.random_actions(runner.batch, ts=t)
             else:
-                acts = mac.select_actions(runner.batch, t_ep=t, t_env=runner.t_env)
-                runner.batch.update({"actions": acts}, ts=t, mark_filled=False, preprocess=False)
+                runner.select_into_batch(t)
             if state["timing"]:
                 s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s0.record()

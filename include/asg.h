@@ -30,6 +30,8 @@
  *                              mock_constellation_env.py:122, action_selectors/sap_selectors.py:32,90,
  *                              action_selectors/non_rl_selectors.py:47
  *   asg_haa_select             HAASelector.select_action (action_selectors/non_rl_selectors.py:19-50)
+ *   asg_epsilon_greedy         EpsilonGreedyActionSelector.select_action
+ *                              (action_selectors/classic_selectors.py:28-54)
  *   asg_get_returns            the runners' episode_return accumulation
  *                              (episode_runner.py:84, parallel_runner.py:173-176)
  */
@@ -176,6 +178,17 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
                    const int64_t prev_strides[2], int64_t B, int n, int m,
                    const double *T_trans_dev, double lambda_, float *col_out,
                    int32_t *status_out, void *hip_stream);
+
+/* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
+ * per row, with probability epsilon a uniformly random available action, else the first
+ * maximal available Q (NaN propagates as in torch.max).  Randomness: Philox keyed by
+ * (seed, counter, row).  out [B][n] int64 (strided, e.g. the EpisodeBatch actions row);
+ * status [1] int32 device word set to ASG_E_INVALID_ARG if a row with no available action
+ * had to explore (torch's Categorical would raise).  May be NULL. */
+int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
+                       const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon,
+                       uint64_t seed, uint64_t counter, int64_t *out, const int64_t out_strides[2],
+                       int32_t *status, void *hip_stream);
 
 #ifdef __cplusplus
 }

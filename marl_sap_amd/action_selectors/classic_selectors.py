@@ -1,8 +1,11 @@
-"""Classic selectors (reference: action_selectors/classic_selectors.py:7-54), batched
-torch ops on the GPU."""
+"""Classic selectors (reference: action_selectors/classic_selectors.py:7-54) on the GPU.
+Epsilon-greedy is one fused HIP pass (asg_epsilon_greedy) over the Q-values."""
+import ctypes
+
 import torch
 from torch.distributions import Categorical
 
+from .. import _lib
 from ..components.epsilon_schedules import DecayThenFlatSchedule
 
 
@@ -25,26 +28,43 @@ class MultinomialActionSelector:
 
 class EpsilonGreedyActionSelector:
     """With prob. epsilon a uniformly random AVAILABLE action, else argmax over available
-    actions (first maximal index)."""
+    actions (first maximal index) -- one HIP kernel per call; `out` (an int64 [B, n] view,
+    e.g. the EpisodeBatch actions row) receives the actions in place."""
 
     def __init__(self, args):
         self.args = args
         self.schedule = DecayThenFlatSchedule(args.epsilon_start, args.epsilon_finish, args.epsilon_anneal_time,
                                               decay="linear")
         self.epsilon = self.schedule.eval(0)
+        self.seed = int(getattr(args, "seed", 0) or 0) * 0x9E3779B1 + torch.initial_seed()
+        self.calls = 0
+        self.status = None
 
-    def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None):
+    def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None, out=None):
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:
             self.epsilon = self.args.evaluation_epsilon
-        masked_q = agent_inputs.masked_fill(avail_actions == 0, -float("inf"))
-        greedy = masked_q.max(dim=2)[1]
-        if self.epsilon <= 0.0:
-            return greedy
-        pick_random = torch.rand_like(agent_inputs[:, :, 0]) < self.epsilon
-        B, n, m = agent_inputs.shape
-        random_actions = torch.multinomial(avail_actions.reshape(B * n, m).float(), 1).view(B, n)
-        return torch.where(pick_random, random_actions, greedy)
+        q = agent_inputs if agent_inputs.dtype == torch.float32 else agent_inputs.float()
+        B, n, m = q.shape
+        if out is None:
+            out = torch.empty((B, n), dtype=torch.int64, device=q.device)
+        av = avail_actions if avail_actions.dtype == torch.bool else avail_actions != 0
+        if self.status is None or self.status.device != q.device:
+            self.status = torch.zeros(1, dtype=torch.int32, device=q.device)
+        self.calls += 1
+        with torch.cuda.device(q.device):
+            _lib.check(_lib.lib().asg_epsilon_greedy(
+                ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), ctypes.c_void_p(av.data_ptr()),
+                _lib.i64arr(av.stride()), B, n, m, float(self.epsilon), self.seed & 0xFFFFFFFFFFFFFFFF, self.calls,
+                ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), ctypes.c_void_p(self.status.data_ptr()),
+                _lib.stream_ptr(q.device)))
+        return out
+
+    def flush(self):
+        """Raise (once per episode, from the runner) if a row had nothing to explore."""
+        if self.status is not None and int(self.status.item()) != 0:
+            self.status.zero_()
+            raise ValueError("epsilon-greedy exploration over a row with no available action")
 
 
 class SoftPoliciesSelector:

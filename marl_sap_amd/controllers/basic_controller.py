@@ -11,6 +11,14 @@ from ..action_selectors import REGISTRY as action_REGISTRY
 from ..modules.agents import REGISTRY as agent_REGISTRY
 
 
+def _accepts_out(selector):
+    import inspect
+    try:
+        return "out" in inspect.signature(selector.select_action).parameters
+    except (TypeError, ValueError):
+        return False
+
+
 class BasicMAC:
     def __init__(self, scheme, groups, args):
         self.n = args.n
@@ -21,11 +29,14 @@ class BasicMAC:
         self.action_selector = action_REGISTRY[args.action_selector](args)
         self.hidden_states = None
 
-    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False):
+    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False, out=None):
+        """`out` (optional, int64 [B, n]): selectors that support it write the actions
+        there in place (the runner passes the EpisodeBatch actions row)."""
         avail_actions = ep_batch["avail_actions"][:, t_ep]
         agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode, action_selection_mode=True)
+        kw = {"out": out} if out is not None and _accepts_out(self.action_selector) else {}
         return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env,
-                                                  test_mode=test_mode, beta=ep_batch["beta"][bs, t_ep])
+                                                  test_mode=test_mode, beta=ep_batch["beta"][bs, t_ep], **kw)
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

@@ -17,13 +17,13 @@ class JumpstartMAC(BasicMAC):
                                                             args.jumpstart_epsilon_anneal_time, decay="linear")
         self.jumpstart_epsilon = self.jumpstart_eps_schedule.eval(0)
 
-    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False):
+    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False, out=None):
         self.jumpstart_epsilon = self.jumpstart_eps_schedule.eval(t_env)
         if test_mode:
             self.jumpstart_epsilon = self.args.jumpstart_evaluation_epsilon
         if np.random.rand() < self.jumpstart_epsilon:
             return self.jumpstart_action_selector.select_action(ep_batch[bs, t_ep])
-        return super().select_actions(ep_batch, t_ep, t_env, bs=bs, test_mode=test_mode)
+        return super().select_actions(ep_batch, t_ep, t_env, bs=bs, test_mode=test_mode, out=out)
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

@@ -137,6 +137,9 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
         if ((e = hipMalloc(&st.table, sizeof(double) * E * T * n * m)) != hipSuccess) goto oom;
         if ((e = hipMemsetAsync(st.table, 0, sizeof(double) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
     }
+    if (st.bids) {
+        if ((e = hipMalloc(&st.assign, sizeof(int) * E * n)) != hipSuccess) goto oom;
+    }
     if (st.rng_mode == ASG_RNG_MT19937) {
         if ((e = hipMalloc(&st.mt, sizeof(uint32_t) * E * 625)) != hipSuccess) goto oom;
         if ((e = asg::launch_mt_seed(st, h->stream)) != hipSuccess) goto oom;
@@ -163,6 +166,7 @@ int asg_destroy(asg_handle *h) {
     (void)hipFree(const_cast<double *>(st.T_trans));
     (void)hipFree(st.table);
     (void)hipFree(st.mt);
+    (void)hipFree(st.assign);
     delete h;
     return ASG_OK;
 }
@@ -333,6 +337,21 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
     hipError_t e = asg::launch_haa_select(beta, beta_strides, prev, prev_strides, B, n, m, T_trans_dev, lambda_,
                                           col_out, status_out, static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_haa_select");
+}
+
+int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
+                       const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
+                       uint64_t counter, int64_t *out, const int64_t out_strides[2], int32_t *status,
+                       void *hip_stream) {
+    if (!q || !q_strides || !avail || !avail_strides || !out || !out_strides || B < 0 || n <= 0 || m <= 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_epsilon_greedy: bad arguments");
+    if (!(epsilon >= 0.0 && epsilon <= 1.0))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_epsilon_greedy: epsilon must be in [0, 1]");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_eps_greedy(q, q_strides, avail, avail_strides, B, n, m, (float)epsilon, seed,
+                                          (uint32_t)counter, out, out_strides, status,
+                                          static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_epsilon_greedy");
 }
 
 }  // extern "C"

@@ -61,31 +61,39 @@ __device__ __forceinline__ EnvKey env_key(uint64_t seed, int64_t global_env) {
                   (uint32_t)(seed >> 32) ^ (uint32_t)global_env};
 }
 
-// Bump parameters of one (agent i, task j) pair under Philox (the distribution of
-// generate_benefits_over_time, mock_constellation_env.py:281-293).
-struct Bump {
-    double scale;   // 0 when the pair is inactive
-    double center;
-    double s2;
+// Bump parameters of one (agent i, task j) pair under Philox, evaluated in float32
+// (the distribution of generate_benefits_over_time, mock_constellation_env.py:281-293):
+// active with probability 0.25 (rand() > 0.75), center ~ U(0, T), width ~ U(wmin, wmax),
+// sigma_2 = sqrt(w^2 / -8 / ln 0.05), value(t) = scale * exp(-(t - c)^2 / sigma_2 / 2).
+// One Philox call per pair; the per-task scale (choice([1,1,1,10])) is a per-task draw.
+struct Bump32 {
+    float scale;  // 0 when the pair is inactive
+    float center;
+    float a;      // 1 / (2 sigma_2)
 };
 
-__device__ __forceinline__ Bump philox_bump(EnvKey key, uint32_t episode, int i, int j, int m,
-                                            int T, double wmin, double wmax, bool dense) {
+__device__ __forceinline__ float philox_task_scale(EnvKey key, uint32_t episode, int j) {
     const u32x4 sc = philox4x32_10(u32x4{(uint32_t)j, 0u, kCtrScale, episode}, key.k0, key.k1);
-    const double scale = (sc.x & 3u) == 3u ? 10.0 : 1.0;  // choice([1, 1, 1, 10])
-    const uint32_t pair = (uint32_t)(i * m + j);
-    const u32x4 a = philox4x32_10(u32x4{pair, 0u, kCtrPair, episode}, key.k0, key.k1);
-    const bool active = dense || (u01_53(a.x, a.y) > 0.75);
-    Bump b;
-    b.scale = active ? scale : 0.0;
-    b.center = 0.0 + (double)T * u01_53(a.z, a.w);
-    const u32x4 s = philox4x32_10(u32x4{pair, 0u, kCtrSpread, episode}, key.k0, key.k1);
-    b.s2 = bump_s2(wmin + (wmax - wmin) * u01_53(s.x, s.y));
+    return (sc.x & 3u) == 3u ? 10.0f : 1.0f;
+}
+
+__device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale, int T,
+                                                float wmin, float wmax, bool dense) {
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair, 0u, kCtrPair, episode}, key.k0, key.k1);
+    constexpr float k2m32 = 2.3283064365386963e-10f;  // 2^-32
+    const bool active = dense || r.x >= 0xC0000000u;
+    Bump32 b;
+    b.scale = active ? scale : 0.0f;
+    b.center = (float)T * ((float)r.y * k2m32);
+    const float spread = wmin + (wmax - wmin) * ((float)r.z * k2m32);
+    const float s2 = sqrtf(spread * spread / -8.0f / (float)kLog005);
+    b.a = 0.5f / s2;
     return b;
 }
 
-__device__ __forceinline__ double bump_at(const Bump &b, int t) {
-    return b.scale == 0.0 ? 0.0 : bump_value(b.scale, b.center, b.s2, t);
+__device__ __forceinline__ float bump32_at(const Bump32 &b, int t) {
+    const float x = (float)t - b.center;
+    return b.scale * __expf(-(x * x) * b.a);
 }
 
 // ---------------------------------------------------------------------------------

@@ -17,68 +17,96 @@
 namespace asg {
 
 // ------------------------------------------------------------------------------------
-// benefit sources
+// benefit sources.  A source is bound to one env (`bind`) and yields per-pair evaluators.
 // ------------------------------------------------------------------------------------
-struct BumpSrc {
+struct BumpSrc {  // Philox, float32 bumps regenerated on the fly (no table in HBM)
     uint64_t seed;
     int64_t env_base;
     uint32_t episode;
     int n, m, T;
-    double wmin, wmax;
+    float wmin, wmax;
     bool dense;
 
-    struct Pair {
-        Bump b;
-        __device__ double at(int t) const { return bump_at(b, t); }
+    static constexpr bool kNeedsScale = true;
+    struct Env {
+        EnvKey key;
+        uint32_t episode;
+        int m, T;
+        float wmin, wmax;
+        bool dense;
+        const float *scale;  // LDS [m]
+        struct Pair {
+            Bump32 b;
+            __device__ float at(int t) const { return bump32_at(b, t); }
+        };
+        __device__ Pair pair(int i, int j) const {
+            return Pair{philox_bump32(key, episode, i * m + j, scale[j], T, wmin, wmax, dense)};
+        }
     };
-    __device__ Pair pair(int64_t e, int i, int j) const {
-        return Pair{philox_bump(env_key(seed, env_base + e), episode, i, j, m, T, wmin, wmax, dense)};
+    // fills scale[0..m) cooperatively (caller syncs)
+    __device__ void fill_scale(int64_t e, float *scale) const {
+        const EnvKey key = env_key(seed, env_base + e);
+        for (int j = threadIdx.x; j < m; j += blockDim.x) scale[j] = philox_task_scale(key, episode, j);
+    }
+    __device__ Env bind(int64_t e, const float *scale) const {
+        return Env{env_key(seed, env_base + e), episode, m, T, wmin, wmax, dense, scale};
     }
 };
 
-struct TableSrc {
-    const double *tab;  // [E][T][n][m]
+struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
+    const double *tab;
     int n, m, T;
 
-    struct Pair {
-        const double *p;  // &tab[e][0][i][j]
-        int64_t tstride;
-        __device__ double at(int t) const { return p[t * tstride]; }
+    static constexpr bool kNeedsScale = false;
+    struct Env {
+        const double *p;  // &tab[e][0][0][0]
+        int m;
+        int64_t nm;
+        struct Pair {
+            const double *p;
+            int64_t tstride;
+            __device__ double at(int t) const { return p[t * tstride]; }
+        };
+        __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, nm}; }
     };
-    __device__ Pair pair(int64_t e, int i, int j) const {
+    __device__ void fill_scale(int64_t, float *) const {}
+    __device__ Env bind(int64_t e, const float *) const {
         const int64_t nm = (int64_t)n * m;
-        return Pair{tab + e * (int64_t)T * nm + (int64_t)i * m + j, nm};
+        return Env{tab + e * (int64_t)T * nm, m, nm};
     }
 };
 
 // ------------------------------------------------------------------------------------
 // pre-transition row writer: obs = [onehot(assign) | B(k) .. B(k+L-1)] (zeros past T),
 // beta = B(k) (zeros when k >= T), avail_actions = 1; optionally actions_onehot of the
-// post-transition row `ts_onehot`.  VEC consecutive tasks per work item.
+// post-transition row `ts_onehot`.  VEC consecutive tasks per work item; every store of
+// a wave covers whole 128-B lines of one agent's rows.
 // ------------------------------------------------------------------------------------
-template <int VEC, class Src>
-__device__ void write_pre_row(const Src &src, const asg_batch_view &bv, int64_t e, int ts, int k,
-                              int n, int m, int T, int L, const int *s_assign, int ts_onehot) {
+template <int VEC, class EnvB>
+__device__ void write_pre_row(const EnvB &src, const asg_batch_view &bv, int64_t e, int ts, int k, int n, int m,
+                              int T, int L, const int *s_assign, int ts_onehot) {
     const int groups = m / VEC;
+    const int64_t os = bv.obs.stride[3];
     for (int idx = threadIdx.x; idx < n * groups; idx += blockDim.x) {
         const int i = idx / groups;
         const int j0 = (idx - i * groups) * VEC;
         const int a = s_assign ? s_assign[i] : -1;
         float oh[VEC];
+        typename EnvB::Pair P[VEC];
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
-        // benefits for lookahead blocks l = 0..L-1 at time k + l
-        typename Src::Pair P[VEC];
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) P[q] = src.pair(e, i, j0 + q);
+        for (int q = 0; q < VEC; ++q) {
+            oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
+            P[q] = src.pair(i, j0 + q);
+        }
         float *ob = fptr<float>(bv.obs, e, ts, i, j0);
-        const int64_t os = bv.obs.stride[3];
         if (VEC == 4) {
             *reinterpret_cast<float4 *>(ob) = make_float4(oh[0], oh[1], oh[2], oh[3]);
         } else {
             for (int q = 0; q < VEC; ++q) ob[q * os] = oh[q];
         }
         float b0[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) b0[q] = 0.0f;
         for (int l = 0; l < L; ++l) {
             const int t = k + l;
             float val[VEC];
@@ -95,9 +123,9 @@ __device__ void write_pre_row(const Src &src, const asg_batch_view &bv, int64_t 
                 for (int q = 0; q < VEC; ++q) o[q * os] = val[q];
             }
         }
-        if (L == 0) {
+        if (L == 0 && k < T) {
 #pragma unroll
-            for (int q = 0; q < VEC; ++q) b0[q] = (k < T) ? (float)P[q].at(k) : 0.0f;
+            for (int q = 0; q < VEC; ++q) b0[q] = (float)P[q].at(k);
         }
         if (bv.beta.ptr) {
             float *bp = fptr<float>(bv.beta, e, ts, i, j0);
@@ -118,10 +146,10 @@ __device__ void write_pre_row(const Src &src, const asg_batch_view &bv, int64_t 
         if (ts_onehot >= 0 && bv.actions_onehot.ptr) {
             int64_t *hp = fptr<int64_t>(bv.actions_onehot, e, ts_onehot, i, j0);
             if (VEC == 4) {
-                reinterpret_cast<longlong2 *>(hp)[0] = make_longlong2(oh[0] != 0.f, oh[1] != 0.f);
-                reinterpret_cast<longlong2 *>(hp)[1] = make_longlong2(oh[2] != 0.f, oh[3] != 0.f);
+                reinterpret_cast<longlong2 *>(hp)[0] = make_longlong2(a == j0, a == j0 + 1);
+                reinterpret_cast<longlong2 *>(hp)[1] = make_longlong2(a == j0 + 2, a == j0 + 3);
             } else {
-                for (int q = 0; q < VEC; ++q) hp[q * bv.actions_onehot.stride[3]] = (oh[q] != 0.f);
+                for (int q = 0; q < VEC; ++q) hp[q * bv.actions_onehot.stride[3]] = (a == j0 + q);
             }
         }
     }
@@ -136,9 +164,11 @@ __global__ void __launch_bounds__(256) reset_kernel(Src src, asg_batch_view bv, 
     extern __shared__ int s_dyn[];
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m;
+    int *perm = s_dyn;                                   // [m]
+    float *s_scale = reinterpret_cast<float *>(s_dyn + m);  // [m]
+    src.fill_scale(e, s_scale);
     if (philox_perm) {
         // Fisher-Yates from the top, Philox-drawn (distribution of choice(m, n, False))
-        int *perm = s_dyn;
         for (int j = threadIdx.x; j < m; j += blockDim.x) perm[j] = j;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -157,70 +187,81 @@ __global__ void __launch_bounds__(256) reset_kernel(Src src, asg_batch_view bv, 
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         if (bv.prev_assigns.ptr)
-            *fptr<int64_t>(bv.prev_assigns, e, ts, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : st.prev[e * n + i];
+            *fptr<int64_t>(bv.prev_assigns, e, ts, i, 0) =
+                (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : st.prev[e * n + i];
     }
     if (threadIdx.x == 0) {
         st.returns[e] = 0.0;
         if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts, 0, 0) = 1;
     }
-    write_pre_row<VEC>(src, bv, e, ts, 0, n, m, st.T, st.L, nullptr, -1);
+    write_pre_row<VEC>(src.bind(e, s_scale), bv, e, ts, 0, n, m, st.T, st.L, nullptr, -1);
+}
+
+// ------------------------------------------------------------------------------------
+// bids_as_actions: assignments = LSA(bids, maximize)[1]  (mock :121-122), one wave per
+// env, ahead of the step kernel; result in st.assign [E][n]
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) bids_assign_kernel(asg_batch_view bv, EnvState st, int ts) {
+    extern __shared__ double s_lsa[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m;
+    float *cost = reinterpret_cast<float *>(s_lsa);                                  // [n][m]
+    double *u = reinterpret_cast<double *>(cost + n * m + ((n * m) & 1));           // [n]
+    int *c4r = reinterpret_cast<int *>(u + n);                                      // [n]
+    int *r4c = c4r + n;                                                             // [m]
+    int *path = r4c + m;                                                            // [m]
+    const float *bids = fptr<float>(bv.actions, e, ts, 0, 0);
+    int status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, cost);
+    if (status == ASG_OK) {
+        LsaScratch sc{u, c4r, r4c, path};
+        const DenseCost<float> acc{cost, m};
+        if (m <= 64) status = lsa_solve_wave<1>(acc, n, m, sc);
+        else if (m <= 128) status = lsa_solve_wave<2>(acc, n, m, sc);
+        else if (m <= 256) status = lsa_solve_wave<4>(acc, n, m, sc);
+        else status = lsa_solve_wave<16>(acc, n, m, sc);
+    }
+    for (int i = threadIdx.x; i < n; i += kWave) st.assign[e * n + i] = status == ASG_OK ? c4r[i] : -1;
+    if (threadIdx.x == 0 && status != ASG_OK) atomicCAS(st.err, 0, status);
 }
 
 // ------------------------------------------------------------------------------------
 // step (mock_constellation_env.py:116-162 plus the runner's batch updates)
 // ------------------------------------------------------------------------------------
-template <int VEC, class Src>
+template <int VEC, class Src, bool BIDS>
 __global__ void __launch_bounds__(256) step_kernel(Src src, asg_batch_view bv, EnvState st, int ts, int k) {
     extern __shared__ int s_dyn[];
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m, T = st.T, L = st.L;
-    int *s_act = s_dyn;                                    // [n]
-    int *s_cnt = s_act + n;                                // [m]
-    double *s_rew = reinterpret_cast<double *>(s_cnt + m + ((n + m) & 1));  // [n], 8-aligned
+    int *s_act = s_dyn;                                                          // [n]
+    int *s_cnt = s_act + n;                                                      // [m]
+    float *s_scale = reinterpret_cast<float *>(s_cnt + m);                       // [m]
+    double *s_rew = reinterpret_cast<double *>(s_scale + m + ((n + 2 * m) & 1));  // [n], 8-aligned
     __shared__ int s_err;
 
     if (threadIdx.x == 0) s_err = 0;
     for (int j = threadIdx.x; j < m; j += blockDim.x) s_cnt[j] = 0;
+    src.fill_scale(e, s_scale);
     __syncthreads();
-    if (st.bids) {
-        // bids_as_actions: assignments = LSA(bids, maximize)[1]  (mock :121-122), wave 0
-        if (threadIdx.x < kWave) {
-            float *cost = reinterpret_cast<float *>(s_rew + n);          // [n][m]
-            double *u = reinterpret_cast<double *>(cost + n * m + ((n * m) & 1));
-            int *c4r = reinterpret_cast<int *>(u + n);
-            int *r4c = c4r + n;
-            int *path = r4c + m;
-            const float *bids = fptr<float>(bv.actions, e, ts, 0, 0);
-            int status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3],
-                                                      n, m, true, cost);
-            if (status == ASG_OK) {
-                LsaScratch sc{u, c4r, r4c, path};
-                const DenseCost<float> acc{cost, m};
-                if (m <= 64) status = lsa_solve_wave<1>(acc, n, m, sc);
-                else if (m <= 128) status = lsa_solve_wave<2>(acc, n, m, sc);
-                else if (m <= 256) status = lsa_solve_wave<4>(acc, n, m, sc);
-                else status = lsa_solve_wave<16>(acc, n, m, sc);
-            }
-            const int lane = threadIdx.x;
-            for (int i = lane; i < n; i += kWave) s_act[i] = status == ASG_OK ? c4r[i] : 0;
-            if (lane == 0 && status != ASG_OK) s_err = status;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int a;
+        if (BIDS) {
+            a = st.assign[e * n + i];
+        } else {
+            const int64_t a64 = *fptr<int64_t>(bv.actions, e, ts, i, 0);
+            a = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
+            if (a < 0) s_err = ASG_E_ACTION_RANGE;
         }
-    } else {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int64_t a = *fptr<int64_t>(bv.actions, e, ts, i, 0);
-            const bool ok = a >= 0 && a < m;
-            s_act[i] = ok ? (int)a : 0;
-            if (!ok) s_err = ASG_E_ACTION_RANGE;
-        }
+        a = a < 0 ? 0 : a;
+        s_act[i] = a;
+        atomicAdd(&s_cnt[a], 1);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&s_cnt[s_act[i]], 1);
-    __syncthreads();
+    const auto env = src.bind(e, s_scale);
     // rewards (mock :126-138): only the chosen task's beta_hat is needed per agent
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int j = s_act[i];
         const int p = st.prev[e * n + i];
-        const double beta = src.pair(e, i, j).at(k);
+        const double beta = (double)env.pair(i, j).at(k);
         const double tt = st.T_trans ? st.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
         const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
         const double bh = beta - st.lambda_ * pen;
@@ -231,16 +272,15 @@ __global__ void __launch_bounds__(256) step_kernel(Src src, asg_batch_view bv, E
         if (bv.prev_assigns.ptr)
             *fptr<int64_t>(bv.prev_assigns, e, ts + 1, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
     }
-    const bool done = k + 1 >= T;
     // next pre-transition row (mock :141-160) + this row's OneHot of the actions
-    write_pre_row<VEC>(src, bv, e, ts + 1, k + 1, n, m, T, L, s_act, st.bids ? -1 : ts);
+    write_pre_row<VEC>(env, bv, e, ts + 1, k + 1, n, m, T, L, s_act, BIDS ? -1 : ts);
     __syncthreads();
     if (threadIdx.x == 0) {
         // episode_return += sum(rewards): Python sums the float64 list left to right
         double s = 0.0;
         for (int i = 0; i < n; ++i) s += s_rew[i];
         st.returns[e] += s;
-        bool term = done;  // terminated = done != info.get("T", False)
+        bool term = k + 1 >= T;  // terminated = done != info.get("T", False)
         if (st.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
         if (bv.terminated.ptr) *fptr<uint8_t>(bv.terminated, e, ts, 0, 0) = term;
         if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts + 1, 0, 0) = 1;
@@ -265,12 +305,17 @@ __global__ void random_actions_kernel(asg_batch_view bv, EnvState st, int ts, in
 // ------------------------------------------------------------------------------------
 template <class Src>
 __global__ void export_table_kernel(Src src, EnvState st, double *out) {
+    extern __shared__ int s_dyn[];
+    float *s_scale = reinterpret_cast<float *>(s_dyn);
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m, T = st.T;
+    src.fill_scale(e, s_scale);
+    __syncthreads();
+    const auto env = src.bind(e, s_scale);
     for (int p = threadIdx.x; p < n * m; p += blockDim.x) {
         const int i = p / m, j = p - i * m;
-        const auto P = src.pair(e, i, j);
-        for (int t = 0; t < T; ++t) out[((e * n + i) * (int64_t)m + j) * T + t] = P.at(t);
+        const auto P = env.pair(i, j);
+        for (int t = 0; t < T; ++t) out[((e * n + i) * (int64_t)m + j) * T + t] = (double)P.at(t);
     }
 }
 
@@ -463,29 +508,37 @@ static bool vec4_ok(const asg_batch_view &b, int m) {
 }
 
 static size_t step_lds_bytes(const EnvState &st) {
-    size_t b = sizeof(int) * (st.n + st.m + ((st.n + st.m) & 1)) + sizeof(double) * st.n;
-    if (st.bids) {
-        b += sizeof(float) * ((size_t)st.n * st.m + ((st.n * st.m) & 1)) + sizeof(double) * st.n +
-             sizeof(int) * (st.n + 2 * st.m);
-    }
-    return b + 16;
+    return sizeof(int) * (st.n + 2 * st.m + 1) + sizeof(double) * st.n + 16;
+}
+
+template <class Src, bool BIDS>
+static void launch_step_t(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts, int k,
+                          hipStream_t s) {
+    const size_t lds = step_lds_bytes(st);
+    if (vec4_ok(bv, st.m))
+        hipLaunchKernelGGL((step_kernel<4, Src, BIDS>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
+    else
+        hipLaunchKernelGGL((step_kernel<1, Src, BIDS>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
 }
 
 template <class Src>
 static hipError_t launch_step_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts, int k,
                                   hipStream_t s) {
-    const size_t lds = step_lds_bytes(st);
-    if (vec4_ok(bv, st.m))
-        hipLaunchKernelGGL((step_kernel<4, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
-    else
-        hipLaunchKernelGGL((step_kernel<1, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
+    if (st.bids) {
+        const size_t lds = sizeof(float) * ((size_t)st.n * st.m + 1) + sizeof(double) * st.n +
+                           sizeof(int) * (st.n + 2 * st.m) + 32;
+        hipLaunchKernelGGL(bids_assign_kernel, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        launch_step_t<Src, true>(src, bv, st, ts, k, s);
+    } else {
+        launch_step_t<Src, false>(src, bv, st, ts, k, s);
+    }
     return hipGetLastError();
 }
 
 template <class Src>
 static hipError_t launch_reset_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts,
                                    bool philox_perm, hipStream_t s) {
-    const size_t lds = sizeof(int) * st.m + 16;
+    const size_t lds = sizeof(int) * 2 * st.m + 16;
     if (vec4_ok(bv, st.m))
         hipLaunchKernelGGL((reset_kernel<4, Src>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, philox_perm);
     else
@@ -494,7 +547,7 @@ static hipError_t launch_reset_src(const Src &src, const asg_batch_view &bv, con
 }
 
 static BumpSrc bump_src(const EnvState &st) {
-    return BumpSrc{st.seed, st.env_base, st.episode, st.n, st.m, st.T, st.wmin, st.wmax,
+    return BumpSrc{st.seed, st.env_base, st.episode, st.n, st.m, st.T, (float)st.wmin, (float)st.wmax,
                    st.benefit_mode == ASG_BENEFIT_DENSE};
 }
 static TableSrc table_src(const EnvState &st) { return TableSrc{st.table, st.n, st.m, st.T}; }
@@ -530,10 +583,11 @@ hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, i
 }
 
 hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s) {
+    const size_t lds = sizeof(float) * st.m + 16;
     if (uses_table(st))
-        hipLaunchKernelGGL((export_table_kernel<TableSrc>), dim3(st.E), dim3(256), 0, s, table_src(st), st, out);
+        hipLaunchKernelGGL((export_table_kernel<TableSrc>), dim3(st.E), dim3(256), lds, s, table_src(st), st, out);
     else
-        hipLaunchKernelGGL((export_table_kernel<BumpSrc>), dim3(st.E), dim3(256), 0, s, bump_src(st), st, out);
+        hipLaunchKernelGGL((export_table_kernel<BumpSrc>), dim3(st.E), dim3(256), lds, s, bump_src(st), st, out);
     return hipGetLastError();
 }
 

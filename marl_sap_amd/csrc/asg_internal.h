@@ -26,6 +26,7 @@ struct EnvState {
     double *returns;       // [E] float64 episode returns
     double *table;         // [E][T][n][m] float64 (MT19937 / injected modes)
     uint32_t *mt;          // [E][625] MT19937 key + pos (compat mode)
+    int *assign;           // [E][n] LSA assignments of the bids (bids_as_actions)
     int *err;              // sticky device error code
 };
 
@@ -47,5 +48,9 @@ hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], con
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s);
+
+hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t *avail, const int64_t as[3],
+                             int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter, int64_t *out,
+                             const int64_t os[2], int *err, hipStream_t s);
 
 }  // namespace asg

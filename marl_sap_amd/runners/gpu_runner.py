@@ -90,8 +90,7 @@ class GpuVecRunner:
         self.reset()
         self.mac.init_hidden(batch_size=self.batch_size)
         for t in range(self.T):
-            actions = self.mac.select_actions(self.batch, t_ep=t, t_env=self.t_env, test_mode=test_mode)
-            self.batch.update({"actions": actions}, ts=t, mark_filled=False, preprocess=False)
+            self.select_into_batch(t, test_mode)
             self.env.step(self.batch, ts=t)
         self.t = self.T
         if self.protocol == "parallel":
@@ -99,12 +98,22 @@ class GpuVecRunner:
             self.batch.update({"actions": actions}, ts=self.T, mark_filled=False)
         return self.batch
 
+    def select_into_batch(self, t, test_mode=False):
+        """mac.select_actions at t_ep = t, actions written into the batch row t (in place
+        when the selector supports `out`, else through EpisodeBatch.update)."""
+        row = self.batch["actions"][:, t, :, 0] if not self.env.bids_as_actions else None
+        actions = self.mac.select_actions(self.batch, t_ep=t, t_env=self.t_env, test_mode=test_mode, out=row)
+        if row is None or actions is not row:
+            self.batch.update({"actions": actions}, ts=t, mark_filled=False, preprocess=False)
+
     def finish_episode(self, test_mode=False):
         """Per-episode host sync: device errors, returns gather, counters, logging."""
         self.env.sync()
         for sel in (getattr(self.mac, "action_selector", None), getattr(self.mac, "jumpstart_action_selector", None)):
+            if hasattr(sel, "flush"):
+                sel.flush()
             st = getattr(sel, "status", None)
-            if st is not None:
+            if hasattr(st, "flush"):
                 st.flush()
         returns = asg_dist.all_gather_returns(self.env.get_returns())
         self.last_returns = returns

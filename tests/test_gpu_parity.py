@@ -346,3 +346,62 @@ def test_single_env_plugin_matches_golden(golden):
         assert d == d0
         pre = env.get_pretransition_data()
         np.testing.assert_array_equal(np.array(pre["obs"][0], np.float32), oe._obs.astype(np.float32))
+
+
+# ------------------------------------------------------------------------------ fused epsilon-greedy
+def _eg(eps, seed=0):
+    from types import SimpleNamespace
+
+    from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector
+    return EpsilonGreedyActionSelector(SimpleNamespace(epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
+                                                       evaluation_epsilon=0.0, seed=seed))
+
+
+@pytest.mark.parametrize("B,n,m", [(512, 64, 64), (64, 7, 10), (32, 5, 100), (16, 9, 200), (1, 1, 1)])
+def test_epsilon_greedy_greedy_matches_torch(B, n, m):
+    g = torch.Generator(device=DEV).manual_seed(B + n + m)
+    q = torch.randn((B, n, m), device=DEV, generator=g)
+    avail = torch.rand((B, n, m), device=DEV, generator=g) > 0.3
+    avail[..., 0] |= ~avail.any(-1)  # every row has an available action
+    q[0, 0, :] = 1.0                  # ties: first maximal available index
+    sel = _eg(0.0)
+    a = sel.select_action(q, avail, 0)
+    ref = q.masked_fill(~avail, -float("inf")).max(dim=2)[1]
+    assert torch.equal(a, ref)
+    if m > 1:
+        q[1, 0, m // 2] = float("nan")  # an available NaN propagates like torch.max
+        avail[1, 0, m // 2] = True
+        a = sel.select_action(q, avail, 0)
+        assert a[1, 0].item() == m // 2
+    sel.flush()
+
+
+def test_epsilon_greedy_exploration_distribution():
+    B, n, m = 4096, 16, 10
+    q = torch.randn((B, n, m), device=DEV)
+    avail = torch.ones((B, n, m), dtype=torch.bool, device=DEV)
+    avail[:, :, 7:] = False
+    sel = _eg(1.0)
+    a = sel.select_action(q, avail, 0)
+    counts = torch.bincount(a.flatten(), minlength=m).cpu().numpy()
+    assert counts[7:].sum() == 0
+    expect = B * n / 7
+    assert np.all(np.abs(counts[:7] - expect) < 5 * np.sqrt(expect))
+    greedy = q.masked_fill(~avail, -float("inf")).max(2)[1]
+    sel = _eg(0.3)
+    frac = (sel.select_action(q, avail, 0) != greedy).float().mean().item()
+    assert abs(frac - 0.3 * 6 / 7) < 0.01
+    sel.flush()
+
+
+def test_epsilon_greedy_writes_batch_row_in_place():
+    E, n, m, T = 8, 6, 8, 4
+    env = AssignEnvBatch(n, m, T, 2, 0.5, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    q = torch.randn((E, n, m), device=DEV)
+    row = b["actions"][:, 1, :, 0]
+    out = _eg(0.0).select_action(q, b["avail_actions"][:, 0], 0, out=row)
+    assert out is row
+    assert torch.equal(b["actions"][:, 1, :, 0], q.max(2)[1])
+    assert (b["actions"][:, 0] == 0).all() and (b["actions"][:, 2:] == 0).all()
