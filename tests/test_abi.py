@@ -1,0 +1,79 @@
+"""The C-ABI library loads and exports every symbol include/asg.h declares; ctypes
+struct layouts match the C header; argument validation works without a GPU (no compute
+calls are made here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "asg.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(asg_\w+)\s*\(", src, re.M)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from marl_sap_amd import build, _lib
+    build.build()
+    return _lib.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    from marl_sap_amd import _lib
+    names = _declared()
+    assert len(names) >= 19
+    assert sorted(_lib.EXPORTS) == names
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}$", nm, re.M), n
+    assert L.asg_abi_version() == 1
+
+
+def test_struct_layout_matches_header(tmp_path):
+    from marl_sap_amd import _lib
+    c = tmp_path / "layout.c"
+    c.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "asg.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu\\n",'
+                 'sizeof(asg_field), sizeof(asg_batch_view), sizeof(asg_config), offsetof(asg_config, seed),'
+                 'offsetof(asg_config, T_trans), offsetof(asg_batch_view, filled));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(_lib.AsgField), ctypes.sizeof(_lib.AsgBatchView), ctypes.sizeof(_lib.AsgConfig),
+            _lib.AsgConfig.seed.offset, _lib.AsgConfig.T_trans.offset, _lib.AsgBatchView.filled.offset]
+    assert got == want
+
+
+def test_create_validates_without_gpu(L):
+    from marl_sap_amd import _lib
+    cfg = _lib.AsgConfig(num_envs=4, n=8, m=4, T=5, L=1, lambda_=0.5)
+    h = ctypes.c_void_p()
+    rc = L.asg_create(ctypes.byref(cfg), 0, None, ctypes.byref(h))
+    assert rc == _lib.ASG_E_INVALID_ARG and not h.value
+    assert "larger sample" in _lib.last_error()
+    with pytest.raises(ValueError, match="larger sample"):
+        _lib.check(rc)
+    cfg = _lib.AsgConfig(num_envs=0, n=4, m=4, T=5, L=1)
+    assert L.asg_create(ctypes.byref(cfg), 0, None, ctypes.byref(h)) == _lib.ASG_E_INVALID_ARG
+    cfg = _lib.AsgConfig(num_envs=1, n=4, m=4, T=5, L=1, rng_mode=1, benefit_mode=1)
+    assert L.asg_create(ctypes.byref(cfg), 0, None, ctypes.byref(h)) == _lib.ASG_E_INVALID_ARG
+    assert "dense" in _lib.last_error()
+
+
+def test_kernel_entry_points_validate_without_gpu(L):
+    from marl_sap_amd import _lib
+    st = _lib.i64arr([16, 4, 1])
+    assert L.asg_lsa_batched(None, 5, st, 1, 4, 4, 0, None, None, None, None) == _lib.ASG_E_INVALID_ARG
+    assert L.asg_lsa_batched(None, 0, st, 1, 2000, 4, 0, None, None, None, None) == _lib.ASG_E_INVALID_ARG
+    assert L.asg_lsa_batched(None, 0, st, 0, 4, 4, 0, None, None, None, None) == _lib.ASG_OK  # empty batch
+    assert L.asg_haa_select(None, st, None, st, 1, 4, 4, None, 0.5, None, None, None) == _lib.ASG_E_INVALID_ARG
+    assert L.asg_epsilon_greedy(None, st, None, st, 1, 4, 4, 0.1, 0, 0, None, st, None, None) == \
+        _lib.ASG_E_INVALID_ARG
+    assert L.asg_reset(None, None, 0) == _lib.ASG_E_INVALID_ARG
+    assert L.asg_step(None, None, 0) == _lib.ASG_E_INVALID_ARG

@@ -1,0 +1,106 @@
+"""Host-side mirror of the reference interfaces (CPU): EpisodeBatch layout/semantics
+against the reference's own batch dumps, time-major storage equivalence, ReplayBuffer,
+schedules, OneHot, scheme -- and the CPU-baseline port against the golden vectors."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from marl_sap_amd.components import DecayThenFlatSchedule, EpisodeBatch, OneHot, ReplayBuffer
+from marl_sap_amd.envs.assign_env import make_scheme
+
+
+def _batch(n, m, T, L=3, B=2, time_major=False, bids=False):
+    scheme, pre = make_scheme(n, m, L, bids)
+    return EpisodeBatch(scheme, {"agents": n}, B, T + 1, preprocess=pre, device="cpu", time_major=time_major)
+
+
+def test_layout_matches_reference_dump(golden):
+    g = golden("runner_dumps")
+    for tag in ["ep_eg_4", "par_sap_8"]:
+        n, m, T, B = [int(x) for x in g[f"{tag}__cfg"][:4]]
+        b = _batch(n, m, T, B=B)
+        for k, v in b.data.transition_data.items():
+            ref = g[f"{tag}__{k}"]
+            assert tuple(v.shape) == ref.shape, k
+            assert str(v.dtype).replace("torch.", "") == str(ref.dtype), k
+
+
+@pytest.mark.parametrize("time_major", [False, True])
+def test_update_and_slicing_semantics(time_major):
+    n, m, T = 3, 4, 5
+    b = _batch(n, m, T, B=3, time_major=time_major)
+    obs = np.arange(3 * n * 4 * m, dtype=np.float64).reshape(3, n, 4 * m)
+    b.update({"obs": list(obs), "beta": [np.ones((n, m))] * 3}, ts=2)
+    assert (b["filled"][:, 2] == 1).all() and b["filled"].sum() == 3
+    np.testing.assert_array_equal(b["obs"][:, 2].numpy(), obs.astype(np.float32))
+    b.update({"actions": torch.tensor([[0, 1, 3]] * 3)}, ts=2, mark_filled=False)
+    assert b["actions_onehot"].dtype == torch.int64
+    assert b["actions_onehot"][0, 2].tolist() == [[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]]
+    b.update({"actions": torch.tensor([[2, 2, 2]])}, bs=[1], ts=3, mark_filled=False)
+    assert b["actions"][1, 3, :, 0].tolist() == [2, 2, 2] and b["actions"][0, 3].sum() == 0
+    sub = b[1:3, 2:4]
+    assert sub.batch_size == 2 and sub.max_seq_length == 2 and sub["obs"].shape == (2, 2, n, 4 * m)
+    with pytest.raises(ValueError):
+        b.update({"obs": [np.zeros((n + 1, 4 * m))] * 3}, ts=0)
+    with pytest.raises(KeyError):
+        b.update({"nope": [0]}, ts=0)
+    if time_major:  # one time step of all envs is one contiguous slab
+        assert b["obs"][:, 2].is_contiguous()
+
+
+def test_replay_buffer_ring():
+    n, m, T = 2, 3, 2
+    scheme, pre = make_scheme(n, m, 1)
+    rb = ReplayBuffer(scheme, {"agents": n}, 5, T + 1, preprocess=pre)
+    for ep in range(4):
+        b = EpisodeBatch(scheme, {"agents": n}, 2, T + 1, preprocess=pre, time_major=True)
+        b.update({"actions": torch.full((2, n), ep % m)}, ts=0)
+        rb.insert_episode_batch(b)
+    assert rb.episodes_in_buffer == 5 and rb.buffer_index == 3
+    assert rb.can_sample(5) and not rb.can_sample(6)
+    assert rb["actions"][:, 0, 0, 0].tolist() == [2, 3 % m, 3 % m, 1, 2]
+    s = rb.sample(3, rng=np.random.RandomState(0))
+    assert s.batch_size == 3
+
+
+def test_schedule_onehot_scheme():
+    s = DecayThenFlatSchedule(1.0, 0.05, 100, decay="linear")
+    assert s.eval(0) == 1.0 and abs(s.eval(50) - 0.525) < 1e-12 and s.eval(1000) == 0.05
+    oh = OneHot(5)
+    assert oh.infer_output_info((1,), torch.int64) == ((5,), torch.int64)
+    assert oh.transform(torch.tensor([[3], [0]])).tolist() == [[0, 0, 0, 1, 0], [1, 0, 0, 0, 0]]
+    scheme, pre = make_scheme(4, 6, 3, bids_as_actions=True)
+    assert scheme["actions"]["vshape"] == (6,) and pre == {}
+    scheme, pre = make_scheme(4, 6, 3)
+    assert scheme["obs"]["vshape"] == 24 and scheme["beta"]["part_of_state"]
+
+
+def test_cpu_baseline_port_matches_golden(golden):
+    """The timed CPU baseline (oracle/cpu_parallel_runner.py) is the reference algorithm."""
+    from oracle.cpu_parallel_runner import NumpyMockEnv
+    g = golden("mock_reset")
+    for c in (0, 5, 9):
+        n, m, T, L, s = [int(x) for x in g[f"c{c}_shape"]]
+        np.random.seed(s)
+        env = NumpyMockEnv(n, m, T, L, 0.5)
+        env.reset()
+        np.testing.assert_array_equal(env.sat_prox_mat, g[f"c{c}_table"])
+        np.testing.assert_array_equal(env.prev_assigns, g[f"c{c}_prev_assigns"])
+    st = golden("mock_step")
+    c = 2
+    n, m, T, L = [int(x) for x in st[f"c{c}_spec"]]
+    env = NumpyMockEnv(n, m, T, L, float(st[f"c{c}_lambda"]))
+    env.sat_prox_mat = st[f"c{c}_table"]
+    env.k, env.curr_assignment = 0, np.zeros((n, m))
+    env.beta, env.prev_assigns = env.sat_prox_mat[:, :, 0], st[f"c{c}_prev0"]
+    for t in range(T):
+        r, d, _ = env.step(list(st[f"c{c}_actions"][t]))
+        np.testing.assert_array_equal(np.array(r), st[f"c{c}_rewards"][t])
+
+
+def test_cpu_baseline_runs():
+    from oracle.cpu_parallel_runner import run_parallel_baseline
+    rate, steps, secs = run_parallel_baseline(n=4, m=4, T=3, L=1, workers=2, episodes=1)
+    assert steps == 6 and rate > 0
