@@ -178,7 +178,7 @@ def main():
             "metric": "env steps/sec (whole node), 64-agent assignment env, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (Philox bump benefits, random-init RNN agent)",
             "config": {"workload": f"{a.n}-agent/{a.m}-task assignment env, {E} envs per GPU, T={a.T}, L={a.L}, "
                                    f"BasicMAC+RNN(GRU 64, fp32) + {args.action_selector if a.selector != 'random' else 'random'} "
