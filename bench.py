@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--benefits", default="bump", choices=["bump", "dense"])
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-episodes", type=int, default=3)
+    p.add_argument("--agent", default="rnn_fused", choices=["rnn_fused", "rnn"],
+                   help="rnn_fused: the same RNNAgent (weights, fp32) with its inference forward as one HIP kernel")
     p.add_argument("--seed", type=int, default=0)
     return p.parse_args()
 
@@ -67,8 +69,8 @@ def make_args(a, E):
         env_args=dict(n=a.n, m=a.m, T=a.T, L=a.L, lambda_=0.5, bids_as_actions=False, seed=a.seed,
                       benefits=a.benefits),
         env_rng="philox", env_quirks=(), runner_protocol="episode", test_nepisode=1,
-        runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, agent="rnn", hidden_dim=64, use_rnn=True,
-        obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
+        runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, hidden_dim=64, use_rnn=True,
+        obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel, agent=a.agent,
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac")
 
 
@@ -181,7 +183,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (Philox bump benefits, random-init RNN agent)",
             "config": {"workload": f"{a.n}-agent/{a.m}-task assignment env, {E} envs per GPU, T={a.T}, L={a.L}, "
-                                   f"BasicMAC+RNN(GRU 64, fp32) + {args.action_selector if a.selector != 'random' else 'random'} "
+                                   f"BasicMAC+{a.agent}(GRU 64, fp32) + {args.action_selector if a.selector != 'random' else 'random'} "
                                    f"selector, {a.benefits} benefits",
                        "envs_per_gpu": E, "global_envs": world * E, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
                        "parallelism": f"env-sharded x{world} (RCCL gather of returns per episode)"},

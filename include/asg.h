@@ -32,6 +32,8 @@
  *   asg_haa_select             HAASelector.select_action (action_selectors/non_rl_selectors.py:19-50)
  *   asg_epsilon_greedy         EpsilonGreedyActionSelector.select_action
  *                              (action_selectors/classic_selectors.py:28-54)
+ *   asg_rnn_agent_forward      RNNAgent.forward (modules/agents/rnn_agent.py:23-31) as called by
+ *                              BasicMAC.forward for action selection (basic_controller.py:26-48)
  *   asg_get_returns            the runners' episode_return accumulation
  *                              (episode_runner.py:84, parallel_runner.py:173-176)
  */
@@ -189,6 +191,20 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon,
                        uint64_t seed, uint64_t counter, int64_t *out, const int64_t out_strides[2],
                        int32_t *status, void *hip_stream);
+
+/* RNNAgent forward (inference) for R agent rows in one fused f32-MFMA kernel:
+ *   x = relu(X W1^T + b1); GRUCell(x, h) (use_rnn) or relu(x W_ih^T + b_ih); q = h' W2^T + b2.
+ * X [R][K] f32 (row stride x_stride, K % 4 == 0, 16-B aligned rows); h_in [R][hidden] with
+ * row stride h_stride (0 = one row broadcast to all, NULL = zeros); weights in torch
+ * nn.Linear / nn.GRUCell layouts (W1 [hidden][K], W_ih / W_hh [3*hidden][hidden] or
+ * W_ih = W_rnn [hidden][hidden] with W_hh = NULL when use_rnn = 0, W2 [n_out][hidden]),
+ * contiguous.  Outputs h_out [R][hidden], q_out [R][n_out], contiguous.  hidden must be
+ * 64, n_out one of 16, 32, 48, 64. */
+int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,
+                          int64_t h_stride, const float *W1, const float *b1, const float *W_ih,
+                          const float *b_ih, const float *W_hh, const float *b_hh, const float *W2,
+                          const float *b2, int hidden, int n_out, int use_rnn, float *h_out,
+                          float *q_out, void *hip_stream);
 
 #ifdef __cplusplus
 }

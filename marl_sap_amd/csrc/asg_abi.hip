@@ -94,6 +94,8 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
         return fail(nullptr, ASG_E_INVALID_ARG, "unknown rng_mode");
     if (cfg->benefit_mode < ASG_BENEFIT_BUMP || cfg->benefit_mode > ASG_BENEFIT_INJECTED)
         return fail(nullptr, ASG_E_INVALID_ARG, "unknown benefit_mode");
+    if (cfg->bids_as_actions && (int64_t)cfg->n * cfg->m > 16384)
+        return fail(nullptr, ASG_E_INVALID_ARG, "bids_as_actions supports n * m <= 16384 (the bid matrix is solved in LDS)");
     if (cfg->rng_mode == ASG_RNG_MT19937 && cfg->benefit_mode == ASG_BENEFIT_DENSE)
         return fail(nullptr, ASG_E_INVALID_ARG, "dense benefits are a Philox-mode workload");
     asg_handle *h = new (std::nothrow) asg_handle();
@@ -352,6 +354,25 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
                                           (uint32_t)counter, out, out_strides, status,
                                           static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_epsilon_greedy");
+}
+
+int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in, int64_t h_stride,
+                          const float *W1, const float *b1, const float *W_ih, const float *b_ih, const float *W_hh,
+                          const float *b_hh, const float *W2, const float *b2, int hidden, int n_out, int use_rnn,
+                          float *h_out, float *q_out, void *hip_stream) {
+    if (!x || !W1 || !b1 || !W_ih || !b_ih || !W2 || !b2 || !h_out || !q_out || R < 0 || K <= 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: bad arguments");
+    if (use_rnn && (!W_hh || !b_hh))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: GRU weights missing");
+    if (hidden != 64 || n_out <= 0 || n_out > 64 || n_out % 16 != 0 || K % 4 != 0 || x_stride % 4 != 0 || h_stride % 4 != 0 ||
+        (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
+        return fail(nullptr, ASG_E_INVALID_ARG,
+                    "asg_rnn_agent_forward: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0 and 16-B aligned rows");
+    if (R == 0) return ASG_OK;
+    hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, W1, b1, W_ih, b_ih, W_hh, b_hh, W2,
+                                             b2, n_out, use_rnn, h_out, q_out,
+                                             static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_forward");
 }
 
 }  // extern "C"

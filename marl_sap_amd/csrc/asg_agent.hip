@@ -1,0 +1,266 @@
+// asg_agent.hip -- fused RNNAgent forward for action selection (gfx950, f32 MFMA).
+//
+// RNNAgent.forward (modules/agents/rnn_agent.py:23-31) over all B*n agent rows of one
+// env step, in ONE pass over the observation slab:
+//     x  = relu(obs @ W1^T + b1)
+//     gi = x @ W_ih^T + b_ih ; gh = h @ W_hh^T + b_hh            (use_rnn: GRUCell)
+//     r = sigmoid(gi_r + gh_r); z = sigmoid(gi_z + gh_z); n = tanh(gi_n + r * gh_n)
+//     h' = n + z * (h - n)
+//   or h' = relu(x @ W_rnn^T + b_rnn)                             (use_rnn = False)
+//     q  = h' @ W2^T + b2
+// The PyTorch path runs this as 4 hipBLASLt GEMMs plus the GRU cell's elementwise kernel
+// (which also writes a 5*hidden backward workspace per row): ~6 GB of HBM traffic per
+// step at 64 agents x 16,384 envs.  Here every intermediate stays in registers / LDS:
+// HBM sees the observation rows once, h in, h' and q out.
+//
+// Arithmetic: v_mfma_f32_16x16x4_f32 -- exact fp32 products, fp32 accumulation (a k-ordered
+// fmaf chain), i.e. fp32 like the reference; only the summation order differs from
+// hipBLASLt's.  One wave owns 32 rows (2 row tiles of 16); the K dimension is walked in
+// chunks of 16 so each lane loads 4 consecutive k values as one float4 (the MFMA k slots
+// of step e map to k = 16t + 4q + e, identically for A and B).
+#include "asg_device.h"
+#include "asg_internal.h"
+
+namespace asg {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRowsPerWave = 32;
+constexpr int kHid = 64;          // hidden_dim
+constexpr int kLdsStride = kHid + 4;  // padded row (floats) of the LDS row tiles
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 ldg4(const float *p, bool ok) {
+    return ok ? *reinterpret_cast<const float4 *>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float comp(const float4 &v, int e) {
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// acc[rt][ct] += A(rows of `a_src`, k) * W^T(k, cols 16*ct0 .. 16*(ct0+NCT)-1) over K,
+// A rows come from a row-major [32][lda] LDS tile; W is row-major [cols][K] in global.
+template <int NCT>
+__device__ __forceinline__ void gemm_lds_a(f32x4 (&acc)[2][NCT], const float *a_lds, int lda, const float *W,
+                                           int ldw, int col0, int K) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    for (int t = 0; t < K / 16; ++t) {
+        float4 a4[2], b4[NCT];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+            a4[rt] = *reinterpret_cast<const float4 *>(a_lds + (16 * rt + r) * lda + 16 * t + 4 * q);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+            b4[ct] = *reinterpret_cast<const float4 *>(W + (int64_t)(col0 + 16 * ct + r) * ldw + 16 * t + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) acc[rt][ct] = mfma4(comp(a4[rt], e), comp(b4[ct], e), acc[rt][ct]);
+    }
+}
+
+constexpr int kStageStride = 16 + 4;  // padded row (floats) of the per-block h' stage
+constexpr int kWaveLds = 2 * kRowsPerWave * kLdsStride + kRowsPerWave * kStageStride;  // floats
+
+// NQ = n_out / 16 output tiles of fc2 (n_out <= 64); fc2 is accumulated block by block as
+// each 16-unit block of h' is produced, so h' never needs a full LDS tile.
+template <bool RNN, int NQ>
+__global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
+    const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
+    const float *__restrict__ W1, const float *__restrict__ b1, const float *__restrict__ Wih,
+    const float *__restrict__ bih, const float *__restrict__ Whh, const float *__restrict__ bhh,
+    const float *__restrict__ W2, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q) {
+    extern __shared__ float s_agent[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    float *sx = s_agent + wave * kWaveLds;                 // x = relu(fc1), [32][kLdsStride]
+    float *sh = sx + kRowsPerWave * kLdsStride;            // h_in, [32][kLdsStride]
+    float *sp = sh + kRowsPerWave * kLdsStride;            // h' block stage, [32][kStageStride]
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * kRowsPerWave;
+    if (row0 >= R) return;  // whole wave idle (no block-level barrier below)
+    constexpr int nout = 16 * NQ;
+
+    // ---- h_in -> LDS (row-major, padded) -------------------------------------------
+    for (int idx = lane; idx < kRowsPerWave * kHid / 4; idx += 64) {
+        const int rr = idx / (kHid / 4), c4 = (idx % (kHid / 4)) * 4;
+        const int64_t row = row0 + rr;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (RNN && Hin && row < R) v = *reinterpret_cast<const float4 *>(Hin + row * hs + c4);
+        *reinterpret_cast<float4 *>(sh + rr * kLdsStride + c4) = v;
+    }
+
+    // ---- fc1: x = relu(X W1^T + b1), X rows streamed from HBM ------------------------
+    {
+        f32x4 acc[2][4];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int64_t ra = row0 + r, rb = row0 + 16 + r;
+        const bool oka = ra < R, okb = rb < R;
+        const float *xa = X + (oka ? ra : 0) * xs, *xb = X + (okb ? rb : 0) * xs;
+        const int nt = (K + 15) / 16;
+        float4 a_nxt[2], b_nxt[4];
+        auto load = [&](int t, float4 (&a4)[2], float4 (&b4)[4]) {
+            const int k = 16 * t + 4 * q;
+            const bool okk = k < K;  // K % 4 == 0 (checked on the host)
+            a4[0] = ldg4(xa + k, oka && okk);
+            a4[1] = ldg4(xb + k, okb && okk);
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) b4[ct] = ldg4(W1 + (int64_t)(16 * ct + r) * K + k, okk);
+        };
+        load(0, a_nxt, b_nxt);
+        for (int t = 0; t < nt; ++t) {
+            float4 a4[2] = {a_nxt[0], a_nxt[1]};
+            float4 b4[4] = {b_nxt[0], b_nxt[1], b_nxt[2], b_nxt[3]};
+            if (t + 1 < nt) load(t + 1, a_nxt, b_nxt);  // prefetch the next chunk under the MFMAs
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int ct = 0; ct < 4; ++ct)
+                        acc[rt][ct] = mfma4(comp(a4[rt], e), comp(b4[ct], e), acc[rt][ct]);
+        }
+        // epilogue: C layout (col = lane & 15, row = 4 * (lane >> 4) + v)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) {
+                const int col = 16 * ct + r;
+                const float bb = b1[col];
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    sx[(16 * rt + 4 * q + v) * kLdsStride + col] = fmaxf(acc[rt][ct][v] + bb, 0.f);
+            }
+    }
+    wave_sync();
+
+    // ---- recurrent layer, one 16-unit block of h' at a time; fc2 accumulated per block -------
+    f32x4 aq[2][NQ];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) aq[rt][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int hb = 0; hb < 4; ++hb) {
+        const int u = 16 * hb + r;
+        f32x4 hp[2];
+        if (RNN) {
+            f32x4 gi[2][3], gh[2][3];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int g = 0; g < 3; ++g) gi[rt][g] = gh[rt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < kHid / 16; ++t) {
+                float4 ax[2], ah[2], bi[3], bh[3];
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt) {
+                    ax[rt] = *reinterpret_cast<const float4 *>(sx + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
+                    ah[rt] = *reinterpret_cast<const float4 *>(sh + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
+                }
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    const int64_t wrow = g * kHid + u;
+                    bi[g] = *reinterpret_cast<const float4 *>(Wih + wrow * kHid + 16 * t + 4 * q);
+                    bh[g] = *reinterpret_cast<const float4 *>(Whh + wrow * kHid + 16 * t + 4 * q);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int g = 0; g < 3; ++g) {
+                            gi[rt][g] = mfma4(comp(ax[rt], e), comp(bi[g], e), gi[rt][g]);
+                            gh[rt][g] = mfma4(comp(ah[rt], e), comp(bh[g], e), gh[rt][g]);
+                        }
+            }
+            const float bir = bih[u], biz = bih[kHid + u], bin = bih[2 * kHid + u];
+            const float bhr = bhh[u], bhz = bhh[kHid + u], bhn = bhh[2 * kHid + u];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float h = sh[(16 * rt + 4 * q + v) * kLdsStride + u];
+                    const float rg = sigmoidf_((gi[rt][0][v] + bir) + (gh[rt][0][v] + bhr));
+                    const float zg = sigmoidf_((gi[rt][1][v] + biz) + (gh[rt][1][v] + bhz));
+                    const float ng = tanhf((gi[rt][2][v] + bin) + rg * (gh[rt][2][v] + bhn));
+                    hp[rt][v] = ng + zg * (h - ng);
+                }
+        } else {
+            f32x4 a2[2][1];
+            a2[0][0] = a2[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            gemm_lds_a<1>(a2, sx, kLdsStride, Wih, kHid, 16 * hb, kHid);
+            const float bb = bih[u];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) hp[rt][v] = fmaxf(a2[rt][0][v] + bb, 0.f);
+        }
+        // h' block: to HBM (hidden-state output) and to the LDS stage as fc2's A operand
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int rr = 16 * rt + 4 * q + v;
+                sp[rr * kStageStride + r] = hp[rt][v];
+                if (row0 + rr < R) Hout[(row0 + rr) * kHid + u] = hp[rt][v];
+            }
+        wave_sync();
+        // q += h'[:, block] W2[:, block]^T   (K = 16: one chunk)
+        {
+            float4 a4[2], b4[NQ];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+                a4[rt] = *reinterpret_cast<const float4 *>(sp + (16 * rt + r) * kStageStride + 4 * q);
+#pragma unroll
+            for (int c = 0; c < NQ; ++c)
+                b4[c] = *reinterpret_cast<const float4 *>(W2 + (int64_t)(16 * c + r) * kHid + 16 * hb + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int c = 0; c < NQ; ++c) aq[rt][c] = mfma4(comp(a4[rt], e), comp(b4[c], e), aq[rt][c]);
+        }
+        wave_sync();  // the stage is rewritten by the next block
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            const int col = 16 * c + r;
+            const float bb = b2[col];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int64_t row = row0 + 16 * rt + 4 * q + v;
+                if (row < R) Q[row * nout + col] = aq[rt][c][v] + bb;
+            }
+        }
+}
+
+hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
+                                const float *W1, const float *b1, const float *Wih, const float *bih,
+                                const float *Whh, const float *bhh, const float *W2, const float *b2, int nout,
+                                int use_rnn, float *Hout, float *Q, hipStream_t s) {
+    const int64_t rows_per_block = 4 * kRowsPerWave;
+    const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
+    const size_t lds = sizeof(float) * 4 * kWaveLds;
+#define L_(RNN, NQ)                                                                                             \
+    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, W1, \
+                       b1, Wih, bih, Whh, bhh, W2, b2, Hout, Q)
+    const int nq = nout / 16;
+    if (use_rnn) {
+        if (nq == 1) L_(true, 1); else if (nq == 2) L_(true, 2); else if (nq == 3) L_(true, 3); else L_(true, 4);
+    } else {
+        if (nq == 1) L_(false, 1); else if (nq == 2) L_(false, 2); else if (nq == 3) L_(false, 3); else L_(false, 4);
+    }
+#undef L_
+    return hipGetLastError();
+}
+
+}  // namespace asg

@@ -97,30 +97,100 @@ __device__ __forceinline__ float bump32_at(const Bump32 &b, int t) {
 }
 
 // ---------------------------------------------------------------------------------
-// wave64 reductions (ds_swizzle/DPP via __shfl_xor)
+// wave64 butterflies on the VALU: DPP inside 16-lane rows (quad xor 1, quad xor 2,
+// half-row mirror, row mirror), then v_permlane16_swap / v_permlane32_swap across rows
+// (gfx950).  Every lane ends with the full reduction.  Call in wave-uniform control flow.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_min_f64(double v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o, kWave));
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+// v_permlane{16,32}_swap with both operands = x: element 0 / element 1 of the result
+// hold this lane's and the partner lane's value (lane ^ 16 / lane ^ 32), in an order
+// that depends on the lane -- reductions combine both, so the order never matters.
+struct SwapPair {
+    uint32_t a, b;
+};
+__device__ __forceinline__ SwapPair swap16(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return SwapPair{r[0], r[1]};
+}
+__device__ __forceinline__ SwapPair swap32(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return SwapPair{r[0], r[1]};
+}
+
+template <class T, class Op>
+__device__ __forceinline__ T wave_allreduce(T v, Op op) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit values");
+    auto dstep = [&](auto perm) {  // DPP: partner value from a lane permutation
+        if constexpr (sizeof(T) == 4) {
+            v = op(v, __builtin_bit_cast(T, perm(__builtin_bit_cast(uint32_t, v))));
+        } else {
+            const uint64_t x = __builtin_bit_cast(uint64_t, v);
+            const uint64_t y = (uint64_t)perm((uint32_t)x) | ((uint64_t)perm((uint32_t)(x >> 32)) << 32);
+            v = op(v, __builtin_bit_cast(T, y));
+        }
+    };
+    auto sstep = [&](auto swp) {   // permlane swap: combine both halves of the pair
+        if constexpr (sizeof(T) == 4) {
+            const SwapPair p = swp(__builtin_bit_cast(uint32_t, v));
+            v = op(__builtin_bit_cast(T, p.a), __builtin_bit_cast(T, p.b));
+        } else {
+            const uint64_t x = __builtin_bit_cast(uint64_t, v);
+            const SwapPair lo = swp((uint32_t)x), hi = swp((uint32_t)(x >> 32));
+            v = op(__builtin_bit_cast(T, (uint64_t)lo.a | ((uint64_t)hi.a << 32)),
+                   __builtin_bit_cast(T, (uint64_t)lo.b | ((uint64_t)hi.b << 32)));
+        }
+    };
+    dstep([](uint32_t x) { return dpp32<0xB1>(x); });   // quad_perm [1,0,3,2]
+    dstep([](uint32_t x) { return dpp32<0x4E>(x); });   // quad_perm [2,3,0,1]
+    dstep([](uint32_t x) { return dpp32<0x141>(x); });  // row_half_mirror
+    dstep([](uint32_t x) { return dpp32<0x140>(x); });  // row_mirror
+    sstep([](uint32_t x) { return swap16(x); });
+    sstep([](uint32_t x) { return swap32(x); });
     return v;
+}
+
+__device__ __forceinline__ double wave_min_f64(double v) {
+    return wave_allreduce(v, [](double a, double b) { return fmin(a, b); });
 }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint64_t w = __shfl_xor(v, o, kWave);
-        v = w > v ? w : v;
-    }
-    return v;
+    return wave_allreduce(v, [](uint64_t a, uint64_t b) { return a > b ? a : b; });
 }
 __device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, kWave));
-    return v;
+    return wave_allreduce(v, [](int a, int b) { return a > b ? a : b; });
 }
 __device__ __forceinline__ int wave_or_i32(int v) {
+    return wave_allreduce(v, [](int a, int b) { return a | b; });
+}
+
+// uniform read of a lane-distributed register array: element idx lives in lane idx % 64,
+// slot idx / 64 (idx wave-uniform)
+template <int N, class T>
+__device__ __forceinline__ T lane_get(const T (&x)[N], int idx) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit values");
+    const int slot = idx >> 6, src = idx & 63;
+    T sel = x[0];
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o, kWave);
-    return v;
+    for (int c = 1; c < N; ++c)
+        if (c == slot) sel = x[c];
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sel), src));
+    } else {
+        const uint64_t u = __builtin_bit_cast(uint64_t, sel);
+        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, src);
+        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+        return __builtin_bit_cast(T, (uint64_t)lo | ((uint64_t)hi << 32));
+    }
+}
+template <int N, class T>
+__device__ __forceinline__ void lane_set(T (&x)[N], int idx, T val) {
+    const int slot = idx >> 6, dst = idx & 63;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+        if (c == slot && lane == dst) x[c] = val;
 }
 
 // wave-scope barrier with LDS/global ordering (a workgroup may hold other waves that do

@@ -201,27 +201,29 @@ __global__ void __launch_bounds__(256) reset_kernel(Src src, asg_batch_view bv, 
 // bids_as_actions: assignments = LSA(bids, maximize)[1]  (mock :121-122), one wave per
 // env, ahead of the step kernel; result in st.assign [E][n]
 // ------------------------------------------------------------------------------------
+template <int CPL>
 __global__ void __launch_bounds__(64) bids_assign_kernel(asg_batch_view bv, EnvState st, int ts) {
     extern __shared__ double s_lsa[];
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m;
-    float *cost = reinterpret_cast<float *>(s_lsa);                                  // [n][m]
-    double *u = reinterpret_cast<double *>(cost + n * m + ((n * m) & 1));           // [n]
-    int *c4r = reinterpret_cast<int *>(u + n);                                      // [n]
-    int *r4c = c4r + n;                                                             // [m]
-    int *path = r4c + m;                                                            // [m]
+    float *cost = reinterpret_cast<float *>(s_lsa);  // [n][m]
     const float *bids = fptr<float>(bv.actions, e, ts, 0, 0);
     int status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, cost);
     if (status == ASG_OK) {
-        LsaScratch sc{u, c4r, r4c, path};
-        const DenseCost<float> acc{cost, m};
-        if (m <= 64) status = lsa_solve_wave<1>(acc, n, m, sc);
-        else if (m <= 128) status = lsa_solve_wave<2>(acc, n, m, sc);
-        else if (m <= 256) status = lsa_solve_wave<4>(acc, n, m, sc);
-        else status = lsa_solve_wave<16>(acc, n, m, sc);
+        int c4r[CPL];
+        status = lsa_solve_wave<CPL>(DenseCost<float>{cost, m}, n, m, c4r);
+        if (status == ASG_OK) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int i = (int)threadIdx.x + kWave * c;
+                if (i < n) st.assign[e * n + i] = c4r[c];
+            }
+        }
     }
-    for (int i = threadIdx.x; i < n; i += kWave) st.assign[e * n + i] = status == ASG_OK ? c4r[i] : -1;
-    if (threadIdx.x == 0 && status != ASG_OK) atomicCAS(st.err, 0, status);
+    if (status != ASG_OK) {
+        for (int i = threadIdx.x; i < n; i += kWave) st.assign[e * n + i] = -1;
+        if (threadIdx.x == 0) atomicCAS(st.err, 0, status);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -525,9 +527,13 @@ template <class Src>
 static hipError_t launch_step_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts, int k,
                                   hipStream_t s) {
     if (st.bids) {
-        const size_t lds = sizeof(float) * ((size_t)st.n * st.m + 1) + sizeof(double) * st.n +
-                           sizeof(int) * (st.n + 2 * st.m) + 32;
-        hipLaunchKernelGGL(bids_assign_kernel, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        const size_t lds = sizeof(float) * (size_t)st.n * st.m + 32;
+        // bids matrices are at most 16384 entries (checked at create): m <= 16384 / n
+        if (st.m <= 64) hipLaunchKernelGGL(bids_assign_kernel<1>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        else if (st.m <= 128) hipLaunchKernelGGL(bids_assign_kernel<2>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        else if (st.m <= 256) hipLaunchKernelGGL(bids_assign_kernel<4>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        else if (st.m <= 512) hipLaunchKernelGGL(bids_assign_kernel<8>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        else hipLaunchKernelGGL(bids_assign_kernel<16>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
         launch_step_t<Src, true>(src, bv, st, ts, k, s);
     } else {
         launch_step_t<Src, false>(src, bv, st, ts, k, s);

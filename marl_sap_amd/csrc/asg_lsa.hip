@@ -37,22 +37,31 @@ __device__ int lsa_check_wave(const IT *C, int64_t rs, int64_t cs, int nr0, int 
     return wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
 }
 
-template <int CPL, class Acc>
-__device__ int solve_cpl(const Acc &acc, int nr, int nc, LsaScratch s) {
-    return lsa_solve_wave<CPL>(acc, nr, nc, s);
+// Solve with the smallest columns-per-lane that fits, then hand the register-resident
+// assignment to `emit(col4row)` (a generic lambda taking int (&)[CPL]).
+template <int CPL, class Acc, class Emit>
+__device__ int solve_emit_cpl(const Acc &acc, int nr, int nc, Emit &emit) {
+    int c4r[CPL];
+    const int status = lsa_solve_wave<CPL>(acc, nr, nc, c4r);
+    if (status == ASG_OK) emit(c4r);
+    return status;
 }
 
-template <class Acc>
-__device__ int solve_any(const Acc &acc, int nr, int nc, LsaScratch s) {
-    if (nc <= 64) return solve_cpl<1>(acc, nr, nc, s);
-    if (nc <= 128) return solve_cpl<2>(acc, nr, nc, s);
-    if (nc <= 256) return solve_cpl<4>(acc, nr, nc, s);
-    if (nc <= 512) return solve_cpl<8>(acc, nr, nc, s);
-    return solve_cpl<16>(acc, nr, nc, s);
-}
+// columns per lane for a working matrix of nc columns (one kernel instantiation each,
+// so the register budget of a 64-column problem is not that of a 1024-column one)
+static int cpl_for(int nc) { return nc <= 64 ? 1 : nc <= 128 ? 2 : nc <= 256 ? 4 : nc <= 512 ? 8 : 16; }
 
-// LDS carve: [cost (optional)][u: nr f64][col4row: nr][row4col: nc][path: nc][mark: nr0]
-template <typename IT, typename CT, bool LDS_COST>
+#define ASG_DISPATCH_CPL(nc, LAUNCH) \
+    switch (cpl_for(nc)) {            \
+        case 1: LAUNCH(1); break;     \
+        case 2: LAUNCH(2); break;     \
+        case 4: LAUNCH(4); break;     \
+        case 8: LAUNCH(8); break;     \
+        default: LAUNCH(16); break;   \
+    }
+
+// LDS carve: [cost (optional)][mark: nr0 ints]
+template <int CPL, typename IT, typename CT, bool LDS_COST>
 __global__ void __launch_bounds__(64) lsa_batched_kernel(const IT *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
                                                          int nc0, int maximize, int64_t *row_out, int64_t *col_out,
                                                          int32_t *status_out) {
@@ -65,54 +74,49 @@ __global__ void __launch_bounds__(64) lsa_batched_kernel(const IT *C, int64_t s0
     char *p = reinterpret_cast<char *>(s_lsa);
     CT *cost = reinterpret_cast<CT *>(p);
     if (LDS_COST) p += ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
-    LsaScratch sc;
-    sc.u = reinterpret_cast<double *>(p);
-    p += sizeof(double) * nr;
-    sc.col4row = reinterpret_cast<int *>(p);
-    p += sizeof(int) * nr;
-    sc.row4col = reinterpret_cast<int *>(p);
-    p += sizeof(int) * nc;
-    sc.path = reinterpret_cast<int *>(p);
-    p += sizeof(int) * nc;
     int *mark = reinterpret_cast<int *>(p);
-
+    int64_t *ro = row_out ? row_out + b * k : nullptr;
+    int64_t *co = col_out ? col_out + b * k : nullptr;
+    auto emit = [&](const auto &c4r) { lsa_emit_wave(c4r, nr0, nc0, mark, ro, co, nullptr); };
     int status;
     if (LDS_COST) {
         status = lsa_stage_wave<IT, CT>(Cb, s1, s2, nr0, nc0, maximize != 0, cost);
-        if (status == ASG_OK) status = solve_any(DenseCost<CT>{cost, nc}, nr, nc, sc);
+        if (status == ASG_OK) status = solve_emit_cpl<CPL>(DenseCost<CT>{cost, nc}, nr, nc, emit);
     } else {
         status = lsa_check_wave<IT>(Cb, s1, s2, nr0, nc0, maximize != 0);
-        if (status == ASG_OK) status = solve_any(GlobalCost<IT>{Cb, s1, s2, tr, maximize != 0}, nr, nc, sc);
+        if (status == ASG_OK)
+            status = solve_emit_cpl<CPL>(GlobalCost<IT>{Cb, s1, s2, tr, maximize != 0}, nr, nc, emit);
     }
     const int lane = threadIdx.x;
-    if (status == ASG_OK) {
-        lsa_emit_wave(sc.col4row, nr0, nc0, mark, row_out ? row_out + b * k : nullptr,
-                      col_out ? col_out + b * k : nullptr, nullptr);
-    } else {
+    if (status != ASG_OK) {
         for (int r = lane; r < k; r += kWave) {
-            if (row_out) row_out[b * k + r] = -1;
-            if (col_out) col_out[b * k + r] = -1;
+            if (ro) ro[r] = -1;
+            if (co) co[r] = -1;
         }
     }
     if (lane == 0 && status_out) status_out[b] = status;
 }
 
-static size_t lsa_scratch_bytes(int nr, int nc, int nr0) {
-    return sizeof(double) * nr + sizeof(int) * (nr + 2 * nc + nr0) + 64;
-}
+static size_t lsa_scratch_bytes(int nr0) { return sizeof(int) * nr0 + 64; }
 
 template <typename IT, typename CT>
 static hipError_t launch_lsa_t(const IT *C, const int64_t st[3], int64_t B, int nr0, int nc0, int maximize,
                                int64_t *row_out, int64_t *col_out, int32_t *status_out, hipStream_t s) {
     const int nr = nc0 < nr0 ? nc0 : nr0, nc = nc0 < nr0 ? nr0 : nc0;
     const size_t cost_bytes = ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
-    const size_t scratch = lsa_scratch_bytes(nr, nc, nr0);
+    const size_t scratch = lsa_scratch_bytes(nr0);
     if (cost_bytes <= kLdsCostBudget) {
-        hipLaunchKernelGGL((lsa_batched_kernel<IT, CT, true>), dim3(B), dim3(64), cost_bytes + scratch, s, C, st[0],
-                           st[1], st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+#define L_(CPL)                                                                                                   \
+    hipLaunchKernelGGL((lsa_batched_kernel<CPL, IT, CT, true>), dim3(B), dim3(64), cost_bytes + scratch, s, C, \
+                       st[0], st[1], st[2], nr0, nc0, maximize, row_out, col_out, status_out)
+        ASG_DISPATCH_CPL(nc, L_)
+#undef L_
     } else {
-        hipLaunchKernelGGL((lsa_batched_kernel<IT, CT, false>), dim3(B), dim3(64), scratch, s, C, st[0], st[1],
-                           st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+#define L_(CPL)                                                                                                 \
+    hipLaunchKernelGGL((lsa_batched_kernel<CPL, IT, CT, false>), dim3(B), dim3(64), scratch, s, C, st[0], st[1], \
+                       st[2], nr0, nc0, maximize, row_out, col_out, status_out)
+        ASG_DISPATCH_CPL(nc, L_)
+#undef L_
     }
     return hipGetLastError();
 }
@@ -183,7 +187,7 @@ struct HaaCost {
     }
 };
 
-template <bool STAGE>
+template <int CPL, bool STAGE>
 __global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
                                                         const int64_t *prev, int64_t p0, int64_t p1, int n, int m,
                                                         const double *T_trans, double lambda_, float *col_out,
@@ -195,15 +199,6 @@ __global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64
     float *sb = reinterpret_cast<float *>(p);
     if (STAGE) p += ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
     int *sp = reinterpret_cast<int *>(p);
-    p += ((sizeof(int) * n + 15) / 16) * 16;
-    LsaScratch sc;
-    sc.u = reinterpret_cast<double *>(p);
-    p += sizeof(double) * n;
-    sc.col4row = reinterpret_cast<int *>(p);
-    p += sizeof(int) * n;
-    sc.row4col = reinterpret_cast<int *>(p);
-    p += sizeof(int) * m;
-    sc.path = reinterpret_cast<int *>(p);
     int bad = 0;
     for (int idx = lane; idx < n * m; idx += kWave) {
         const int i = idx / m, j = idx - i * m;
@@ -213,13 +208,16 @@ __global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64
     }
     for (int i = lane; i < n; i += kWave) sp[i] = (int)prev[b * p0 + i * p1];
     wave_sync();
+    float *co = col_out + b * n;
+    auto emit = [&](const auto &c4r) { lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co); };
     int status = wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
     if (status == ASG_OK) {
         const HaaCost acc = STAGE ? HaaCost{sb, m, 1, sp, T_trans, lambda_, m}
                                   : HaaCost{beta + b * b0, b1, b2, sp, T_trans, lambda_, m};
-        status = solve_any(acc, n, m, sc);
+        status = solve_emit_cpl<CPL>(acc, n, m, emit);
     }
-    for (int i = lane; i < n; i += kWave) col_out[b * n + i] = status == ASG_OK ? (float)sc.col4row[i] : -1.0f;
+    if (status != ASG_OK)
+        for (int i = lane; i < n; i += kWave) co[i] = -1.0f;
     if (lane == 0 && status_out) status_out[b] = status;
 }
 
@@ -227,13 +225,20 @@ hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s) {
     const size_t cost = ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
-    const size_t rest = ((sizeof(int) * n + 15) / 16) * 16 + sizeof(double) * n + sizeof(int) * (n + 2 * m) + 64;
-    if (cost <= kLdsCostBudget)
-        hipLaunchKernelGGL(haa_select_kernel<true>, dim3(B), dim3(64), cost + rest, s, beta, bs[0], bs[1], bs[2],
-                           prev, ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out);
-    else
-        hipLaunchKernelGGL(haa_select_kernel<false>, dim3(B), dim3(64), rest, s, beta, bs[0], bs[1], bs[2], prev,
-                           ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out);
+    const size_t rest = ((sizeof(int) * n + 15) / 16) * 16 + 64;
+    if (cost <= kLdsCostBudget) {
+#define L_(CPL)                                                                                                 \
+    hipLaunchKernelGGL((haa_select_kernel<CPL, true>), dim3(B), dim3(64), cost + rest, s, beta, bs[0], bs[1], bs[2], \
+                       prev, ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out)
+        ASG_DISPATCH_CPL(m, L_)
+#undef L_
+    } else {
+#define L_(CPL)                                                                                                  \
+    hipLaunchKernelGGL((haa_select_kernel<CPL, false>), dim3(B), dim3(64), rest, s, beta, bs[0], bs[1], bs[2], prev, \
+                       ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out)
+        ASG_DISPATCH_CPL(m, L_)
+#undef L_
+    }
     return hipGetLastError();
 }
 

@@ -20,14 +20,6 @@
 
 namespace asg {
 
-// Scratch in LDS for one problem: u[nr] (f64), col4row[nr], row4col[nc], path[nc] (i32)
-struct LsaScratch {
-    double *u;
-    int *col4row;
-    int *row4col;
-    int *path;
-};
-
 // Row-major cost matrix in LDS (already transposed / sign-flipped)
 template <typename CT>
 struct DenseCost {
@@ -37,29 +29,25 @@ struct DenseCost {
 };
 
 // Solve on the working matrix acc(i, j), i < nr <= nc <= 64*CPL (scipy's orientation).
-// Returns 0 or ASG_E_LSA_INFEASIBLE; s.col4row holds the assignment.
-// All 64 lanes of the wave must call it with identical arguments.
+// All per-row and per-column state lives in registers, distributed over the lanes
+// (column j / row r in lane j%64, slot j/64); only the cost matrix is in memory.  The
+// per-iteration reductions are VALU butterflies (DPP + permlane swaps) and the uniform
+// reads are v_readlane, so the serial augmenting-path loop has no LDS round trip except
+// the cost-row read.  Returns 0 or ASG_E_LSA_INFEASIBLE; col4row[c] holds the column
+// assigned to row lane + 64c.  All 64 lanes must call it with identical arguments.
 template <int CPL, class Acc>
-__device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, LsaScratch s) {
+__device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL]) {
     const int lane = threadIdx.x & (kWave - 1);
-    for (int r = lane; r < nr; r += kWave) {
-        s.u[r] = 0.0;
-        s.col4row[r] = -1;
-    }
-    double v[CPL];
-    int r4c[CPL];
+    double v[CPL], u[CPL];
+    int r4c[CPL], path[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-        const int j = lane + kWave * c;
         v[c] = 0.0;
+        u[c] = 0.0;
         r4c[c] = -1;
-        if (j < nc) {
-            s.row4col[j] = -1;
-            s.path[j] = -1;
-        }
+        path[c] = -1;
+        col4row[c] = -1;
     }
-    wave_sync();
-
     for (int cur = 0; cur < nr; ++cur) {
         double spc[CPL];
         int pos[CPL];
@@ -75,7 +63,7 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, LsaScratch s) {
         double minv = 0.0;
         int i = cur, sink = -1;
         while (sink == -1) {
-            const double ui = s.u[i];
+            const double ui = lane_get(u, i);
             double lo = __builtin_inf();
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
@@ -84,36 +72,50 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, LsaScratch s) {
                     const double r = ((minv + acc(i, j)) - ui) - v[c];
                     if (r < spc[c]) {
                         spc[c] = r;
-                        s.path[j] = i;
+                        path[c] = i;
                     }
                     lo = fmin(lo, spc[c]);
                 }
             }
             const double lowest = wave_min_f64(lo);
             if (lowest == __builtin_inf()) return ASG_E_LSA_INFEASIBLE;  // uniform branch
-            // packed selection key, reduced with max:
-            //   bit 63      : candidate is unassigned
-            //   bits 62..32 : unassigned ? pos : (2^30 - pos)   (largest pos vs smallest pos)
-            //   bits 31..0  : column index
-            uint64_t key = 0;
+            // candidates (remaining columns at the minimum): one ballot per slot.  With a
+            // single candidate (the common case for float data) it is the selection;
+            // ties fall back to the packed-key reduction below.
+            int total = 0, jsel = -1, psel = -1;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const int j = lane + kWave * c;
-                if (pos[c] >= 0 && spc[c] == lowest) {
-                    const bool un = r4c[c] == -1;
-                    const uint64_t k = un ? ((1ull << 63) | ((uint64_t)pos[c] << 32) | (uint32_t)j)
-                                          : (((uint64_t)((1u << 30) - (uint32_t)pos[c]) << 32) | (uint32_t)j);
-                    key = k > key ? k : key;
+                const uint64_t msk = __ballot(pos[c] >= 0 && spc[c] == lowest);
+                const int cnt = __popcll(msk);
+                if (cnt == 1 && total == 0) {
+                    const int src = __builtin_ctzll(msk);
+                    jsel = src + kWave * c;
+                    psel = __builtin_amdgcn_readlane(pos[c], src);
                 }
+                total += cnt;
             }
-            key = wave_max_u64(key);
-            const int jsel = (int)(uint32_t)key;
-            const int last = nrem - 1;
-            int psel = -1;
+            if (total != 1) {
+                // packed selection key, reduced with max:
+                //   bit 63      : candidate is unassigned
+                //   bits 62..32 : unassigned ? pos : (2^30 - pos)   (largest pos vs smallest pos)
+                //   bits 31..0  : column index
+                uint64_t key = 0;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c)
-                if (lane + kWave * c == jsel) psel = pos[c];
-            psel = wave_max_i32(psel);
+                for (int c = 0; c < CPL; ++c) {
+                    const int j = lane + kWave * c;
+                    if (pos[c] >= 0 && spc[c] == lowest) {
+                        const uint64_t k = (r4c[c] == -1)
+                                               ? ((1ull << 63) | ((uint64_t)pos[c] << 32) | (uint32_t)j)
+                                               : (((uint64_t)((1u << 30) - (uint32_t)pos[c]) << 32) | (uint32_t)j);
+                        key = k > key ? k : key;
+                    }
+                }
+                key = wave_max_u64(key);
+                const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
+                jsel = __builtin_amdgcn_readfirstlane((uint32_t)key);
+                psel = (khi >> 31) ? (int)(khi & 0x7fffffffu) : (int)((1u << 30) - khi);
+            }
+            const int last = nrem - 1;
             // remaining[index] = remaining[--num_remaining]
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
@@ -125,40 +127,45 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, LsaScratch s) {
             }
             --nrem;
             minv = lowest;
-            const int owner = s.row4col[jsel];
+            const int owner = lane_get(r4c, jsel);
             if (owner == -1) sink = jsel; else i = owner;
         }
-        // dual update: u[cur] += minv; u[row4col[j]] += minv - spc[j] for the other
-        // rows of the tree (one per scanned assigned column); v[j] -= minv - spc[j]
-        if (lane == 0) s.u[cur] += minv;
-        wave_sync();
+        // dual update (scipy: u[cur] += minv; u[r] += minv - spc[col4row[r]] for the
+        // other visited rows; v[j] -= minv - spc[j] for the scanned columns).  A row
+        // r != cur was visited iff its matched column col4row[r] was scanned.
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const int j = lane + kWave * c;
-            if (sc[c]) {
-                const double d = minv - spc[c];
-                if (j != sink) s.u[r4c[c]] += d;
-                v[c] -= d;
-            }
-        }
-        wave_sync();
-        // augment along path back to cur
-        if (lane == 0) {
-            int j = sink;
-            while (true) {
-                const int pi = s.path[j];
-                s.row4col[j] = pi;
-                const int t = s.col4row[pi];
-                s.col4row[pi] = j;
-                j = t;
-                if (pi == cur) break;
-            }
-        }
-        wave_sync();
+            const int r = lane + kWave * c;
+            const int jm = col4row[c];
+            // gather (sc, spc) of column jm from its owner lane
+            double spc_j = 0.0;
+            int sc_j = 0;
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int j = lane + kWave * c;
-            if (j < nc) r4c[c] = s.row4col[j];
+            for (int c2 = 0; c2 < CPL; ++c2) {
+                const double sv = __shfl(spc[c2], jm & 63, kWave);
+                const int sb = __shfl((int)sc[c2], jm & 63, kWave);
+                if (jm >= 0 && (jm >> 6) == c2) {
+                    spc_j = sv;
+                    sc_j = sb;
+                }
+            }
+            if (r < nr) {
+                if (r == cur) u[c] += minv;
+                else if (jm >= 0 && sc_j) u[c] += minv - spc_j;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+            if (sc[c]) v[c] -= minv - spc[c];
+        // augment along path back to cur (uniform loop of lane reads/writes)
+        int j = sink;
+        while (true) {
+            const int pi = lane_get(path, j);
+            lane_set(r4c, j, pi);
+            const int t = lane_get(col4row, pi);
+            lane_set(col4row, pi, j);
+            j = t;
+            if (pi == cur) break;
         }
     }
     return ASG_OK;
@@ -188,22 +195,31 @@ __device__ int lsa_stage_wave(const IT *C, int64_t rs, int64_t cs, int nr0, int 
 // scipy's output convention from the working solution: (arange(nr), col4row) or, when
 // transposed, (col4row[argsort(col4row)], argsort(col4row)).  `mark` is LDS scratch of
 // nr0 ints (only used when transposed).
-__device__ inline void lsa_emit_wave(const int *col4row, int nr0, int nc0, int *mark,
-                                     int64_t *row_out, int64_t *col_out, float *colf_out) {
+template <int CPL>
+__device__ void lsa_emit_wave(const int (&col4row)[CPL], int nr0, int nc0, int *mark, int64_t *row_out,
+                              int64_t *col_out, float *colf_out) {
     const int lane = threadIdx.x & (kWave - 1);
     if (nc0 >= nr0) {
-        for (int r = lane; r < nr0; r += kWave) {
-            if (row_out) row_out[r] = r;
-            if (col_out) col_out[r] = col4row[r];
-            if (colf_out) colf_out[r] = (float)col4row[r];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int r = lane + kWave * c;
+            if (r < nr0) {
+                if (row_out) row_out[r] = r;
+                if (col_out) col_out[r] = col4row[c];
+                if (colf_out) colf_out[r] = (float)col4row[c];
+            }
         }
         return;
     }
-    // transposed: working rows are original columns (nc0 of them), col4row[c] is the
-    // original row matched to original column c; emit sorted by original row
+    // transposed: working rows are original columns (nc0 of them), col4row is the
+    // original row matched to each original column; emit sorted by original row
     for (int r = lane; r < nr0; r += kWave) mark[r] = -1;
     wave_sync();
-    for (int c = lane; c < nc0; c += kWave) mark[col4row[c]] = c;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int oc = lane + kWave * c;
+        if (oc < nc0) mark[col4row[c]] = oc;
+    }
     wave_sync();
     int base = 0;
     for (int r0 = 0; r0 < nr0; r0 += kWave) {

@@ -1,3 +1,3 @@
-from .rnn_agent import RNNAgent
+from .rnn_agent import RNNAgent, RNNFusedAgent
 
-REGISTRY = {"rnn": RNNAgent}
+REGISTRY = {"rnn": RNNAgent, "rnn_fused": RNNFusedAgent}

@@ -1,7 +1,12 @@
 """Shared-parameter agent network (reference: modules/agents/rnn_agent.py:7-31):
 fc1 -> ReLU -> GRUCell (use_rnn) or Linear+ReLU -> fc2, fp32, run in PyTorch-ROCm."""
+import ctypes
+
+import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ... import _lib
 
 
 class RNNAgent(nn.Module):
@@ -27,3 +32,46 @@ class RNNAgent(nn.Module):
             h = F.relu(self.rnn(x))
         q = self.fc2(h)
         return q, h
+
+
+class RNNFusedAgent(RNNAgent):
+    """RNNAgent with the same parameters / state_dict, whose inference forward (no autograd:
+    the rollout's action selection) is one fused HIP kernel (asg_rnn_agent_forward: f32
+    MFMA, fc1 + GRUCell + fc2 with every intermediate on chip).  With autograd enabled
+    (learner training) it is the plain PyTorch module, so gradients are unchanged."""
+
+    def __init__(self, input_shape, args):
+        super().__init__(input_shape, args)
+        if args.hidden_dim != 64 or args.m % 16 != 0 or args.m > 64 or input_shape % 4 != 0:
+            raise ValueError("rnn_fused needs hidden_dim == 64, m in {16, 32, 48, 64} and an input size "
+                             "divisible by 4; use agent 'rnn'")
+
+    def forward(self, inputs, hidden_state):
+        if torch.is_grad_enabled() or not inputs.is_cuda:
+            return super().forward(inputs, hidden_state)
+        x = inputs
+        if x.dtype != torch.float32 or x.stride(-1) != 1 or x.stride(0) % 4 != 0 or x.data_ptr() % 16 != 0:
+            x = x.float().contiguous()
+        R, K = x.shape
+        H = self.args.hidden_dim
+        h = hidden_state
+        if h.dim() == 3 and h.stride(0) == 0 and h.stride(1) == 0 and h.stride(2) == 1:
+            hs = 0  # init_hidden's expanded zero row: one row broadcast to all agents
+        else:
+            h = h.reshape(-1, H)
+            if h.stride(-1) != 1 or h.stride(0) % 4 != 0 or h.data_ptr() % 16 != 0:
+                h = h.contiguous()
+            hs = h.stride(0)
+        h_out = torch.empty((R, H), dtype=torch.float32, device=x.device)
+        q = torch.empty((R, self.args.m), dtype=torch.float32, device=x.device)
+        rnn = self.args.use_rnn
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        w_ih = self.rnn.weight_ih if rnn else self.rnn.weight
+        b_ih = self.rnn.bias_ih if rnn else self.rnn.bias
+        with torch.cuda.device(x.device):
+            _lib.check(_lib.lib().asg_rnn_agent_forward(
+                p(x), x.stride(0), R, K, p(h), hs, p(self.fc1.weight), p(self.fc1.bias), p(w_ih), p(b_ih),
+                p(self.rnn.weight_hh) if rnn else None, p(self.rnn.bias_hh) if rnn else None,
+                p(self.fc2.weight), p(self.fc2.bias), H, self.args.m, int(bool(rnn)), p(h_out), p(q),
+                _lib.stream_ptr(x.device)))
+        return q, h_out

@@ -165,6 +165,10 @@ void ora_beta_hat(const double *beta, const int64_t *prev, int n, int m,
 /* ------------------------------------------------------------------------------ */
 /* scipy linear_sum_assignment restatement                  */
 /* ------------------------------------------------------------------------------ */
+/* inner-loop iterations of the last ora_lsa call (instrumentation for tuning) */
+static long g_lsa_iters;
+long ora_lsa_iterations(void) { return g_lsa_iters; }
+
 /* returns 0 ok, -1 invalid entries (NaN / -inf after sign), -2 infeasible.
  * row/col receive min(nr, nc) entries. */
 int ora_lsa(const double *C_in, int nr0, int nc0, int maximize, int64_t *row_out, int64_t *col_out) {
@@ -190,6 +194,7 @@ int ora_lsa(const double *C_in, int nr0, int nc0, int maximize, int64_t *row_out
     for (int i = 0; i < nr; i++) col4row[i] = -1;
     for (int j = 0; j < nc; j++) { row4col[j] = -1; path[j] = -1; }
     int status = 0;
+    g_lsa_iters = 0;
 
     for (int cur = 0; cur < nr; cur++) {
         double minv = 0.0;
@@ -199,6 +204,7 @@ int ora_lsa(const double *C_in, int nr0, int nc0, int maximize, int64_t *row_out
         for (int j = 0; j < nc; j++) spc[j] = INFINITY;
         int64_t i = cur, sink = -1;
         while (sink == -1) {
+            g_lsa_iters++;
             int64_t index = -1;
             double lowest = INFINITY;
             SR[i] = 1;

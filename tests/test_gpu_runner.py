@@ -40,12 +40,16 @@ def _args(n, m, T, B, seed, use_rnn, rname, sel, macname):
         jumpstart_epsilon_anneal_time=1000, jumpstart_evaluation_epsilon=1.0)
 
 
+@pytest.mark.parametrize("agent", ["rnn", "rnn_fused"])
 @pytest.mark.parametrize("tag", TAGS)
-def test_runner_matches_reference_dump(golden, tag):
+def test_runner_matches_reference_dump(golden, tag, agent):
     g = golden("runner_dumps")
     n, m, T, B, seed, use_rnn = [int(x) for x in g[f"{tag}__cfg"]]
     rname, sel, macname = [str(x) for x in g[f"{tag}__names"]]
+    if agent == "rnn_fused" and m % 16:
+        pytest.skip("fused agent needs m % 16 == 0")
     args = _args(n, m, T, B, seed, use_rnn, rname, sel, macname)
+    args.agent = agent
     runner = r_REGISTRY[rname](args, _Logger())
     env = runner.get_env()
     mac = mac_REGISTRY[macname](env.scheme, {"agents": n}, args)
