@@ -194,17 +194,21 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
 
 /* RNNAgent forward (inference) for R agent rows in one fused f32-MFMA kernel:
  *   x = relu(X W1^T + b1); GRUCell(x, h) (use_rnn) or relu(x W_ih^T + b_ih); q = h' W2^T + b2.
+ * Weights are first packed (asg_rnn_agent_pack, once per weight update) from the torch
+ * nn.Linear / nn.GRUCell layouts (W1 [hidden][K], W_ih / W_hh [3*hidden][hidden] -- or
+ * W_ih = W_rnn [hidden][hidden] and W_hh = NULL when use_rnn = 0 -- and W2 [n_out][hidden])
+ * into a device buffer of asg_rnn_agent_packed_size() bytes.
  * X [R][K] f32 (row stride x_stride, K % 4 == 0, 16-B aligned rows); h_in [R][hidden] with
- * row stride h_stride (0 = one row broadcast to all, NULL = zeros); weights in torch
- * nn.Linear / nn.GRUCell layouts (W1 [hidden][K], W_ih / W_hh [3*hidden][hidden] or
- * W_ih = W_rnn [hidden][hidden] with W_hh = NULL when use_rnn = 0, W2 [n_out][hidden]),
- * contiguous.  Outputs h_out [R][hidden], q_out [R][n_out], contiguous.  hidden must be
- * 64, n_out one of 16, 32, 48, 64. */
+ * row stride h_stride (0 = one row broadcast to all, NULL = zeros); biases contiguous.
+ * Outputs h_out [R][hidden], q_out [R][n_out], contiguous.  hidden must be 64, n_out one
+ * of 16, 32, 48, 64. */
+int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn);
+int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, const float *W2, int K,
+                       int hidden, int n_out, int use_rnn, void *packed, void *hip_stream);
 int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,
-                          int64_t h_stride, const float *W1, const float *b1, const float *W_ih,
-                          const float *b_ih, const float *W_hh, const float *b_hh, const float *W2,
-                          const float *b2, int hidden, int n_out, int use_rnn, float *h_out,
-                          float *q_out, void *hip_stream);
+                          int64_t h_stride, const void *packed, const float *b1, const float *b_ih,
+                          const float *b_hh, const float *b2, int hidden, int n_out, int use_rnn,
+                          float *h_out, float *q_out, void *hip_stream);
 
 #ifdef __cplusplus
 }

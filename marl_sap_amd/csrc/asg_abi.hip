@@ -356,21 +356,40 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_epsilon_greedy");
 }
 
+static bool agent_shape_ok(int K, int hidden, int n_out) {
+    return hidden == 64 && n_out > 0 && n_out <= 64 && n_out % 16 == 0 && K > 0 && K % 4 == 0;
+}
+
+int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn) {
+    if (!agent_shape_ok(K, hidden, n_out)) return fail(nullptr, ASG_E_INVALID_ARG, "bad agent shape");
+    return asg::rnn_agent_packed_f4(K, n_out, use_rnn) * 16;
+}
+
+int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, const float *W2, int K, int hidden,
+                       int n_out, int use_rnn, void *packed, void *hip_stream) {
+    if (!W1 || !W_ih || !W2 || !packed || (use_rnn && !W_hh))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_pack: NULL weight or output");
+    if (!agent_shape_ok(K, hidden, n_out))
+        return fail(nullptr, ASG_E_INVALID_ARG,
+                    "asg_rnn_agent_pack: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0");
+    hipError_t e = asg::launch_rnn_agent_pack(W1, W_ih, W_hh, W2, K, n_out, use_rnn, static_cast<float4 *>(packed),
+                                              static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_pack");
+}
+
 int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in, int64_t h_stride,
-                          const float *W1, const float *b1, const float *W_ih, const float *b_ih, const float *W_hh,
-                          const float *b_hh, const float *W2, const float *b2, int hidden, int n_out, int use_rnn,
-                          float *h_out, float *q_out, void *hip_stream) {
-    if (!x || !W1 || !b1 || !W_ih || !b_ih || !W2 || !b2 || !h_out || !q_out || R < 0 || K <= 0)
+                          const void *packed, const float *b1, const float *b_ih, const float *b_hh, const float *b2,
+                          int hidden, int n_out, int use_rnn, float *h_out, float *q_out, void *hip_stream) {
+    if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !q_out || R < 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: bad arguments");
-    if (use_rnn && (!W_hh || !b_hh))
-        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: GRU weights missing");
-    if (hidden != 64 || n_out <= 0 || n_out > 64 || n_out % 16 != 0 || K % 4 != 0 || x_stride % 4 != 0 || h_stride % 4 != 0 ||
+    if (!agent_shape_ok(K, hidden, n_out) || x_stride % 4 != 0 || h_stride % 4 != 0 ||
         (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG,
-                    "asg_rnn_agent_forward: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0 and 16-B aligned rows");
+                    "asg_rnn_agent_forward: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0 and 16-B "
+                    "aligned rows");
     if (R == 0) return ASG_OK;
-    hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, W1, b1, W_ih, b_ih, W_hh, b_hh, W2,
-                                             b2, n_out, use_rnn, h_out, q_out,
+    hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed),
+                                             b1, b_ih, b_hh, b2, n_out, use_rnn, h_out, q_out,
                                              static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_forward");
 }

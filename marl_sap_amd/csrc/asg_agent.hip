@@ -42,11 +42,35 @@ __device__ __forceinline__ float comp(const float4 &v, int e) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Packed weight layout ("fragment order"): for W [C][K] row-major (torch nn.Linear), block
+// (t, ct) holds, for lane l, W[16 ct + (l & 15)][16 t + 4 (l >> 4) .. + 3] as one float4,
+// so one wave loads a whole MFMA B-operand chunk as 1 KiB of contiguous memory.  K is
+// zero-padded to a multiple of 16.  Offsets (in float4) of the four matrices:
+//   W1: [K16/16][4][64]; W_ih: [4][12][64]; W_hh: [4][12][64] (GRU) ; W2: [4][nq][64]
+__device__ __forceinline__ int64_t pk(int t, int ct, int nct, int lane) { return ((int64_t)t * nct + ct) * 64 + lane; }
+
+__global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
+    const int nct = C / 16, nt = (K + 15) / 16;
+    const int64_t total = (int64_t)nt * nct * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(i & 63);
+        const int ct = (int)((i >> 6) % nct);
+        const int t = (int)((i >> 6) / nct);
+        const int row = 16 * ct + (lane & 15), k = 16 * t + 4 * (lane >> 4);
+        float4 v;
+        v.x = k + 0 < K ? W[(int64_t)row * K + k + 0] : 0.f;
+        v.y = k + 1 < K ? W[(int64_t)row * K + k + 1] : 0.f;
+        v.z = k + 2 < K ? W[(int64_t)row * K + k + 2] : 0.f;
+        v.w = k + 3 < K ? W[(int64_t)row * K + k + 3] : 0.f;
+        out[i] = v;
+    }
+}
+
 // acc[rt][ct] += A(rows of `a_src`, k) * W^T(k, cols 16*ct0 .. 16*(ct0+NCT)-1) over K,
 // A rows come from a row-major [32][lda] LDS tile; W is row-major [cols][K] in global.
 template <int NCT>
-__device__ __forceinline__ void gemm_lds_a(f32x4 (&acc)[2][NCT], const float *a_lds, int lda, const float *W,
-                                           int ldw, int col0, int K) {
+__device__ __forceinline__ void gemm_lds_a(f32x4 (&acc)[2][NCT], const float *a_lds, int lda, const float4 *Wp,
+                                           int wnct, int ct0, int K) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     for (int t = 0; t < K / 16; ++t) {
         float4 a4[2], b4[NCT];
@@ -54,8 +78,7 @@ __device__ __forceinline__ void gemm_lds_a(f32x4 (&acc)[2][NCT], const float *a_
         for (int rt = 0; rt < 2; ++rt)
             a4[rt] = *reinterpret_cast<const float4 *>(a_lds + (16 * rt + r) * lda + 16 * t + 4 * q);
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
-            b4[ct] = *reinterpret_cast<const float4 *>(W + (int64_t)(col0 + 16 * ct + r) * ldw + 16 * t + 4 * q);
+        for (int ct = 0; ct < NCT; ++ct) b4[ct] = Wp[pk(t, ct0 + ct, wnct, lane)];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -73,9 +96,9 @@ constexpr int kWaveLds = 2 * kRowsPerWave * kLdsStride + kRowsPerWave * kStageSt
 template <bool RNN, int NQ>
 __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
-    const float *__restrict__ W1, const float *__restrict__ b1, const float *__restrict__ Wih,
-    const float *__restrict__ bih, const float *__restrict__ Whh, const float *__restrict__ bhh,
-    const float *__restrict__ W2, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q) {
+    const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
+    const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
+    const float4 *__restrict__ W2p, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q) {
     extern __shared__ float s_agent[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     float *sx = s_agent + wave * kWaveLds;                 // x = relu(fc1), [32][kLdsStride]
@@ -105,20 +128,26 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
         const bool oka = ra < R, okb = rb < R;
         const float *xa = X + (oka ? ra : 0) * xs, *xb = X + (okb ? rb : 0) * xs;
         const int nt = (K + 15) / 16;
-        float4 a_nxt[2], b_nxt[4];
+        // two chunks in flight: chunk t is consumed while t+1 and t+2 are loading
+        float4 a0[2], b0[4], a1[2], b1r[4];
         auto load = [&](int t, float4 (&a4)[2], float4 (&b4)[4]) {
             const int k = 16 * t + 4 * q;
-            const bool okk = k < K;  // K % 4 == 0 (checked on the host)
+            const bool okk = t < nt && k < K;  // K % 4 == 0 (checked on the host)
             a4[0] = ldg4(xa + k, oka && okk);
             a4[1] = ldg4(xb + k, okb && okk);
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) b4[ct] = ldg4(W1 + (int64_t)(16 * ct + r) * K + k, okk);
+            for (int ct = 0; ct < 4; ++ct) b4[ct] = t < nt ? W1p[pk(t, ct, 4, lane)] : make_float4(0.f, 0.f, 0.f, 0.f);
         };
-        load(0, a_nxt, b_nxt);
+        load(0, a0, b0);
+        load(1, a1, b1r);
         for (int t = 0; t < nt; ++t) {
-            float4 a4[2] = {a_nxt[0], a_nxt[1]};
-            float4 b4[4] = {b_nxt[0], b_nxt[1], b_nxt[2], b_nxt[3]};
-            if (t + 1 < nt) load(t + 1, a_nxt, b_nxt);  // prefetch the next chunk under the MFMAs
+            float4 a4[2] = {a0[0], a0[1]};
+            float4 b4[4] = {b0[0], b0[1], b0[2], b0[3]};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a0[i] = a1[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b0[i] = b1r[i];
+            if (t + 2 < nt) load(t + 2, a1, b1r);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -156,18 +185,27 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
             for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
                 for (int g = 0; g < 3; ++g) gi[rt][g] = gh[rt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float4 bi[3], bh[3];
+            auto wload = [&](int t, float4 (&wi)[3], float4 (&wh)[3]) {
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    wi[g] = Wihp[pk(t, 4 * g + hb, 12, lane)];
+                    wh[g] = Whhp[pk(t, 4 * g + hb, 12, lane)];
+                }
+            };
+            wload(0, bi, bh);
             for (int t = 0; t < kHid / 16; ++t) {
-                float4 ax[2], ah[2], bi[3], bh[3];
+                float4 ax[2], ah[2], ci[3], ch[3];
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    ci[g] = bi[g];
+                    ch[g] = bh[g];
+                }
+                if (t + 1 < kHid / 16) wload(t + 1, bi, bh);  // weights of the next chunk in flight
 #pragma unroll
                 for (int rt = 0; rt < 2; ++rt) {
                     ax[rt] = *reinterpret_cast<const float4 *>(sx + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
                     ah[rt] = *reinterpret_cast<const float4 *>(sh + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
-                }
-#pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    const int64_t wrow = g * kHid + u;
-                    bi[g] = *reinterpret_cast<const float4 *>(Wih + wrow * kHid + 16 * t + 4 * q);
-                    bh[g] = *reinterpret_cast<const float4 *>(Whh + wrow * kHid + 16 * t + 4 * q);
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
@@ -175,8 +213,8 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
                     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
                         for (int g = 0; g < 3; ++g) {
-                            gi[rt][g] = mfma4(comp(ax[rt], e), comp(bi[g], e), gi[rt][g]);
-                            gh[rt][g] = mfma4(comp(ah[rt], e), comp(bh[g], e), gh[rt][g]);
+                            gi[rt][g] = mfma4(comp(ax[rt], e), comp(ci[g], e), gi[rt][g]);
+                            gh[rt][g] = mfma4(comp(ah[rt], e), comp(ch[g], e), gh[rt][g]);
                         }
             }
             const float bir = bih[u], biz = bih[kHid + u], bin = bih[2 * kHid + u];
@@ -194,7 +232,7 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
         } else {
             f32x4 a2[2][1];
             a2[0][0] = a2[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-            gemm_lds_a<1>(a2, sx, kLdsStride, Wih, kHid, 16 * hb, kHid);
+            gemm_lds_a<1>(a2, sx, kLdsStride, Wihp, 4, hb, kHid);
             const float bb = bih[u];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
@@ -218,8 +256,7 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
             for (int rt = 0; rt < 2; ++rt)
                 a4[rt] = *reinterpret_cast<const float4 *>(sp + (16 * rt + r) * kStageStride + 4 * q);
 #pragma unroll
-            for (int c = 0; c < NQ; ++c)
-                b4[c] = *reinterpret_cast<const float4 *>(W2 + (int64_t)(16 * c + r) * kHid + 16 * hb + 4 * q);
+            for (int c = 0; c < NQ; ++c) b4[c] = W2p[pk(hb, c, NQ, lane)];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -243,16 +280,46 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
         }
 }
 
+// float4 count of the packed weight buffer
+int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
+    const int64_t w1 = (int64_t)((K + 15) / 16) * 4 * 64;
+    const int64_t wr = use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64;
+    const int64_t w2 = 4 * (int64_t)(nout / 16) * 64;
+    return w1 + wr + w2;
+}
+
+hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
+                                 int use_rnn, float4 *packed, hipStream_t s) {
+    float4 *p = packed;
+    auto one = [&](const float *W, int C, int KK) {
+        const int64_t n = (int64_t)((KK + 15) / 16) * (C / 16) * 64;
+        hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, C, KK, p);
+        p += n;
+    };
+    one(W1, kHid, K);
+    if (use_rnn) {
+        one(Wih, 3 * kHid, kHid);
+        one(Whh, 3 * kHid, kHid);
+    } else {
+        one(Wih, kHid, kHid);
+    }
+    one(W2, nout, kHid);
+    return hipGetLastError();
+}
+
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
-                                const float *W1, const float *b1, const float *Wih, const float *bih,
-                                const float *Whh, const float *bhh, const float *W2, const float *b2, int nout,
-                                int use_rnn, float *Hout, float *Q, hipStream_t s) {
+                                const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                const float *b2, int nout, int use_rnn, float *Hout, float *Q, hipStream_t s) {
     const int64_t rows_per_block = 4 * kRowsPerWave;
     const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
     const size_t lds = sizeof(float) * 4 * kWaveLds;
-#define L_(RNN, NQ)                                                                                             \
-    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, W1, \
-                       b1, Wih, bih, Whh, bhh, W2, b2, Hout, Q)
+    const float4 *W1p = packed;
+    const float4 *Wihp = W1p + (int64_t)((K + 15) / 16) * 4 * 64;
+    const float4 *Whhp = Wihp + (use_rnn ? 4 * 12 * 64 : 4 * 4 * 64);
+    const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
+#define L_(RNN, NQ)                                                                                              \
+    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, W1p, \
+                       b1, Wihp, bih, Whhp, bhh, W2p, b2, Hout, Q)
     const int nq = nout / 16;
     if (use_rnn) {
         if (nq == 1) L_(true, 1); else if (nq == 2) L_(true, 2); else if (nq == 3) L_(true, 3); else L_(true, 4);

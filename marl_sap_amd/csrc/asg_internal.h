@@ -53,9 +53,11 @@ hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t 
                              int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter, int64_t *out,
                              const int64_t os[2], int *err, hipStream_t s);
 
+int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
+hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
+                                 int use_rnn, float4 *packed, hipStream_t s);
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
-                                const float *W1, const float *b1, const float *Wih, const float *bih,
-                                const float *Whh, const float *bhh, const float *W2, const float *b2, int nout,
-                                int use_rnn, float *Hout, float *Q, hipStream_t s);
+                                const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                const float *b2, int nout, int use_rnn, float *Hout, float *Q, hipStream_t s);
 
 }  // namespace asg

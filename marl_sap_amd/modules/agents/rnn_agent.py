@@ -66,12 +66,29 @@ class RNNFusedAgent(RNNAgent):
         q = torch.empty((R, self.args.m), dtype=torch.float32, device=x.device)
         rnn = self.args.use_rnn
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-        w_ih = self.rnn.weight_ih if rnn else self.rnn.weight
         b_ih = self.rnn.bias_ih if rnn else self.rnn.bias
         with torch.cuda.device(x.device):
+            packed = self._packed(K, x.device)
             _lib.check(_lib.lib().asg_rnn_agent_forward(
-                p(x), x.stride(0), R, K, p(h), hs, p(self.fc1.weight), p(self.fc1.bias), p(w_ih), p(b_ih),
-                p(self.rnn.weight_hh) if rnn else None, p(self.rnn.bias_hh) if rnn else None,
-                p(self.fc2.weight), p(self.fc2.bias), H, self.args.m, int(bool(rnn)), p(h_out), p(q),
-                _lib.stream_ptr(x.device)))
+                p(x), x.stride(0), R, K, p(h), hs, p(packed), p(self.fc1.bias), p(b_ih),
+                p(self.rnn.bias_hh) if rnn else None, p(self.fc2.bias), H, self.args.m, int(bool(rnn)), p(h_out),
+                p(q), _lib.stream_ptr(x.device)))
         return q, h_out
+
+    def _packed(self, K, device):
+        """Weights in the kernel's fragment order, re-packed only when a weight changed
+        (optimizer steps bump the tensors' version counters; load_state_dict too)."""
+        rnn = self.args.use_rnn
+        ws = [self.fc1.weight, self.rnn.weight_ih if rnn else self.rnn.weight,
+              self.rnn.weight_hh if rnn else None, self.fc2.weight]
+        key = (K, str(device), tuple((w.data_ptr(), w._version) for w in ws if w is not None))
+        if getattr(self, "_pack_key", None) != key:
+            L = _lib.lib()
+            nbytes = L.asg_rnn_agent_packed_size(K, self.args.hidden_dim, self.args.m, int(bool(rnn)))
+            _lib.check(int(nbytes) if nbytes < 0 else 0)
+            buf = torch.empty(int(nbytes) // 4, dtype=torch.float32, device=device)
+            p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+            _lib.check(L.asg_rnn_agent_pack(p(ws[0]), p(ws[1]), p(ws[2]), p(ws[3]), K, self.args.hidden_dim,
+                                            self.args.m, int(bool(rnn)), p(buf), _lib.stream_ptr(device)))
+            self._pack_buf, self._pack_key = buf, key
+        return self._pack_buf
