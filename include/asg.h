@@ -209,6 +209,18 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
                           int64_t h_stride, const void *packed, const float *b1, const float *b_ih,
                           const float *b_hh, const float *b2, int hidden, int n_out, int use_rnn,
                           float *h_out, float *q_out, void *hip_stream);
+/* asg_rnn_agent_forward + asg_epsilon_greedy fused: the Q tile never leaves the chip
+ * (q_out may be NULL).  Rows are (env, agent) = (row / n, row % n); avail [env][agent][m]
+ * bool with strides avail_strides = {env, agent} (task stride 1); actions written to
+ * out[env * out_strides[0] + agent * out_strides[1]] (int64).  Same Philox stream as
+ * asg_epsilon_greedy for equal (seed, counter): identical actions. */
+int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,
+                         int64_t h_stride, const void *packed, const float *b1, const float *b_ih,
+                         const float *b_hh, const float *b2, int hidden, int n_out, int use_rnn,
+                         float *h_out, float *q_out, const uint8_t *avail,
+                         const int64_t avail_strides[2], int n, double epsilon, uint64_t seed,
+                         uint64_t counter, int64_t *out, const int64_t out_strides[2],
+                         int32_t *status, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,18 @@ class EpsilonGreedyActionSelector:
         self.calls = 0
         self.status = None
 
+    def fused_params(self, t_env, test_mode, device):
+        """Epsilon / seed / call counter / status word for a kernel that fuses this
+        selector into the agent forward (asg_rnn_agent_select); same state updates as
+        select_action."""
+        self.epsilon = self.schedule.eval(t_env)
+        if test_mode:
+            self.epsilon = self.args.evaluation_epsilon
+        if self.status is None or self.status.device != device:
+            self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        self.calls += 1
+        return self.epsilon, self.seed, self.calls, self.status
+
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None, out=None):
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:

@@ -33,10 +33,25 @@ class BasicMAC:
         """`out` (optional, int64 [B, n]): selectors that support it write the actions
         there in place (the runner passes the EpisodeBatch actions row)."""
         avail_actions = ep_batch["avail_actions"][:, t_ep]
+        if out is not None and self._fused_select_ok(bs):
+            # agent forward + epsilon-greedy in one HIP kernel: Q never leaves the chip
+            eps, seed, counter, status = self.action_selector.fused_params(t_env, test_mode, out.device)
+            self.hidden_states = self.selector_agent.forward_select(
+                self._build_inputs(ep_batch, t_ep), self.hidden_states, avail_actions, self.n, eps, seed, counter,
+                out, status)
+            return out
         agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode, action_selection_mode=True)
         kw = {"out": out} if out is not None and _accepts_out(self.action_selector) else {}
         return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env,
                                                   test_mode=test_mode, beta=ep_batch["beta"][bs, t_ep], **kw)
+
+    def _fused_select_ok(self, bs):
+        from ..action_selectors.classic_selectors import EpsilonGreedyActionSelector
+        from ..modules.agents.rnn_agent import RNNFusedAgent
+        return (not torch.is_grad_enabled() and isinstance(bs, slice) and bs == slice(None)
+                and self.agent_output_type == "q" and type(self.action_selector) is EpsilonGreedyActionSelector
+                and isinstance(self.selector_agent, RNNFusedAgent)
+                and not getattr(self.args, "unfused_selection", False))
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

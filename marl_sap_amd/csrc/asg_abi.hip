@@ -389,9 +389,30 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
                     "aligned rows");
     if (R == 0) return ASG_OK;
     hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed),
-                                             b1, b_ih, b_hh, b2, n_out, use_rnn, h_out, q_out,
+                                             b1, b_ih, b_hh, b2, n_out, use_rnn, h_out, q_out, nullptr,
                                              static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_forward");
+}
+
+int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in, int64_t h_stride,
+                         const void *packed, const float *b1, const float *b_ih, const float *b_hh, const float *b2,
+                         int hidden, int n_out, int use_rnn, float *h_out, float *q_out, const uint8_t *avail,
+                         const int64_t avail_strides[2], int n, double epsilon, uint64_t seed, uint64_t counter,
+                         int64_t *out, const int64_t out_strides[2], int32_t *status, void *hip_stream) {
+    if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !avail || !avail_strides || !out || !out_strides ||
+        !status || R < 0 || n <= 0 || (use_rnn && !b_hh))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: bad arguments");
+    if (!agent_shape_ok(K, hidden, n_out) || x_stride % 4 != 0 || h_stride % 4 != 0 ||
+        (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: unsupported shape / alignment");
+    if (!(epsilon >= 0.0 && epsilon <= 1.0))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: epsilon must be in [0, 1]");
+    if (R == 0) return ASG_OK;
+    hipError_t e = asg::launch_rnn_agent_select(
+        x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed), b1, b_ih, b_hh, b2, n_out, use_rnn,
+        h_out, q_out, avail, avail_strides[0], avail_strides[1], n, (float)epsilon, seed, (uint32_t)counter, out,
+        out_strides[0], out_strides[1], status, static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_select");
 }
 
 }  // extern "C"

@@ -93,12 +93,13 @@ constexpr int kWaveLds = 2 * kRowsPerWave * kLdsStride + kRowsPerWave * kStageSt
 
 // NQ = n_out / 16 output tiles of fc2 (n_out <= 64); fc2 is accumulated block by block as
 // each 16-unit block of h' is produced, so h' never needs a full LDS tile.
-template <bool RNN, int NQ>
+template <bool RNN, int NQ, bool SEL>
 __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
-    const float4 *__restrict__ W2p, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q) {
+    const float4 *__restrict__ W2p, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q,
+    SelectArgs sel) {
     extern __shared__ float s_agent[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     float *sx = s_agent + wave * kWaveLds;                 // x = relu(fc1), [32][kLdsStride]
@@ -115,6 +116,42 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (RNN && Hin && row < R) v = *reinterpret_cast<const float4 *>(Hin + row * hs + c4);
         *reinterpret_cast<float4 *>(sh + rr * kLdsStride + c4) = v;
+    }
+
+    // ---- selection mask, loaded early (its latency hides under fc1): bit (rt, v, c) =
+    //      avail[row 16 rt + 4 q + v][task 16 c + r]
+    uint32_t avbits = 0;
+    // (env, agent) of row row0 + d without a 64-bit division per row
+    int64_t sel_b0 = 0;
+    int sel_i0 = 0;
+    if (SEL) {
+        sel_b0 = row0 / sel.n;
+        sel_i0 = (int)(row0 - sel_b0 * sel.n);
+    }
+    auto env_agent = [&](int d, int64_t &b, int &i) {
+        b = sel_b0;
+        i = sel_i0 + d;
+        while (i >= sel.n) {
+            i -= sel.n;
+            ++b;
+        }
+    };
+    if (SEL) {
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int64_t row = row0 + 16 * rt + 4 * q + v;
+                if (row < R) {
+                    int64_t b;
+                    int i;
+                    env_agent(16 * rt + 4 * q + v, b, i);
+                    const uint8_t *ar = sel.avail + b * sel.a0 + (int64_t)i * sel.a1;
+#pragma unroll
+                    for (int c = 0; c < NQ; ++c)
+                        if (ar[16 * c + r]) avbits |= 1u << ((rt * 4 + v) * 4 + c);
+                }
+            }
     }
 
     // ---- fc1: x = relu(X W1^T + b1), X rows streamed from HBM ------------------------
@@ -270,14 +307,90 @@ __global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
-            const int col = 16 * c + r;
-            const float bb = b2[col];
+            const float bb = b2[16 * c + r];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) aq[rt][c][v] += bb;
+        }
+    if (Q) {
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int c = 0; c < NQ; ++c)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int64_t row = row0 + 16 * rt + 4 * q + v;
+                    if (row < R) Q[row * nout + 16 * c + r] = aq[rt][c][v];
+                }
+    }
+    if (SEL) {
+        // the 16 lanes of a DPP row (same q) hold the nout Q-values of one agent row
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 const int64_t row = row0 + 16 * rt + 4 * q + v;
-                if (row < R) Q[row * nout + col] = aq[rt][c][v] + bb;
+                const bool live = row < R;
+                int64_t b;
+                int i;
+                env_agent(16 * rt + 4 * q + v, b, i);
+                float best = -__builtin_inff();
+                int bj = 0x7fffffff;
+                uint32_t rowmask[NQ];  // availability bits of this row, task 16c + lane-in-row
+#pragma unroll
+                for (int c = 0; c < NQ; ++c) {
+                    const int col = 16 * c + r;
+                    const bool av = live && ((avbits >> ((rt * 4 + v) * 4 + c)) & 1u);
+                    rowmask[c] = (uint32_t)(__ballot(av) >> (16 * q)) & 0xFFFFu;
+                    const float x = av ? aq[rt][c][v] : -__builtin_inff();
+                    if (better(x, col, best, bj)) {
+                        best = x;
+                        bj = col;
+                    }
+                }
+                auto red = [&](auto perm) {
+                    const float ob = __builtin_bit_cast(float, perm(__builtin_bit_cast(uint32_t, best)));
+                    const int oj = (int)perm((uint32_t)bj);
+                    if (better(ob, oj, best, bj)) {
+                        best = ob;
+                        bj = oj;
+                    }
+                };
+                red([](uint32_t x) { return dpp32<0xB1>(x); });
+                red([](uint32_t x) { return dpp32<0x4E>(x); });
+                red([](uint32_t x) { return dpp32<0x141>(x); });
+                red([](uint32_t x) { return dpp32<0x140>(x); });
+                int action = bj == 0x7fffffff ? 0 : bj;
+                if (r == 0 && live) {
+                    if (sel.epsilon > 0.0f) {
+                        const u32x4 rr = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect,
+                                                             sel.counter}, sel.k0, sel.k1);
+                        constexpr float k2m24 = 5.9604644775390625e-08f;
+                        if ((float)(rr.x >> 8) * k2m24 < sel.epsilon) {  // explore: Categorical(avail)
+                            // tasks in index order j = 16 c + bit, from the row's ballot masks
+                            int cnt = 0;
+#pragma unroll
+                            for (int c = 0; c < NQ; ++c) cnt += __popc(rowmask[c]);
+                            if (cnt == 0) {
+                                atomicCAS(sel.err, 0, ASG_E_INVALID_ARG);
+                            } else {
+                                int target = (int)(((uint64_t)rr.y * (uint64_t)cnt) >> 32);
+#pragma unroll
+                                for (int c = 0; c < NQ; ++c) {
+                                    const int pc = __popc(rowmask[c]);
+                                    if (target >= 0 && target < pc) {
+                                        uint32_t msk = rowmask[c];
+                                        for (int k = 0; k < target; ++k) msk &= msk - 1;  // drop lowest bits
+                                        action = 16 * c + __builtin_ctz(msk);
+                                    }
+                                    target -= pc;
+                                }
+                            }
+                        }
+                    }
+                    sel.out[b * sel.o0 + (int64_t)i * sel.o1] = action;
+                }
             }
-        }
+    }
 }
 
 // float4 count of the packed weight buffer
@@ -309,7 +422,8 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
 
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
                                 const float4 *packed, const float *b1, const float *bih, const float *bhh,
-                                const float *b2, int nout, int use_rnn, float *Hout, float *Q, hipStream_t s) {
+                                const float *b2, int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel,
+                                hipStream_t s) {
     const int64_t rows_per_block = 4 * kRowsPerWave;
     const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
     const size_t lds = sizeof(float) * 4 * kWaveLds;
@@ -317,17 +431,34 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     const float4 *Wihp = W1p + (int64_t)((K + 15) / 16) * 4 * 64;
     const float4 *Whhp = Wihp + (use_rnn ? 4 * 12 * 64 : 4 * 4 * 64);
     const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
-#define L_(RNN, NQ)                                                                                              \
-    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, W1p, \
-                       b1, Wihp, bih, Whhp, bhh, W2p, b2, Hout, Q)
+    const SelectArgs sa = sel ? *sel : SelectArgs{};
+#define L_(RNN, NQ, SEL)                                                                                      \
+    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ, SEL>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, \
+                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, Hout, Q, sa)
+#define NQ_(RNN, SEL)                   \
+    if (nq == 1) L_(RNN, 1, SEL);       \
+    else if (nq == 2) L_(RNN, 2, SEL);  \
+    else if (nq == 3) L_(RNN, 3, SEL);  \
+    else L_(RNN, 4, SEL);
     const int nq = nout / 16;
     if (use_rnn) {
-        if (nq == 1) L_(true, 1); else if (nq == 2) L_(true, 2); else if (nq == 3) L_(true, 3); else L_(true, 4);
+        if (sel) { NQ_(true, true) } else { NQ_(true, false) }
     } else {
-        if (nq == 1) L_(false, 1); else if (nq == 2) L_(false, 2); else if (nq == 3) L_(false, 3); else L_(false, 4);
+        if (sel) { NQ_(false, true) } else { NQ_(false, false) }
     }
+#undef NQ_
 #undef L_
     return hipGetLastError();
+}
+
+hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
+                                   const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                   const float *b2, int nout, int use_rnn, float *Hout, float *Q,
+                                   const uint8_t *avail, int64_t a0, int64_t a1, int n, float epsilon, uint64_t seed,
+                                   uint32_t counter, int64_t *out, int64_t o0, int64_t o1, int *err, hipStream_t s) {
+    const SelectArgs sa{avail, a0, a1, n, epsilon, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5bd1e995u, counter,
+                        out, o0, o1, err};
+    return launch_rnn_agent_fwd(X, xs, R, K, Hin, hs, packed, b1, bih, bhh, b2, nout, use_rnn, Hout, Q, &sa, s);
 }
 
 }  // namespace asg

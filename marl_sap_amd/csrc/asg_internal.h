@@ -30,6 +30,19 @@ struct EnvState {
     int *err;              // sticky device error code
 };
 
+// fused epsilon-greedy selection on the Q tile (EpsilonGreedyActionSelector, see
+// asg_select.hip for the standalone form): rows are (env b, agent i) = (row / n, row % n)
+struct SelectArgs {
+    const uint8_t *avail;  // avail_actions, task stride 1
+    int64_t a0, a1;        // (env, agent) strides of avail
+    int n;                 // agents per env
+    float epsilon;
+    uint32_t k0, k1, counter;
+    int64_t *out;          // actions (int64), (env, agent) strides o0, o1
+    int64_t o0, o1;
+    int *err;              // sticky: exploration over a row with no available action
+};
+
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s);
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
@@ -58,6 +71,12 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
                                  int use_rnn, float4 *packed, hipStream_t s);
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
                                 const float4 *packed, const float *b1, const float *bih, const float *bhh,
-                                const float *b2, int nout, int use_rnn, float *Hout, float *Q, hipStream_t s);
+                                const float *b2, int nout, int use_rnn, float *Hout, float *Q,
+                                const SelectArgs *sel, hipStream_t s);
+hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
+                                   const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                   const float *b2, int nout, int use_rnn, float *Hout, float *Q,
+                                   const uint8_t *avail, int64_t a0, int64_t a1, int n, float epsilon, uint64_t seed,
+                                   uint32_t counter, int64_t *out, int64_t o0, int64_t o1, int *err, hipStream_t s);
 
 }  // namespace asg

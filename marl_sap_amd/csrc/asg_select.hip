@@ -12,16 +12,6 @@
 
 namespace asg {
 
-constexpr uint32_t kCtrSelect = 6u;
-
-// "a beats b" in torch.max order: NaN wins, then larger value, then smaller index
-__device__ __forceinline__ bool better(float va, int ja, float vb, int jb) {
-    const bool na = va != va, nb = vb != vb;
-    if (na != nb) return na;
-    if (na) return ja < jb;
-    return va > vb || (va == vb && ja < jb);
-}
-
 template <bool VEC4>
 __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2,
                                                          const uint8_t *avail, int64_t a0, int64_t a1, int64_t a2,

@@ -46,13 +46,10 @@ class RNNFusedAgent(RNNAgent):
             raise ValueError("rnn_fused needs hidden_dim == 64, m in {16, 32, 48, 64} and an input size "
                              "divisible by 4; use agent 'rnn'")
 
-    def forward(self, inputs, hidden_state):
-        if torch.is_grad_enabled() or not inputs.is_cuda:
-            return super().forward(inputs, hidden_state)
+    def _prep(self, inputs, hidden_state):
         x = inputs
         if x.dtype != torch.float32 or x.stride(-1) != 1 or x.stride(0) % 4 != 0 or x.data_ptr() % 16 != 0:
             x = x.float().contiguous()
-        R, K = x.shape
         H = self.args.hidden_dim
         h = hidden_state
         if h.dim() == 3 and h.stride(0) == 0 and h.stride(1) == 0 and h.stride(2) == 1:
@@ -62,18 +59,42 @@ class RNNFusedAgent(RNNAgent):
             if h.stride(-1) != 1 or h.stride(0) % 4 != 0 or h.data_ptr() % 16 != 0:
                 h = h.contiguous()
             hs = h.stride(0)
-        h_out = torch.empty((R, H), dtype=torch.float32, device=x.device)
-        q = torch.empty((R, self.args.m), dtype=torch.float32, device=x.device)
-        rnn = self.args.use_rnn
+        return x, h, hs
+
+    def _common(self, x, h, hs):
+        R, K = x.shape
+        rnn = bool(self.args.use_rnn)
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-        b_ih = self.rnn.bias_ih if rnn else self.rnn.bias
+        h_out = torch.empty((R, self.args.hidden_dim), dtype=torch.float32, device=x.device)
+        args = [p(x), x.stride(0), R, K, p(h), hs, p(self._packed(K, x.device)), p(self.fc1.bias),
+                p(self.rnn.bias_ih if rnn else self.rnn.bias), p(self.rnn.bias_hh) if rnn else None,
+                p(self.fc2.bias), self.args.hidden_dim, self.args.m, int(rnn), p(h_out)]
+        return h_out, args, p
+
+    def forward(self, inputs, hidden_state):
+        if torch.is_grad_enabled() or not inputs.is_cuda:
+            return super().forward(inputs, hidden_state)
+        x, h, hs = self._prep(inputs, hidden_state)
         with torch.cuda.device(x.device):
-            packed = self._packed(K, x.device)
-            _lib.check(_lib.lib().asg_rnn_agent_forward(
-                p(x), x.stride(0), R, K, p(h), hs, p(packed), p(self.fc1.bias), p(b_ih),
-                p(self.rnn.bias_hh) if rnn else None, p(self.fc2.bias), H, self.args.m, int(bool(rnn)), p(h_out),
-                p(q), _lib.stream_ptr(x.device)))
+            h_out, args, p = self._common(x, h, hs)
+            q = torch.empty((x.shape[0], self.args.m), dtype=torch.float32, device=x.device)
+            _lib.check(_lib.lib().asg_rnn_agent_forward(*args, p(q), _lib.stream_ptr(x.device)))
         return q, h_out
+
+    def forward_select(self, inputs, hidden_state, avail, n, epsilon, seed, counter, out, status, q_out=None):
+        """forward + epsilon-greedy in one kernel (asg_rnn_agent_select): actions into `out`
+        ([B, n] int64 view, e.g. the EpisodeBatch actions row); avail [B, n, m] bool.
+        Returns the new hidden state [B*n, hidden]."""
+        x, h, hs = self._prep(inputs, hidden_state)
+        if avail.dtype != torch.bool or avail.stride(-1) != 1:
+            avail = (avail != 0).contiguous()
+        with torch.cuda.device(x.device):
+            h_out, args, p = self._common(x, h, hs)
+            _lib.check(_lib.lib().asg_rnn_agent_select(
+                *args, p(q_out), p(avail), _lib.i64arr(avail.stride()[:2]), n, float(epsilon),
+                seed & 0xFFFFFFFFFFFFFFFF, counter, p(out), _lib.i64arr(out.stride()), p(status),
+                _lib.stream_ptr(x.device)))
+        return h_out
 
     def _packed(self, K, device):
         """Weights in the kernel's fragment order, re-packed only when a weight changed

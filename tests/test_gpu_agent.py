@@ -59,3 +59,31 @@ def test_fused_agent_reads_time_major_obs_slab():
         q1, _ = fused(x, h)
     torch.testing.assert_close(q1, q0, rtol=1e-5, atol=2e-5)
     assert torch.equal(q1.view(E, n, m).max(2)[1], q0.view(E, n, m).max(2)[1])
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.3])
+def test_fused_select_equals_forward_then_selector(eps):
+    """asg_rnn_agent_select == asg_rnn_agent_forward followed by asg_epsilon_greedy with
+    the same Philox (seed, counter): same actions, same hidden state."""
+    from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector
+    B, n, m, K = 300, 64, 64, 256
+    torch.manual_seed(1)
+    args = SimpleNamespace(hidden_dim=64, use_rnn=True, m=m, epsilon_start=eps, epsilon_finish=eps,
+                           epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=5)
+    agent = RNNFusedAgent(K, args).to(DEV)
+    x = torch.randn((B * n, K), device=DEV)
+    h = torch.randn((B * n, 64), device=DEV)
+    avail = torch.rand((B, n, m), device=DEV) > 0.2
+    avail[..., 3] = True
+    sel = EpsilonGreedyActionSelector(args)
+    with torch.no_grad():
+        q, h1 = agent(x, h)
+        a1 = sel.select_action(q.view(B, n, m), avail, 0)
+        sel2 = EpsilonGreedyActionSelector(args)
+        e, seed, counter, status = sel2.fused_params(0, False, DEV)
+        assert (seed, counter) == (sel.seed, sel.calls)
+        out = torch.full((B, n), -7, dtype=torch.int64, device=DEV)
+        h2 = agent.forward_select(x, h, avail, n, e, seed, counter, out, status)
+    assert torch.equal(h2, h1)
+    assert torch.equal(out, a1)
+    assert int(status.item()) == 0
