@@ -55,7 +55,8 @@ def parse():
     p.add_argument("--selector", default="eps", choices=["eps", "sap", "random"])
     p.add_argument("--benefits", default="bump", choices=["bump", "dense"])
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-episodes", type=int, default=3)
+    p.add_argument("--cpu-episodes", type=int, default=2, help="minimum CPU-baseline episodes")
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample length (s)")
     p.add_argument("--agent", default="rnn_fused", choices=["rnn_fused", "rnn"],
                    help="rnn_fused: the same RNNAgent (weights, fp32) with its inference forward as one HIP kernel")
     p.add_argument("--seed", type=int, default=0)
@@ -87,16 +88,24 @@ def main():
     # the GPU
     cpu = None
     if rank == 0 and world == 1 and a.cpu_baseline:
+        from oracle import oracle as ora
         from oracle.cpu_parallel_runner import run_parallel_baseline
         workers = 8
         rate, steps_done, secs = run_parallel_baseline(n=a.n, m=a.m, T=a.T, L=a.L, workers=workers,
-                                                       episodes=a.cpu_episodes, epsilon=0.05)
+                                                       episodes=a.cpu_episodes, epsilon=0.05,
+                                                       min_seconds=a.cpu_seconds)
+        # second, stronger CPU number: the C oracle env, multi-threaded, random policy (env only)
+        c_envs = 4096 if a.n * a.m <= 4096 else 256
+        c_secs, _ = ora.rollout_random(c_envs, a.n, a.m, a.T, a.L, 0.5, a.seed, workers, 1)
         cpu = {"value": round(rate, 2), "unit": "env-steps/s", "cores": workers + 1, "kind": "port",
-               "sample": f"{a.cpu_episodes} episodes x {workers} subprocess envs x T={a.T} at {a.n}x{a.m} "
-                         f"({steps_done} env-steps, {secs:.1f} s): ParallelRunner Pipe protocol + numpy env "
-                         f"+ CPU RNN agent (oracle/cpu_parallel_runner.py)"}
+               "sample": f"{steps_done // (workers * a.T)} episodes x {workers} subprocess envs x T={a.T} at "
+                         f"{a.n}x{a.m} ({steps_done} env-steps, {secs:.1f} s): the reference's ParallelRunner design "
+                         f"(Pipe protocol, numpy env, CPU RNN agent + eps-greedy; oracle/cpu_parallel_runner.py)",
+               "c_env_only": {"value": round(c_envs * a.T / c_secs, 1), "unit": "env-steps/s", "cores": workers,
+                              "kind": "port", "sample": f"{c_envs} envs x 1 episode, random policy, C oracle "
+                                                        f"(oracle/asg_rollout.c), no agent network"}}
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = asg_dist.local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(a.seed + rank)

@@ -20,13 +20,20 @@ def init_from_env(backend=None):
         return rank_world()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("ASG_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group(backend, device_id=torch.device("cuda", local))
     else:
         dist.init_process_group(backend)
     return rank_world()
+
+
+def local_device_index():
+    """GPU of this rank: LOCAL_RANK (one process per GPU); ranks beyond the visible GPUs
+    wrap around (only meaningful for gloo rehearsals of the multi-rank path)."""
+    n = torch.cuda.device_count()
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(1, n)
 
 
 def all_gather_returns(local):

@@ -112,8 +112,9 @@ def _worker(remote, cfg):
 
 
 def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episodes=2, hidden=64,
-                          epsilon=0.05, seed=0):
-    """Runs `episodes` ParallelRunner-protocol episodes of `workers` envs; returns
+                          epsilon=0.05, seed=0, min_seconds=0.0, max_episodes=10000):
+    """Runs ParallelRunner-protocol episodes of `workers` envs -- `episodes` of them, or
+    more until `min_seconds` have elapsed (bounded by max_episodes); returns
     (env_steps_per_s, env_steps, seconds) over the step loops (resets included, as the
     reference runner's wall time includes them)."""
     import torch
@@ -137,7 +138,9 @@ def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episode
     steps = 0
     t0 = time.perf_counter()
     with torch.no_grad():
-        for _ in range(episodes):
+        ep = 0
+        while ep < episodes or (time.perf_counter() - t0 < min_seconds and ep < max_episodes):
+            ep += 1
             batch = EpisodeBatch(scheme, {"agents": n}, workers, T + 1, preprocess=preprocess, device="cpu")
             for c in parents:
                 c.send(("reset", None))
