@@ -10,7 +10,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmarl_sap_amd.so")
+LIB_PATH = os.environ.get("ASG_LIB_PATH") or os.path.join(HERE, "libmarl_sap_amd.so")
 
 ASG_OK = 0
 ASG_E_INVALID_ARG = -1

@@ -29,19 +29,28 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
+def build(force=False, verbose=False, out=None, extra=()):
+    """Build the library (`out`/`extra`: experiment variants, e.g. -DASG_AGENT_WAVES=3 into
+    build/, loaded with ASG_LIB_PATH; the product library is always LIB)."""
+    if out is None and not force and not needs_build():
         return LIB
-    cmd = [HIPCC] + FLAGS + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB + ".tmp"]
+    target = out or LIB
+    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", target + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc failed building libmarl_sap_amd.so")
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    argv = sys.argv[1:]
+    out = None
+    if "--out" in argv:
+        out = os.path.abspath(argv[argv.index("--out") + 1])
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+    extra = [a for a in argv if a.startswith("-D")]
+    print(build(force="--force" in argv, verbose=True, out=out, extra=extra))

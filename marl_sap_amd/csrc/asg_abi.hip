@@ -357,7 +357,7 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
 }
 
 static bool agent_shape_ok(int K, int hidden, int n_out) {
-    return hidden == 64 && n_out > 0 && n_out <= 64 && n_out % 16 == 0 && K > 0 && K % 4 == 0;
+    return hidden == 64 && n_out > 0 && n_out <= 256 && n_out % 16 == 0 && K > 0 && K % 4 == 0;
 }
 
 int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn) {
@@ -371,7 +371,7 @@ int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, co
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_pack: NULL weight or output");
     if (!agent_shape_ok(K, hidden, n_out))
         return fail(nullptr, ASG_E_INVALID_ARG,
-                    "asg_rnn_agent_pack: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0");
+                    "asg_rnn_agent_pack: needs hidden == 64, n_out a multiple of 16 up to 256, K % 4 == 0");
     hipError_t e = asg::launch_rnn_agent_pack(W1, W_ih, W_hh, W2, K, n_out, use_rnn, static_cast<float4 *>(packed),
                                               static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_pack");
@@ -385,7 +385,7 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
     if (!agent_shape_ok(K, hidden, n_out) || x_stride % 4 != 0 || h_stride % 4 != 0 ||
         (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG,
-                    "asg_rnn_agent_forward: needs hidden == 64, n_out in {16, 32, 48, 64}, K % 4 == 0 and 16-B "
+                    "asg_rnn_agent_forward: needs hidden == 64, n_out a multiple of 16 up to 256, K % 4 == 0 and 16-B "
                     "aligned rows");
     if (R == 0) return ASG_OK;
     hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed),

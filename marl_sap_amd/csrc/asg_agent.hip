@@ -15,9 +15,9 @@
 //
 // Arithmetic: v_mfma_f32_16x16x4_f32 -- exact fp32 products, fp32 accumulation (a k-ordered
 // fmaf chain), i.e. fp32 like the reference; only the summation order differs from
-// hipBLASLt's.  One wave owns 32 rows (2 row tiles of 16); the K dimension is walked in
-// chunks of 16 so each lane loads 4 consecutive k values as one float4 (the MFMA k slots
-// of step e map to k = 16t + 4q + e, identically for A and B).
+// hipBLASLt's (and the r/z gates add the input and hidden products in one accumulator).
+// One wave owns 32 agent rows; all activations stay in registers (see the transposed
+// formulation below), weights come from L1/L2 in a pre-packed fragment order.
 #include "asg_device.h"
 #include "asg_internal.h"
 
@@ -26,8 +26,10 @@ namespace asg {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRowsPerWave = 32;
+#ifndef ASG_AGENT_WAVES
+#define ASG_AGENT_WAVES 2  // waves per SIMD the register budget is fitted to
+#endif
 constexpr int kHid = 64;          // hidden_dim
-constexpr int kLdsStride = kHid + 4;  // padded row (floats) of the LDS row tiles
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -40,7 +42,16 @@ __device__ __forceinline__ float comp(const float4 &v, int e) {
     return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
 
+// GRU nonlinearities on the hardware transcendental units (v_exp_f32, v_rcp_f32): a few
+// ulp from the correctly rounded libm forms, far inside the 1e-5 parity tolerance, and
+// about 5% of the kernel's time.  -DASG_AGENT_EXACT_MATH restores expf / tanhf.
+#ifndef ASG_AGENT_EXACT_MATH
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) { return 2.0f * sigmoidf_(2.0f * x) - 1.0f; }
+#else
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
+#endif
 
 // Packed weight layout ("fragment order"): for W [C][K] row-major (torch nn.Linear), block
 // (t, ct) holds, for lane l, W[16 ct + (l & 15)][16 t + 4 (l >> 4) .. + 3] as one float4,
@@ -66,330 +77,360 @@ __global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
     }
 }
 
-// acc[rt][ct] += A(rows of `a_src`, k) * W^T(k, cols 16*ct0 .. 16*(ct0+NCT)-1) over K,
-// A rows come from a row-major [32][lda] LDS tile; W is row-major [cols][K] in global.
-template <int NCT>
-__device__ __forceinline__ void gemm_lds_a(f32x4 (&acc)[2][NCT], const float *a_lds, int lda, const float4 *Wp,
-                                           int wnct, int ct0, int K) {
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    for (int t = 0; t < K / 16; ++t) {
-        float4 a4[2], b4[NCT];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-            a4[rt] = *reinterpret_cast<const float4 *>(a_lds + (16 * rt + r) * lda + 16 * t + 4 * q);
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) b4[ct] = Wp[pk(t, ct0 + ct, wnct, lane)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int ct = 0; ct < NCT; ++ct) acc[rt][ct] = mfma4(comp(a4[rt], e), comp(b4[ct], e), acc[rt][ct]);
-    }
-}
+// ---------------------------------------------------------------------------------
+// Transposed formulation: every layer computes out^T = W . act^T, i.e. the MFMA A operand
+// is a packed weight fragment and the B operand an activation fragment.  With the
+// 16x16x4 f32 MFMA layouts
+//     A: lane l gives W[16 mt + (l & 15)][k = 16 t + 4 (l >> 4) + e]        (packed float4)
+//     B: lane l gives act[row 16 nt + (l & 15)][k = 16 t + 4 (l >> 4) + e]  (float4 of a row)
+//     C: lane l holds out[row 16 nt + (l & 15)][unit 16 mt + 4 (l >> 4) + v], v = 0..3
+// the accumulator of output tile mt IS the B-operand float4 of the next layer's k-chunk
+// t = mt, so activations go from layer to layer in registers: no LDS, no transposes, no
+// barriers.  One wave owns 32 rows (nt = 0, 1); lane (r, q) = (l & 15, l >> 4).
+// ---------------------------------------------------------------------------------
+// n_out <= 256 (checked by the ABI): a lane keeps 4 availability bits per output tile in a u64
 
-constexpr int kStageStride = 16 + 4;  // padded row (floats) of the per-block h' stage
-constexpr int kWaveLds = 2 * kRowsPerWave * kLdsStride + kRowsPerWave * kStageStride;  // floats
-
-// NQ = n_out / 16 output tiles of fc2 (n_out <= 64); fc2 is accumulated block by block as
-// each 16-unit block of h' is produced, so h' never needs a full LDS tile.
-template <bool RNN, int NQ, bool SEL>
-__global__ void __launch_bounds__(256) rnn_agent_fwd_kernel(
-    const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
+template <bool RNN, bool SEL>
+__device__ __forceinline__ void agent_rows(
+    int64_t row0, const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
-    const float4 *__restrict__ W2p, const float *__restrict__ b2, float *__restrict__ Hout, float *__restrict__ Q,
-    SelectArgs sel) {
-    extern __shared__ float s_agent[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    float *sx = s_agent + wave * kWaveLds;                 // x = relu(fc1), [32][kLdsStride]
-    float *sh = sx + kRowsPerWave * kLdsStride;            // h_in, [32][kLdsStride]
-    float *sp = sh + kRowsPerWave * kLdsStride;            // h' block stage, [32][kStageStride]
-    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * kRowsPerWave;
-    if (row0 >= R) return;  // whole wave idle (no block-level barrier below)
-    constexpr int nout = 16 * NQ;
-
-    // ---- h_in -> LDS (row-major, padded) -------------------------------------------
-    for (int idx = lane; idx < kRowsPerWave * kHid / 4; idx += 64) {
-        const int rr = idx / (kHid / 4), c4 = (idx % (kHid / 4)) * 4;
-        const int64_t row = row0 + rr;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (RNN && Hin && row < R) v = *reinterpret_cast<const float4 *>(Hin + row * hs + c4);
-        *reinterpret_cast<float4 *>(sh + rr * kLdsStride + c4) = v;
+    const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
+    float *__restrict__ Q, const SelectArgs &sel) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    if (row0 >= R) return;  // whole wave idle
+    int64_t rows[2];
+    bool ok[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        rows[nt] = row0 + 16 * nt + r;
+        ok[nt] = rows[nt] < R;
     }
 
-    // ---- selection mask, loaded early (its latency hides under fc1): bit (rt, v, c) =
-    //      avail[row 16 rt + 4 q + v][task 16 c + r]
-    uint32_t avbits = 0;
-    // (env, agent) of row row0 + d without a 64-bit division per row
-    int64_t sel_b0 = 0;
-    int sel_i0 = 0;
-    if (SEL) {
-        sel_b0 = row0 / sel.n;
-        sel_i0 = (int)(row0 - sel_b0 * sel.n);
-    }
-    auto env_agent = [&](int d, int64_t &b, int &i) {
-        b = sel_b0;
-        i = sel_i0 + d;
-        while (i >= sel.n) {
-            i -= sel.n;
-            ++b;
-        }
-    };
-    if (SEL) {
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int64_t row = row0 + 16 * rt + 4 * q + v;
-                if (row < R) {
-                    int64_t b;
-                    int i;
-                    env_agent(16 * rt + 4 * q + v, b, i);
-                    const uint8_t *ar = sel.avail + b * sel.a0 + (int64_t)i * sel.a1;
-#pragma unroll
-                    for (int c = 0; c < NQ; ++c)
-                        if (ar[16 * c + r]) avbits |= 1u << ((rt * 4 + v) * 4 + c);
-                }
-            }
-    }
-
-    // ---- fc1: x = relu(X W1^T + b1), X rows streamed from HBM ------------------------
+    // ---- fc1: x^T = relu(W1 X^T + b1), X rows streamed from HBM, 2 chunks in flight ----
+    f32x4 xB[4][2];
     {
-        f32x4 acc[2][4];
+        f32x4 acc[4][2];  // start from the bias (C layout: unit 16 mt + 4 q + v)
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
+        for (int mt = 0; mt < 4; ++mt) {
+            const float4 bb = *reinterpret_cast<const float4 *>(b1 + 16 * mt + 4 * q);
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int64_t ra = row0 + r, rb = row0 + 16 + r;
-        const bool oka = ra < R, okb = rb < R;
-        const float *xa = X + (oka ? ra : 0) * xs, *xb = X + (okb ? rb : 0) * xs;
-        const int nt = (K + 15) / 16;
-        // two chunks in flight: chunk t is consumed while t+1 and t+2 are loading
-        float4 a0[2], b0[4], a1[2], b1r[4];
-        auto load = [&](int t, float4 (&a4)[2], float4 (&b4)[4]) {
+            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{bb.x, bb.y, bb.z, bb.w};
+        }
+        const float *xr[2] = {X + (ok[0] ? rows[0] : 0) * xs, X + (ok[1] ? rows[1] : 0) * xs};
+        const int nk = (K + 15) / 16;
+        float4 a0[2], w0[4], a1[2], w1[4];
+        auto load = [&](int t, float4 (&a4)[2], float4 (&w4)[4]) {
             const int k = 16 * t + 4 * q;
-            const bool okk = t < nt && k < K;  // K % 4 == 0 (checked on the host)
-            a4[0] = ldg4(xa + k, oka && okk);
-            a4[1] = ldg4(xb + k, okb && okk);
+            const bool okk = k < K;  // K % 4 == 0 (checked on the host)
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) b4[ct] = t < nt ? W1p[pk(t, ct, 4, lane)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int nt = 0; nt < 2; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && okk);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) w4[mt] = W1p[pk(t, mt, 4, lane)];
         };
-        load(0, a0, b0);
-        load(1, a1, b1r);
-        for (int t = 0; t < nt; ++t) {
+        load(0, a0, w0);
+        if (nk > 1) load(1, a1, w1);
+        for (int t = 0; t < nk; ++t) {
             float4 a4[2] = {a0[0], a0[1]};
-            float4 b4[4] = {b0[0], b0[1], b0[2], b0[3]};
+            float4 w4[4] = {w0[0], w0[1], w0[2], w0[3]};
 #pragma unroll
             for (int i = 0; i < 2; ++i) a0[i] = a1[i];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) b0[i] = b1r[i];
-            if (t + 2 < nt) load(t + 2, a1, b1r);
+            for (int i = 0; i < 4; ++i) w0[i] = w1[i];
+            if (t + 2 < nk) load(t + 2, a1, w1);
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
+                for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                    for (int ct = 0; ct < 4; ++ct)
-                        acc[rt][ct] = mfma4(comp(a4[rt], e), comp(b4[ct], e), acc[rt][ct]);
+                    for (int nt = 0; nt < 2; ++nt)
+                        acc[mt][nt] = mfma4(comp(w4[mt], e), comp(a4[nt], e), acc[mt][nt]);
         }
-        // epilogue: C layout (col = lane & 15, row = 4 * (lane >> 4) + v)
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-            for (int ct = 0; ct < 4; ++ct) {
-                const int col = 16 * ct + r;
-                const float bb = b1[col];
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-                for (int v = 0; v < 4; ++v)
-                    sx[(16 * rt + 4 * q + v) * kLdsStride + col] = fmaxf(acc[rt][ct][v] + bb, 0.f);
-            }
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v], 0.f);
     }
-    wave_sync();
 
-    // ---- recurrent layer, one 16-unit block of h' at a time; fc2 accumulated per block -------
-    f32x4 aq[2][NQ];
+    // ---- h_in fragments (B operand of W_hh, and h of the GRU update), issued first -----
+    float4 hB[4][2];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) aq[rt][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < 2; ++nt)
+            hB[t][nt] = ldg4(Hin + (ok[nt] ? rows[nt] : 0) * hs + 16 * t + 4 * q, RNN && Hin && ok[nt]);
+
+    // ---- recurrent layer -> h'^T in registers (hp[hb] = B operand of fc2's chunk hb) ----
+    f32x4 hp[4][2];
+#pragma unroll
     for (int hb = 0; hb < 4; ++hb) {
-        const int u = 16 * hb + r;
-        f32x4 hp[2];
         if (RNN) {
-            f32x4 gi[2][3], gh[2][3];
+            // gate pre-activations: r and z sum the input and hidden products in one
+            // accumulator; n keeps them apart (n = tanh(i_n + r * h_n))
+            // accumulators start from the biases: r, z from b_i + b_h; n's halves apart
+            const int u = 16 * hb + 4 * q;
+            const float4 bir = *reinterpret_cast<const float4 *>(bih + u);
+            const float4 biz = *reinterpret_cast<const float4 *>(bih + kHid + u);
+            const float4 bin = *reinterpret_cast<const float4 *>(bih + 2 * kHid + u);
+            const float4 bhr = *reinterpret_cast<const float4 *>(bhh + u);
+            const float4 bhz = *reinterpret_cast<const float4 *>(bhh + kHid + u);
+            const float4 bhn = *reinterpret_cast<const float4 *>(bhh + 2 * kHid + u);
+            const f32x4 r0 = {bir.x + bhr.x, bir.y + bhr.y, bir.z + bhr.z, bir.w + bhr.w};
+            const f32x4 z0 = {biz.x + bhz.x, biz.y + bhz.y, biz.z + bhz.z, biz.w + bhz.w};
+            f32x4 gr[2], gz[2], gni[2], gnh[2];
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
+            for (int nt = 0; nt < 2; ++nt) {
+                gr[nt] = r0;
+                gz[nt] = z0;
+                gni[nt] = f32x4{bin.x, bin.y, bin.z, bin.w};
+                gnh[nt] = f32x4{bhn.x, bhn.y, bhn.z, bhn.w};
+            }
 #pragma unroll
-                for (int g = 0; g < 3; ++g) gi[rt][g] = gh[rt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-            float4 bi[3], bh[3];
-            auto wload = [&](int t, float4 (&wi)[3], float4 (&wh)[3]) {
+            for (int t = 0; t < 4; ++t) {
+                float4 wc[6];
 #pragma unroll
                 for (int g = 0; g < 3; ++g) {
-                    wi[g] = Wihp[pk(t, 4 * g + hb, 12, lane)];
-                    wh[g] = Whhp[pk(t, 4 * g + hb, 12, lane)];
-                }
-            };
-            wload(0, bi, bh);
-            for (int t = 0; t < kHid / 16; ++t) {
-                float4 ax[2], ah[2], ci[3], ch[3];
-#pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    ci[g] = bi[g];
-                    ch[g] = bh[g];
-                }
-                if (t + 1 < kHid / 16) wload(t + 1, bi, bh);  // weights of the next chunk in flight
-#pragma unroll
-                for (int rt = 0; rt < 2; ++rt) {
-                    ax[rt] = *reinterpret_cast<const float4 *>(sx + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
-                    ah[rt] = *reinterpret_cast<const float4 *>(sh + (16 * rt + r) * kLdsStride + 16 * t + 4 * q);
+                    wc[g] = Wihp[pk(t, 4 * g + hb, 12, lane)];
+                    wc[3 + g] = Whhp[pk(t, 4 * g + hb, 12, lane)];
                 }
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                        for (int g = 0; g < 3; ++g) {
-                            gi[rt][g] = mfma4(comp(ax[rt], e), comp(ci[g], e), gi[rt][g]);
-                            gh[rt][g] = mfma4(comp(ah[rt], e), comp(ch[g], e), gh[rt][g]);
-                        }
+                    for (int nt = 0; nt < 2; ++nt) {
+                        gr[nt] = mfma4(comp(wc[0], e), xB[t][nt][e], gr[nt]);
+                        gz[nt] = mfma4(comp(wc[1], e), xB[t][nt][e], gz[nt]);
+                        gni[nt] = mfma4(comp(wc[2], e), xB[t][nt][e], gni[nt]);
+                        gr[nt] = mfma4(comp(wc[3], e), comp(hB[t][nt], e), gr[nt]);
+                        gz[nt] = mfma4(comp(wc[4], e), comp(hB[t][nt], e), gz[nt]);
+                        gnh[nt] = mfma4(comp(wc[5], e), comp(hB[t][nt], e), gnh[nt]);
+                    }
             }
-            const float bir = bih[u], biz = bih[kHid + u], bin = bih[2 * kHid + u];
-            const float bhr = bhh[u], bhz = bhh[kHid + u], bhn = bhh[2 * kHid + u];
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const float h = sh[(16 * rt + 4 * q + v) * kLdsStride + u];
-                    const float rg = sigmoidf_((gi[rt][0][v] + bir) + (gh[rt][0][v] + bhr));
-                    const float zg = sigmoidf_((gi[rt][1][v] + biz) + (gh[rt][1][v] + bhz));
-                    const float ng = tanhf((gi[rt][2][v] + bin) + rg * (gh[rt][2][v] + bhn));
-                    hp[rt][v] = ng + zg * (h - ng);
+                    const float rg = sigmoidf_(gr[nt][v]);
+                    const float zg = sigmoidf_(gz[nt][v]);
+                    const float ng = tanhf_(gni[nt][v] + rg * gnh[nt][v]);
+                    hp[hb][nt][v] = ng + zg * (comp(hB[hb][nt], v) - ng);
                 }
         } else {
-            f32x4 a2[2][1];
-            a2[0][0] = a2[1][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-            gemm_lds_a<1>(a2, sx, kLdsStride, Wihp, 4, hb, kHid);
-            const float bb = bih[u];
+            const float4 bb = *reinterpret_cast<const float4 *>(bih + 16 * hb + 4 * q);
+            f32x4 a2[2] = {f32x4{bb.x, bb.y, bb.z, bb.w}, f32x4{bb.x, bb.y, bb.z, bb.w}};
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
+            for (int t = 0; t < 4; ++t) {
+                const float4 w = Wihp[pk(t, hb, 4, lane)];
 #pragma unroll
-                for (int v = 0; v < 4; ++v) hp[rt][v] = fmaxf(a2[rt][0][v] + bb, 0.f);
-        }
-        // h' block: to HBM (hidden-state output) and to the LDS stage as fc2's A operand
+                for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int rr = 16 * rt + 4 * q + v;
-                sp[rr * kStageStride + r] = hp[rt][v];
-                if (row0 + rr < R) Hout[(row0 + rr) * kHid + u] = hp[rt][v];
+                    for (int nt = 0; nt < 2; ++nt) a2[nt] = mfma4(comp(w, e), xB[t][nt][e], a2[nt]);
             }
-        wave_sync();
-        // q += h'[:, block] W2[:, block]^T   (K = 16: one chunk)
-        {
-            float4 a4[2], b4[NQ];
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-                a4[rt] = *reinterpret_cast<const float4 *>(sp + (16 * rt + r) * kStageStride + 4 * q);
+            for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int c = 0; c < NQ; ++c) b4[c] = W2p[pk(hb, c, NQ, lane)];
+                for (int v = 0; v < 4; ++v) hp[hb][nt][v] = fmaxf(a2[nt][v], 0.f);
+        }
+        // h' block -> HBM (the new hidden state), one float4 per lane and row
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+            if (ok[nt])
+                *reinterpret_cast<float4 *>(Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
+                    make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
+    }
+
+    // ---- selection state: (env, agent) of each row, running argmax, availability bits ----
+    const uint8_t *arow[2] = {nullptr, nullptr};
+    bool av4 = false;
+    float best[2] = {-__builtin_inff(), -__builtin_inff()};
+    int bj[2] = {0x7fffffff, 0x7fffffff};
+    uint64_t amask[2] = {0, 0};  // bit 4c + v <-> task 16 c + 4 q + v
+    int64_t oidx[2] = {0, 0};
+    if (SEL) {
+        const int64_t b0 = row0 / sel.n;
+        const int i0 = (int)(row0 - b0 * sel.n);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            int64_t b = b0;
+            int i = i0 + 16 * nt + r;
+            while (i >= sel.n) {
+                i -= sel.n;
+                ++b;
+            }
+            arow[nt] = sel.avail + (ok[nt] ? b * sel.a0 + (int64_t)i * sel.a1 : 0);
+            oidx[nt] = b * sel.o0 + (int64_t)i * sel.o1;
+        }
+        av4 = ((reinterpret_cast<uintptr_t>(sel.avail) | (uintptr_t)sel.a0 | (uintptr_t)sel.a1) & 3u) == 0;
+    }
+
+    // ---- fc2 one 16-output tile at a time: q^T = W2 h'^T + b2; Q store and/or argmax ----
+    const int nct = nout / 16;
+    for (int c = 0; c < nct; ++c) {
+        uint32_t av[2] = {0u, 0u};  // 4 availability bits of this lane's tasks, per row
+        if (SEL) {
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const uint8_t *ap = arow[nt] + 16 * c + 4 * q;
+                uint32_t w = 0;
+                if (ok[nt]) {
+                    if (av4) {
+                        w = *reinterpret_cast<const uint32_t *>(ap);
+                    } else {
+                        w = (uint32_t)ap[0] | ((uint32_t)ap[1] << 8) | ((uint32_t)ap[2] << 16) | ((uint32_t)ap[3] << 24);
+                    }
+                }
+                av[nt] = ((w & 0xffu) != 0) | (((w >> 8) & 0xffu) != 0) << 1 | (((w >> 16) & 0xffu) != 0) << 2 |
+                         ((w >> 24) != 0) << 3;
+            }
+        }
+        const float4 bq = *reinterpret_cast<const float4 *>(b2 + 16 * c + 4 * q);
+        f32x4 a2[2] = {f32x4{bq.x, bq.y, bq.z, bq.w}, f32x4{bq.x, bq.y, bq.z, bq.w}};
+        float4 w2[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w2[t] = W2p[pk(t, c, nct, lane)];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
+                for (int nt = 0; nt < 2; ++nt) a2[nt] = mfma4(comp(w2[t], e), hp[t][nt][e], a2[nt]);
 #pragma unroll
-                    for (int c = 0; c < NQ; ++c) aq[rt][c] = mfma4(comp(a4[rt], e), comp(b4[c], e), aq[rt][c]);
-        }
-        wave_sync();  // the stage is rewritten by the next block
-    }
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            const float bb = b2[16 * c + r];
-#pragma unroll
-            for (int v = 0; v < 4; ++v) aq[rt][c][v] += bb;
-        }
-    if (Q) {
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int c = 0; c < NQ; ++c)
+        for (int nt = 0; nt < 2; ++nt) {
+            if (Q && ok[nt])
+                *reinterpret_cast<float4 *>(Q + rows[nt] * nout + 16 * c + 4 * q) =
+                    make_float4(a2[nt][0], a2[nt][1], a2[nt][2], a2[nt][3]);
+            if (SEL) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const int64_t row = row0 + 16 * rt + 4 * q + v;
-                    if (row < R) Q[row * nout + 16 * c + r] = aq[rt][c][v];
+                    const int j = 16 * c + 4 * q + v;
+                    const float x = ((av[nt] >> v) & 1u) ? a2[nt][v] : -__builtin_inff();
+                    const bool b = better(x, j, best[nt], bj[nt]);
+                    best[nt] = b ? x : best[nt];
+                    bj[nt] = b ? j : bj[nt];
                 }
+                amask[nt] |= (uint64_t)av[nt] << (4 * c);
+            }
+        }
     }
-    if (SEL) {
-        // the 16 lanes of a DPP row (same q) hold the nout Q-values of one agent row
+    if (!SEL) return;
+
+    // ---- reduce each row over its 4 lanes (q = 0..3: lane ^ 16, lane ^ 32) -------------
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
+    for (int nt = 0; nt < 2; ++nt) {
+        auto red = [&](auto swp) {
+            const SwapPair pb = swp(__builtin_bit_cast(uint32_t, best[nt]));
+            const SwapPair pj = swp((uint32_t)bj[nt]);
+            float vb = __builtin_bit_cast(float, pb.a);
+            int jb = (int)pj.a;
+            if (better(__builtin_bit_cast(float, pb.b), (int)pj.b, vb, jb)) {
+                vb = __builtin_bit_cast(float, pb.b);
+                jb = (int)pj.b;
+            }
+            best[nt] = vb;
+            bj[nt] = jb;
+        };
+        red(swap16);
+        red(swap32);
+    }
+    // lane q == nt finishes row nt: greedy action, or with probability epsilon the
+    // target-th available task in index order (Categorical over avail, as asg_select.hip)
+    const int nt = q & 1;
+    const int64_t row = rows[nt];
+    int action = bj[nt] == 0x7fffffff ? 0 : bj[nt];
+    bool explore = false;
+    u32x4 rr = u32x4{0u, 0u, 0u, 0u};
+    if (sel.epsilon > 0.0f) {
+        rr = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect, sel.counter}, sel.k0, sel.k1);
+        constexpr float k2m24 = 5.9604644775390625e-08f;
+        explore = ok[nt] && q < 2 && (float)(rr.x >> 8) * k2m24 < sel.epsilon;
+    }
+    if (__ballot(explore)) {  // some row of the wave explores (about epsilon of the rows)
+        // Per 64-task window: the row's availability in task order, assembled from its 4
+        // lanes (task 16 c + 4 q + v is bit 4 c + v of lane q's slice) with two swaps;
+        // the exploring lane then takes the target-th set bit by a popcount bisection.
+        const int nwin = (nct + 3) / 4;
+        int target = -1, found = -1;
+        for (int ntt = 0; ntt < 2; ++ntt) {
+            const bool mine_row = explore && nt == ntt;
+            int cnt = __popcll(amask[ntt]);
+            {
+                const SwapPair c16 = swap16((uint32_t)cnt);
+                const SwapPair c32 = swap32(c16.a + c16.b);
+                cnt = (int)(c32.a + c32.b);
+            }
+            if (mine_row) {
+                if (cnt == 0) atomicCAS(sel.err, 0, ASG_E_INVALID_ARG);
+                else target = (int)(((uint64_t)rr.y * (uint64_t)cnt) >> 32);
+            }
+            for (int w = 0; w < nwin; ++w) {
+                const uint32_t mine = (uint32_t)(amask[ntt] >> (16 * w)) & 0xFFFFu;
+                uint32_t lo = 0, hi = 0;  // this lane's tasks of the window, in task order
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int64_t row = row0 + 16 * rt + 4 * q + v;
-                const bool live = row < R;
-                int64_t b;
-                int i;
-                env_agent(16 * rt + 4 * q + v, b, i);
-                float best = -__builtin_inff();
-                int bj = 0x7fffffff;
-                uint32_t rowmask[NQ];  // availability bits of this row, task 16c + lane-in-row
+                for (int c = 0; c < 2; ++c) lo |= ((mine >> (4 * c)) & 0xFu) << (16 * c + 4 * q);
 #pragma unroll
-                for (int c = 0; c < NQ; ++c) {
-                    const int col = 16 * c + r;
-                    const bool av = live && ((avbits >> ((rt * 4 + v) * 4 + c)) & 1u);
-                    rowmask[c] = (uint32_t)(__ballot(av) >> (16 * q)) & 0xFFFFu;
-                    const float x = av ? aq[rt][c][v] : -__builtin_inff();
-                    if (better(x, col, best, bj)) {
-                        best = x;
-                        bj = col;
-                    }
-                }
-                auto red = [&](auto perm) {
-                    const float ob = __builtin_bit_cast(float, perm(__builtin_bit_cast(uint32_t, best)));
-                    const int oj = (int)perm((uint32_t)bj);
-                    if (better(ob, oj, best, bj)) {
-                        best = ob;
-                        bj = oj;
-                    }
-                };
-                red([](uint32_t x) { return dpp32<0xB1>(x); });
-                red([](uint32_t x) { return dpp32<0x4E>(x); });
-                red([](uint32_t x) { return dpp32<0x141>(x); });
-                red([](uint32_t x) { return dpp32<0x140>(x); });
-                int action = bj == 0x7fffffff ? 0 : bj;
-                if (r == 0 && live) {
-                    if (sel.epsilon > 0.0f) {
-                        const u32x4 rr = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect,
-                                                             sel.counter}, sel.k0, sel.k1);
-                        constexpr float k2m24 = 5.9604644775390625e-08f;
-                        if ((float)(rr.x >> 8) * k2m24 < sel.epsilon) {  // explore: Categorical(avail)
-                            // tasks in index order j = 16 c + bit, from the row's ballot masks
-                            int cnt = 0;
+                for (int c = 2; c < 4; ++c) hi |= ((mine >> (4 * c)) & 0xFu) << (16 * (c - 2) + 4 * q);
+                const SwapPair l16 = swap16(lo), h16 = swap16(hi);
+                const SwapPair l32 = swap32(l16.a | l16.b), h32 = swap32(h16.a | h16.b);
+                uint64_t row_mask = (uint64_t)(l32.a | l32.b) | ((uint64_t)(h32.a | h32.b) << 32);
+                if (mine_row && target >= 0) {
+                    const int pc = __popcll(row_mask);
+                    if (target < pc) {
+                        int k = target, pos = 0;
 #pragma unroll
-                            for (int c = 0; c < NQ; ++c) cnt += __popc(rowmask[c]);
-                            if (cnt == 0) {
-                                atomicCAS(sel.err, 0, ASG_E_INVALID_ARG);
-                            } else {
-                                int target = (int)(((uint64_t)rr.y * (uint64_t)cnt) >> 32);
-#pragma unroll
-                                for (int c = 0; c < NQ; ++c) {
-                                    const int pc = __popc(rowmask[c]);
-                                    if (target >= 0 && target < pc) {
-                                        uint32_t msk = rowmask[c];
-                                        for (int k = 0; k < target; ++k) msk &= msk - 1;  // drop lowest bits
-                                        action = 16 * c + __builtin_ctz(msk);
-                                    }
-                                    target -= pc;
-                                }
-                            }
+                        for (int half = 32; half >= 1; half >>= 1) {
+                            const uint64_t low = row_mask & ((1ull << half) - 1ull);
+                            const int lc = __popcll(low);
+                            const bool up = k >= lc;
+                            k -= up ? lc : 0;
+                            pos += up ? half : 0;
+                            row_mask = up ? (row_mask >> half) : low;
                         }
+                        found = 64 * w + pos;
+                        target = -1;
+                    } else {
+                        target -= pc;
                     }
-                    sel.out[b * sel.o0 + (int64_t)i * sel.o1] = action;
                 }
             }
+        }
+        if (found >= 0) action = found;
+    }
+    if (q < 2 && ok[nt]) sel.out[oidx[nt]] = action;
+}
+
+// One wave per 32 rows, weights read through L1/L2 (any n_out).
+template <bool RNN, bool SEL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AGENT_WAVES))) rnn_agent_fwd_kernel(
+    const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
+    const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
+    const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
+    const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
+    float *__restrict__ Q, SelectArgs sel) {
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
+    agent_rows<RNN, SEL>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel);
+}
+
+// Persistent variant: one 512-thread workgroup per CU copies the recurrent and output
+// weights (packed fragments) into LDS once, then its 8 waves walk 256-row tiles; the
+// gate and fc2 A operands become conflict-free ds_read_b128 instead of L2 round trips.
+constexpr int kLdsWaves = 8;
+template <bool RNN, bool SEL>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rnn_agent_lds_kernel(
+    const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
+    const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
+    const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,
+    float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel) {
+    extern __shared__ float4 s_w[];
+    for (int64_t i = threadIdx.x; i < nrf4; i += blockDim.x) s_w[i] = Wrp[i];
+    __syncthreads();
+    const float4 *Wih = s_w;
+    const float4 *Whh = s_w + (RNN ? 4 * 12 * 64 : 4 * 4 * 64);
+    const float4 *W2 = RNN ? Whh + 4 * 12 * 64 : Whh;
+    const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
+        agent_rows<RNN, SEL>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel);
     }
 }
 
@@ -420,33 +461,53 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     return hipGetLastError();
 }
 
+// ASG_AGENT_LDS_WEIGHTS=0 selects the L2-weight kernel (A/B experiments)
+static bool use_lds_weights() {
+    static const int v = [] {
+        const char *e = getenv("ASG_AGENT_LDS_WEIGHTS");
+        return e ? atoi(e) : 1;
+    }();
+    return v != 0;
+}
+
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
                                 const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                 const float *b2, int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel,
                                 hipStream_t s) {
     const int64_t rows_per_block = 4 * kRowsPerWave;
     const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
-    const size_t lds = sizeof(float) * 4 * kWaveLds;
     const float4 *W1p = packed;
     const float4 *Wihp = W1p + (int64_t)((K + 15) / 16) * 4 * 64;
     const float4 *Whhp = Wihp + (use_rnn ? 4 * 12 * 64 : 4 * 4 * 64);
     const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
     const SelectArgs sa = sel ? *sel : SelectArgs{};
-#define L_(RNN, NQ, SEL)                                                                                      \
-    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, NQ, SEL>), dim3(blocks), dim3(256), lds, s, X, xs, R, K, Hin, hs, \
-                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, Hout, Q, sa)
-#define NQ_(RNN, SEL)                   \
-    if (nq == 1) L_(RNN, 1, SEL);       \
-    else if (nq == 2) L_(RNN, 2, SEL);  \
-    else if (nq == 3) L_(RNN, 3, SEL);  \
-    else L_(RNN, 4, SEL);
-    const int nq = nout / 16;
-    if (use_rnn) {
-        if (sel) { NQ_(true, true) } else { NQ_(true, false) }
-    } else {
-        if (sel) { NQ_(false, true) } else { NQ_(false, false) }
+    // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU)
+    const int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)(nout / 16) * 64;
+    const size_t lds = (size_t)nrf4 * sizeof(float4);
+    if (use_lds_weights() && lds <= 160 * 1024) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
+        const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
+#define LL_(RNN, SEL)                                                                                              \
+    hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, Hin, \
+                       hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa)
+        if (use_rnn) {
+            if (sel) LL_(true, true); else LL_(true, false);
+        } else {
+            if (sel) LL_(false, true); else LL_(false, false);
+        }
+#undef LL_
+        return hipGetLastError();
     }
-#undef NQ_
+#define L_(RNN, SEL)                                                                                          \
+    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, SEL>), dim3(blocks), dim3(256), 0, s, X, xs, R, K, Hin, hs, \
+                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa)
+    if (use_rnn) {
+        if (sel) L_(true, true); else L_(true, false);
+    } else {
+        if (sel) L_(false, true); else L_(false, false);
+    }
 #undef L_
     return hipGetLastError();
 }

@@ -51,12 +51,11 @@ __device__ __forceinline__ double bump_value(double scale, double center, double
 // purposes of Philox counters (counter.z); counter.w = episode
 enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u };
 
-// "a beats b" in torch.max order: NaN wins, then larger value, then smaller index
+// "a beats b" in torch.max order: NaN wins, then larger value, then smaller index.
+// Branch-free (bitwise on the predicates) so it lowers to compares + v_cndmask.
 __device__ __forceinline__ bool better(float va, int ja, float vb, int jb) {
-    const bool na = va != va, nb = vb != vb;
-    if (na != nb) return na;
-    if (na) return ja < jb;
-    return va > vb || (va == vb && ja < jb);
+    const bool na = va != va, nb = vb != vb, lt = ja < jb;
+    return (na & (!nb | lt)) | (!nb & ((va > vb) | ((va == vb) & lt)));
 }
 
 // Key of one env's stream: seed and global env index (a 1-GPU run and an

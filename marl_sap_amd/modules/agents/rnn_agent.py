@@ -37,13 +37,14 @@ class RNNAgent(nn.Module):
 class RNNFusedAgent(RNNAgent):
     """RNNAgent with the same parameters / state_dict, whose inference forward (no autograd:
     the rollout's action selection) is one fused HIP kernel (asg_rnn_agent_forward: f32
-    MFMA, fc1 + GRUCell + fc2 with every intermediate on chip).  With autograd enabled
+    MFMA, fc1 + GRUCell + fc2 with every intermediate in registers; hidden 64, n_out a
+    multiple of 16 up to 256).  With autograd enabled
     (learner training) it is the plain PyTorch module, so gradients are unchanged."""
 
     def __init__(self, input_shape, args):
         super().__init__(input_shape, args)
-        if args.hidden_dim != 64 or args.m % 16 != 0 or args.m > 64 or input_shape % 4 != 0:
-            raise ValueError("rnn_fused needs hidden_dim == 64, m in {16, 32, 48, 64} and an input size "
+        if args.hidden_dim != 64 or args.m % 16 != 0 or args.m > 256 or input_shape % 4 != 0:
+            raise ValueError("rnn_fused needs hidden_dim == 64, m a multiple of 16 up to 256 and an input size "
                              "divisible by 4; use agent 'rnn'")
 
     def _prep(self, inputs, hidden_state):

@@ -17,7 +17,8 @@ DEV = torch.device("cuda", 0)
 
 @pytest.mark.parametrize("R,K,m,use_rnn,hidden", [
     (64 * 256, 256, 64, True, "zero"), (4096 + 37, 256, 64, True, "dense"), (1000, 68, 16, True, "dense"),
-    (513, 256, 48, False, "zero"), (2048, 128, 32, False, "dense"), (31, 20, 64, True, "dense")])
+    (513, 256, 48, False, "zero"), (2048, 128, 32, False, "dense"), (31, 20, 64, True, "dense"),
+    (2000 + 5, 1024, 256, True, "dense"), (777, 512, 128, False, "dense"), (96, 1024, 256, True, "zero")])
 def test_fused_agent_matches_pytorch(R, K, m, use_rnn, hidden):
     torch.manual_seed(R + K)
     args = SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m)
@@ -61,19 +62,21 @@ def test_fused_agent_reads_time_major_obs_slab():
     assert torch.equal(q1.view(E, n, m).max(2)[1], q0.view(E, n, m).max(2)[1])
 
 
-@pytest.mark.parametrize("eps", [0.0, 0.3])
-def test_fused_select_equals_forward_then_selector(eps):
+@pytest.mark.parametrize("eps,B,n,m,K,use_rnn", [
+    (0.0, 300, 64, 64, 256, True), (0.3, 300, 64, 64, 256, True), (0.5, 37, 5, 48, 192, False),
+    (0.4, 50, 8, 256, 1024, True), (1.0, 21, 3, 16, 64, True), (0.3, 40, 7, 144, 576, True)])
+def test_fused_select_equals_forward_then_selector(eps, B, n, m, K, use_rnn):
     """asg_rnn_agent_select == asg_rnn_agent_forward followed by asg_epsilon_greedy with
-    the same Philox (seed, counter): same actions, same hidden state."""
+    the same Philox (seed, counter): same actions, same hidden state (ragged row counts,
+    n_out beyond one 64-task window, random availability)."""
     from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector
-    B, n, m, K = 300, 64, 64, 256
     torch.manual_seed(1)
-    args = SimpleNamespace(hidden_dim=64, use_rnn=True, m=m, epsilon_start=eps, epsilon_finish=eps,
+    args = SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m, epsilon_start=eps, epsilon_finish=eps,
                            epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=5)
     agent = RNNFusedAgent(K, args).to(DEV)
     x = torch.randn((B * n, K), device=DEV)
     h = torch.randn((B * n, 64), device=DEV)
-    avail = torch.rand((B, n, m), device=DEV) > 0.2
+    avail = torch.rand((B, n, m), device=DEV) > (0.2 if m <= 64 else 0.7)
     avail[..., 3] = True
     sel = EpsilonGreedyActionSelector(args)
     with torch.no_grad():
