@@ -42,6 +42,31 @@ def step_bytes(n, m, L):
     return n * m * (4 * (L + 1) + 4 + 1 + 8) + n * (8 + 4 + 8) + 1 + 8
 
 
+F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (= f32 vector peak; MI355X_MICROARCH.md)
+
+
+def agent_flops(n, m, L, hidden=64, use_rnn=True):
+    """Algorithmic flops of one agent row: fc1 (m(L+1) -> hidden), GRUCell (two hidden x
+    3*hidden products), fc2 (hidden -> m); 2 flops per multiply-add."""
+    K = m * (L + 1)
+    rec = 2 * 3 * hidden * hidden if use_rnn else hidden * hidden
+    return 2 * (K * hidden + rec + hidden * m)
+
+
+def agent_roofline(a, E, sel_ms):
+    """The action-selection launch (fused agent forward + epsilon-greedy, or the PyTorch
+    agent + selector kernel), timed with HIP events on its stream, against the f32 MFMA
+    peak: the kernel that takes most of each step's time next to the env step."""
+    if a.selector == "random" or sel_ms <= 0:
+        return None
+    flops = agent_flops(a.n, a.m, a.L) * E * a.n
+    tfs = flops / (sel_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "traffic": None,
+            "kernel": "asg::rnn_agent_lds_kernel" if a.agent == "rnn_fused" else "torch agent + selector",
+            "kernel_ms": round(sel_ms, 4), "flops_per_launch": flops}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -122,6 +147,7 @@ def main():
     runner.setup(env.scheme, {"agents": a.n}, env.preprocess, mac)
 
     ev_pairs = []   # (start, end) HIP events around each env step kernel in the timed region
+    sel_pairs = []  # ... and around each action selection (agent forward + selector)
     state = {"t": a.T, "timing": False}
 
     def one_step():
@@ -134,10 +160,16 @@ def main():
             state["t"] = 0
         t = state["t"]
         with torch.no_grad():
+            if state["timing"]:
+                a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a0.record()
             if a.selector == "random":
                 env.random_actions(runner.batch, ts=t)
             else:
                 runner.select_into_batch(t)
+            if state["timing"]:
+                a1.record()
+                sel_pairs.append((a0, a1))
             if state["timing"]:
                 s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s0.record()
@@ -163,12 +195,15 @@ def main():
     if runner.env.k == a.T:
         runner.finish_episode()  # surfaces any sticky device error of the timed steps
     kern_ms = sum(s.elapsed_time(e) for s, e in ev_pairs) / max(1, len(ev_pairs))
+    sel_ms = sum(s.elapsed_time(e) for s, e in sel_pairs) / max(1, len(sel_pairs))
 
     if world > 1:
         import torch.distributed as tdist
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, sel_ms], dtype=torch.float64, device=dev)
+        if tdist.get_backend() == "gloo":
+            t = t.cpu()
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, sel_ms = float(t[0]), float(t[1]), float(t[2])
 
     total_steps = world * E * a.steps
     value = total_steps / elapsed
@@ -200,6 +235,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "asg::step_kernel", "kernel_ms": round(kern_ms, 4),
                          "bytes_per_launch": per_launch},
+            "roofline_agent": agent_roofline(a, E, sel_ms),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
