@@ -64,6 +64,8 @@ enum asg_dtype {
     ASG_I64 = 2,
     ASG_I32 = 3,
     ASG_BOOL = 4, /* 1 byte, torch.bool */
+    ASG_F16 = 5,  /* IEEE half (RealConstellationEnv scheme) */
+    ASG_I16 = 6,
 };
 
 /* A strided view of one EpisodeBatch field.  ptr addresses element [0, 0, 0, 0] of the
@@ -221,6 +223,42 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
                          const int64_t avail_strides[2], int n, double epsilon, uint64_t seed,
                          uint64_t counter, int64_t *out, const int64_t out_strides[2],
                          int32_t *status, void *hip_stream);
+
+/* ==== RealConstellationEnv ======================================
+ * Batched form of src/envs/real_constellation_env.py with injected benefits
+ * (sat_prox_mat + graphs given: the constant-benefit path, :55-61).  Replaces
+ * RealConstellationEnv.reset (:100-114), .step (:135-175), ._build_obs (:177-230),
+ * .get_pretransition_data (:232-245) and .beta_hat (:259-327) for E envs per handle.
+ * Batch fields use the reference scheme (:80-97): obs f16 [B,T+1,n,obs_size],
+ * actions i16 [B,T+1,n,1], avail bool [B,T+1,n,m], rewards f16 [B,T+1,n] (one vector
+ * per env), terminated bool, prev_assigns i16 [B,T+1,n], beta f16 [B,T+1,n,m,L]
+ * (the asg_field strides cover (B, T+1, n, m); L must be contiguous), actions_onehot
+ * i16 [B,T+1,n,m], filled i64.  Wider float / int dtypes are accepted too.
+ * np.argsort ties (unspecified order in numpy) are broken by the lower index. */
+typedef struct asg_real_handle asg_real_handle;
+
+typedef struct {
+    int64_t num_envs;
+    int32_t n, m, T, L;        /* n = num_planes * num_sats_per_plane (n <= m); L = min(L, T) */
+    int32_t N, M;              /* competitors and tasks in the observation; M even */
+    double lambda_;
+    const double *T_trans;     /* host [m][m] or NULL (= 1 - I) */
+    const double *task_prios;  /* host [m] or NULL (= ones) */
+} asg_real_config;
+
+int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, asg_real_handle **out);
+void asg_real_destroy(asg_real_handle *h);
+int asg_real_set_stream(asg_real_handle *h, void *hip_stream);
+/* sat_prox_mat float64 [count][n][m][T] (reference layout), count = 1 (shared by every
+ * env, the reference's constant benefits) or num_envs; host or device memory. */
+int asg_real_set_benefits(asg_real_handle *h, const double *table, int64_t count, int on_device);
+int asg_real_reset(asg_real_handle *h, const asg_batch_view *view, int ts);
+int asg_real_step(asg_real_handle *h, const asg_batch_view *view, int ts);
+int asg_real_sync_status(asg_real_handle *h);
+int asg_real_get_returns(asg_real_handle *h, double *out_device); /* float64 [E] */
+int asg_real_get_step(const asg_real_handle *h, int *k_out);
+/* get_obs_size (:251-253): M*L + N*M*L + (N*M//2)*L + M */
+int asg_real_obs_size(int N, int M, int L);
 
 #ifdef __cplusplus
 }

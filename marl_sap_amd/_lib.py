@@ -20,7 +20,7 @@ ASG_E_LSA_INVALID = -4
 ASG_E_LSA_INFEASIBLE = -5
 ASG_E_ACTION_RANGE = -6
 
-ASG_F32, ASG_F64, ASG_I64, ASG_I32, ASG_BOOL = 0, 1, 2, 3, 4
+ASG_F32, ASG_F64, ASG_I64, ASG_I32, ASG_BOOL, ASG_F16, ASG_I16 = 0, 1, 2, 3, 4, 5, 6
 ASG_RNG_PHILOX, ASG_RNG_MT19937 = 0, 1
 ASG_BENEFIT_BUMP, ASG_BENEFIT_DENSE, ASG_BENEFIT_INJECTED = 0, 1, 2
 ASG_QUIRK_PREV_ASSIGNS_ZERO = 0x1
@@ -28,7 +28,7 @@ ASG_QUIRK_PARALLEL_TERMINATED = 0x2
 ASG_QUIRK_REPLICATE_STREAM = 0x4
 
 _DTYPES = {torch.float32: ASG_F32, torch.float64: ASG_F64, torch.int64: ASG_I64,
-           torch.int32: ASG_I32, torch.bool: ASG_BOOL}
+           torch.int32: ASG_I32, torch.bool: ASG_BOOL, torch.float16: ASG_F16, torch.int16: ASG_I16}
 
 # every symbol include/asg.h declares (checked by tests/test_abi.py)
 EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "asg_set_stream",
@@ -36,7 +36,9 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_export_benefits", "asg_export_prev_assigns", "asg_get_returns", "asg_get_step",
            "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_epsilon_greedy",
            "asg_rnn_agent_packed_size", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
-           "asg_rnn_agent_select"]
+           "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
+           "asg_real_set_benefits", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
+           "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size"]
 
 
 class AsgField(ctypes.Structure):
@@ -59,6 +61,13 @@ class AsgConfig(ctypes.Structure):
                 ("benefit_mode", ctypes.c_int32), ("quirks", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64), ("env_index_base", ctypes.c_int64),
                 ("T_trans", ctypes.POINTER(ctypes.c_double))]
+
+
+class AsgRealConfig(ctypes.Structure):
+    _fields_ = [("num_envs", ctypes.c_int64), ("n", ctypes.c_int32), ("m", ctypes.c_int32),
+                ("T", ctypes.c_int32), ("L", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32),
+                ("lambda_", ctypes.c_double), ("T_trans", ctypes.POINTER(ctypes.c_double)),
+                ("task_prios", ctypes.POINTER(ctypes.c_double))]
 
 
 _lib = None
@@ -101,8 +110,19 @@ def lib():
         L.asg_rnn_agent_select.argtypes = [vp, i64, i64, i32, vp, i64] + [vp] * 5 + [i32, i32, i32, vp, vp, vp, i64p,
                                                                                  i32, dbl, ctypes.c_uint64,
                                                                                  ctypes.c_uint64, vp, i64p, vp, vp]
+        L.asg_real_create.argtypes = [ctypes.POINTER(AsgRealConfig), i32, vp, ctypes.POINTER(vp)]
+        L.asg_real_destroy.argtypes = [vp]
+        L.asg_real_destroy.restype = None
+        L.asg_real_set_stream.argtypes = [vp, vp]
+        L.asg_real_set_benefits.argtypes = [vp, vp, i64, i32]
+        L.asg_real_reset.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
+        L.asg_real_step.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
+        L.asg_real_sync_status.argtypes = [vp]
+        L.asg_real_get_returns.argtypes = [vp, vp]
+        L.asg_real_get_step.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+        L.asg_real_obs_size.argtypes = [i32, i32, i32]
         for f in EXPORTS:
-            if f not in ("asg_last_error",):
+            if f not in ("asg_last_error", "asg_real_destroy"):
                 getattr(L, f).restype = i32
         L.asg_rnn_agent_packed_size.restype = i64
         if L.asg_abi_version() != 1:
@@ -131,15 +151,18 @@ def i64arr(vals):
 
 
 def field(t):
-    """asg_field of a tensor of up to 4 dims ([B, T+1, d2, d3]); None -> absent."""
+    """asg_field of a tensor of up to 4 dims ([B, T+1, d2, d3]), or 5 dims with a
+    contiguous last dim (the real env's beta [B, T+1, n, m, L]); None -> absent."""
     f = AsgField()
     if t is None:
         f.ptr = None
         return f
     if not t.is_cuda:
         raise ValueError("EpisodeBatch tensors handed to the HIP env must live on the GPU")
+    if t.dim() == 5 and t.stride(-1) == 1:
+        t = t.select(-1, 0)
     if t.dim() > 4:
-        raise ValueError("batch fields have at most 4 dims")
+        raise ValueError("batch fields have at most 4 dims (or 5 with a contiguous last dim)")
     f.ptr = t.data_ptr()
     f.dtype = _DTYPES[t.dtype]
     st = list(t.stride()) + [1] * (4 - t.dim())

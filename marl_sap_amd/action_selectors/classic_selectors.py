@@ -58,7 +58,7 @@ class EpsilonGreedyActionSelector:
             self.epsilon = self.args.evaluation_epsilon
         q = agent_inputs if agent_inputs.dtype == torch.float32 else agent_inputs.float()
         B, n, m = q.shape
-        if out is None:
+        if out is None or out.dtype != torch.int64:
             out = torch.empty((B, n), dtype=torch.int64, device=q.device)
         av = avail_actions if avail_actions.dtype == torch.bool else avail_actions != 0
         if self.status is None or self.status.device != q.device:

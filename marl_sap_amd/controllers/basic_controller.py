@@ -33,6 +33,8 @@ class BasicMAC:
         """`out` (optional, int64 [B, n]): selectors that support it write the actions
         there in place (the runner passes the EpisodeBatch actions row)."""
         avail_actions = ep_batch["avail_actions"][:, t_ep]
+        if out is not None and out.dtype != torch.int64:
+            out = None  # e.g. the real env's int16 actions: the caller casts through update()
         if out is not None and self._fused_select_ok(bs):
             # agent forward + epsilon-greedy in one HIP kernel: Q never leaves the chip
             eps, seed, counter, status = self.action_selector.fused_params(t_env, test_mode, out.device)

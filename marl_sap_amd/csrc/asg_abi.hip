@@ -73,6 +73,8 @@ int check_view(asg_handle *h, const asg_batch_view *b, int ts, bool step) {
 
 }  // namespace
 
+void asg::set_last_error(const std::string &msg) { g_err = msg; }
+
 extern "C" {
 
 int asg_abi_version(void) { return ASG_ABI_VERSION; }

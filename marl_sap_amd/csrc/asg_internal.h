@@ -4,9 +4,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/asg.h"
 
 namespace asg {
+
+// the thread-local message returned by asg_last_error(NULL) (asg_abi.hip)
+void set_last_error(const std::string &msg);
 
 struct EnvState {
     int64_t E;             // envs in this handle

@@ -1,0 +1,607 @@
+// asg_real.hip -- batched RealConstellationEnv, constant-benefit
+// path (injected sat_prox_mat, the only one that runs without the orbital simulator).
+//
+// Reference: src/envs/real_constellation_env.py.  Per env and step:
+//   rewards   beta_hat[i, a_i, 0] / count(a_i) (or the full penalty), with
+//             beta_hat[..., 0] = beta[..., 0] - lambda * T_trans[prev_i, j] * (sum_l beta > 1e-12)  (:135-158, :259-327)
+//   beta      sat_prox_mat[:, :, k:k+L] * task_prios, zero past T                                       (:110, :164-168)
+//   obs       per agent: its top-M tasks (L-deep benefits), the N agents competing hardest for them,
+//             their benefits on those tasks and on their own top M/2 other tasks, and a
+//             one-hot of its previous task among its top M                                             (:177-230)
+// float64 arithmetic as numpy (the L-sum left to right), stored through float32 into
+// the float16 / int16 scheme (real_constellation_env.py:80-97) like torch's casts.
+// np.argsort's unspecified tie order is replaced by the stable order (lower index
+// first), as in oracle/asg_real_oracle.c.
+//
+// Layout: the benefit table is stored time-major, table[e][k][i][j] (float64), so one
+// step reads L contiguous [n][m] slices; env stride 0 = one table shared by all envs
+// (the reference's constant-benefit mode).  Per step: a transition kernel (one workgroup
+// per env: counts, rewards, returns), a strip kernel (one workgroup per S agents of an
+// env: the pre-transition row, the L-summed totals kept in LDS and written task-major,
+// each agent's ranked task lists), and an observation kernel (one wave per agent).
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/asg.h"
+#include "asg_device.h"
+#include "asg_internal.h"
+
+namespace asg {
+
+struct RealState {
+    int64_t E;
+    int n, m, T, L, N, M;
+    double lambda_;
+    const double *table;  // [E or 1][T][n][m]
+    int64_t table_env_stride;
+    const double *prios;    // [m]
+    const double *T_trans;  // [m][m]
+    int *prev;              // [E][n]
+    double *returns;        // [E]
+    double *totT;           // [E][m][n] L-summed totals of the current beta, task-major
+    int *topA;              // [E][n][M]        each agent's top-M tasks, ties -> lower index
+    int *topD;              // [E][n][M + M/2]  its top tasks, ties -> higher index
+    int *err;
+};
+
+__device__ __forceinline__ void store_real(const asg_field &f, int64_t off, double v) {
+    switch (f.dtype) {
+        case ASG_F32: reinterpret_cast<float *>(f.ptr)[off] = (float)v; break;
+        case ASG_F16: reinterpret_cast<__half *>(f.ptr)[off] = __float2half((float)v); break;
+        case ASG_F64: reinterpret_cast<double *>(f.ptr)[off] = v; break;
+        default: break;
+    }
+}
+__device__ __forceinline__ void store_int(const asg_field &f, int64_t off, int64_t v) {
+    switch (f.dtype) {
+        case ASG_I64: reinterpret_cast<int64_t *>(f.ptr)[off] = v; break;
+        case ASG_I32: reinterpret_cast<int32_t *>(f.ptr)[off] = (int32_t)v; break;
+        case ASG_I16: reinterpret_cast<int16_t *>(f.ptr)[off] = (int16_t)v; break;
+        case ASG_BOOL: reinterpret_cast<uint8_t *>(f.ptr)[off] = v != 0; break;
+        default: break;
+    }
+}
+__device__ __forceinline__ int64_t load_int(const asg_field &f, int64_t off) {
+    switch (f.dtype) {
+        case ASG_I64: return reinterpret_cast<const int64_t *>(f.ptr)[off];
+        case ASG_I32: return reinterpret_cast<const int32_t *>(f.ptr)[off];
+        case ASG_I16: return reinterpret_cast<const int16_t *>(f.ptr)[off];
+        default: return 0;
+    }
+}
+__device__ __forceinline__ int64_t foff(const asg_field &f, int64_t b, int64_t t, int64_t d2, int64_t d3) {
+    return b * f.stride[0] + t * f.stride[1] + d2 * f.stride[2] + d3 * f.stride[3];
+}
+
+// beta value (i, j, l) at time k: table slice * task priority, zero past T
+__device__ __forceinline__ double real_beta(const RealState &st, const double *tab, int k, int i, int j, int l) {
+    const int kk = k + l;
+    const double v = kk < st.T ? tab[((int64_t)kk * st.n + i) * st.m + j] : 0.0;
+    return v * st.prios[j];
+}
+
+// wave-wide selection of the best remaining candidate: value order descending, ties to the
+// lower index (HIGHER_TIES = false, np.argsort(-x) stable) or to the higher index
+// (HIGHER_TIES = true: the tail of an ascending stable argsort)
+template <bool HIGHER_TIES>
+__device__ __forceinline__ int wave_select(const double *vals, unsigned char *taken, int len) {
+    const int lane = threadIdx.x & 63;
+    double bv = -INFINITY;
+    int bj = -1;
+    for (int j = lane; j < len; j += 64) {
+        if (taken[j]) continue;
+        const double v = vals[j];
+        const bool better = bj < 0 || v > bv || (v == bv && (HIGHER_TIES ? j > bj : j < bj));
+        if (better) {
+            bv = v;
+            bj = j;
+        }
+    }
+    const double vmax = wave_allreduce(bj >= 0 ? bv : -INFINITY, [](double a, double b) { return a > b ? a : b; });
+    int key;
+    if (HIGHER_TIES) {
+        key = wave_max_i32(bj >= 0 && bv == vmax ? bj : -1);
+    } else {
+        key = -wave_max_i32(bj >= 0 && bv == vmax ? -bj : -0x7fffffff);
+    }
+    return key;
+}
+
+// ---- kernel 1: the transition of each env (step only), one workgroup per env ---------------
+// LDS: actions [n] int, counts [m] int, rewards [n] f64
+__host__ __device__ __forceinline__ size_t transition_lds(int n, int m) {
+    return (size_t)4 * (n + m + 1) + 8 * (size_t)n + 8;
+}
+
+__global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv, RealState st, int ts, int k) {
+    extern __shared__ unsigned char s_raw[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, L = st.L;
+    int *sa = reinterpret_cast<int *>(s_raw);                                        // [n]
+    int *scnt = sa + n;                                                              // [m]
+    double *srew = reinterpret_cast<double *>(scnt + m + (((n + m) & 1) ? 1 : 0));  // [n], 8-B aligned
+    const double *tab = st.table + e * st.table_env_stride;
+    int *prev = st.prev + e * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int64_t a = load_int(bv.actions, foff(bv.actions, e, ts, i, 0));
+        if (a < 0 || a >= m) {
+            atomicCAS(st.err, 0, ASG_E_ACTION_RANGE);
+            a = a < 0 ? 0 : m - 1;
+        }
+        sa[i] = (int)a;
+    }
+    for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[sa[i]], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int c = sa[i];
+        double s = real_beta(st, tab, k, i, c, 0);
+        const double b0 = s;
+        for (int l = 1; l < L; ++l) s = s + real_beta(st, tab, k, i, c, l);
+        const double cond = s > 1e-12 ? 1.0 : 0.0;
+        const double pen = st.T_trans[(int64_t)prev[i] * m + c] * cond;
+        const double bh = b0 - st.lambda_ * pen;
+        const double r = bh > 0 ? bh / (double)scnt[c] : bh;
+        srew[i] = r;
+        if (bv.rewards.ptr) store_real(bv.rewards, foff(bv.rewards, e, ts, i, 0), r);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int i = 0; i < n; ++i) tot += srew[i];  // Python sum(rewards), left to right
+        st.returns[e] += tot;
+        if (bv.terminated.ptr) store_int(bv.terminated, foff(bv.terminated, e, ts, 0, 0), k + 1 >= st.T);
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) prev[i] = sa[i];
+}
+
+// ---- kernel 2: the pre-transition row and each agent's task ranking, one workgroup per
+// strip of S agents of one env --------------------------------------------------------
+// Writes beta (float16 [n][m][L]), avail, prev_assigns, filled (and, after a step, the
+// one-hot of the actions at row ts); keeps the strip's L-summed totals in LDS, writes
+// them task-major (totT, coalesced per task across the strip) and ranks each agent's row:
+//   topA[a] = the M best tasks, ties to the lower index      (np.argsort(-total)[:M], :192)
+//   topD[a] = the M + M/2 best tasks, ties to the higher index (the order of the tail of
+//             np.argsort(row)[:, -M//2:], :212-214); an agent's M/2 best tasks outside
+//             any M-task set are always among them (m >= M + M/2 is required)
+// LDS: totals [S][m] f64, then one `taken` byte row per wave (64 * S threads = S waves)
+__host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
+    return (size_t)S * m * 8 + (size_t)S * ((m + 3) & ~3);
+}
+
+__global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, RealState st, int ts, int knew, int step,
+                                                         int S) {
+    extern __shared__ unsigned char s_raw[];
+    const int n = st.n, m = st.m, L = st.L, M = st.M, MD = st.M + st.M / 2;
+    const int64_t e = blockIdx.y;
+    const int i0 = blockIdx.x * S;
+    const int rows = n - i0 < S ? n - i0 : S;
+    double *tl = reinterpret_cast<double *>(s_raw);                        // [S][m] totals
+    unsigned char *taken_all = s_raw + (size_t)S * m * 8;                   // [S waves][m]
+    const double *tab = st.table + e * st.table_env_stride;
+    int *prev = st.prev + e * n;
+    const int row = step ? ts + 1 : ts;
+    if (!step) {
+        for (int r = threadIdx.x; r < rows; r += blockDim.x) prev[i0 + r] = i0 + r;  // np.arange(n) (:111)
+        if (blockIdx.x == 0 && threadIdx.x == 0) st.returns[e] = 0.0;
+    }
+    for (int64_t p = threadIdx.x; p < (int64_t)rows * m; p += blockDim.x) {
+        const int r = (int)(p / m), j = (int)(p - (int64_t)r * m), i = i0 + r;
+        double sum = 0.0;
+        for (int l = 0; l < L; ++l) {
+            const double b = real_beta(st, tab, knew, i, j, l);
+            sum = l == 0 ? b : sum + b;
+            if (bv.beta.ptr) store_real(bv.beta, foff(bv.beta, e, row, i, j) + l, b);
+        }
+        tl[p] = sum;
+        if (bv.avail_actions.ptr) store_int(bv.avail_actions, foff(bv.avail_actions, e, row, i, j), 1);
+        if (step && bv.actions_onehot.ptr)
+            store_int(bv.actions_onehot, foff(bv.actions_onehot, e, ts, i, j), step ? prev[i] == j : 0);
+    }
+    if (bv.prev_assigns.ptr)
+        for (int r = threadIdx.x; r < rows; r += blockDim.x)
+            store_int(bv.prev_assigns, foff(bv.prev_assigns, e, row, i0 + r, 0), step ? prev[i0 + r] : i0 + r);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && bv.filled.ptr) store_int(bv.filled, foff(bv.filled, e, row, 0, 0), 1);
+    __syncthreads();
+    if (knew >= st.T) return;  // done: no observation pass follows
+    double *totT = st.totT + e * (int64_t)n * m;
+    for (int64_t p = threadIdx.x; p < (int64_t)rows * m; p += blockDim.x) {
+        const int j = (int)(p / rows), r = (int)(p - (int64_t)j * rows);
+        totT[(int64_t)j * n + i0 + r] = tl[(int64_t)r * m + j];
+    }
+    // rank each agent row of the strip, one wave per row
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    unsigned char *taken = taken_all + (size_t)wave * ((m + 3) & ~3);
+    for (int r = wave; r < rows; r += waves) {
+        const double *vals = tl + (int64_t)r * m;
+        const int a = i0 + r;
+        for (int j = lane; j < m; j += 64) taken[j] = 0;
+        wave_sync();
+        int *outA = st.topA + (e * n + a) * (int64_t)M;
+        for (int c = 0; c < M; ++c) {
+            const int j = wave_select<false>(vals, taken, m);
+            if (lane == 0) {
+                outA[c] = j;
+                taken[j] = 1;
+            }
+            wave_sync();
+        }
+        for (int j = lane; j < m; j += 64) taken[j] = 0;
+        wave_sync();
+        int *outD = st.topD + (e * n + a) * (int64_t)MD;
+        for (int c = 0; c < MD; ++c) {
+            const int j = wave_select<true>(vals, taken, m);
+            if (lane == 0) {
+                outD[c] = j;
+                taken[j] = 1;
+            }
+            wave_sync();
+        }
+    }
+}
+
+// ---- kernel 3: observation rows, one wave per agent ---------------------------------------
+// per-wave LDS of the observation pass: best[n] f64, taken[n], top[M], topn[N], oth[N][M/2]
+__host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, int N, int M) {
+    (void)m;
+    return ((size_t)n * 9 + 3 + 4 * (size_t)(M + N + N * (M / 2)) + 15) & ~(size_t)15;
+}
+
+// Observation pass, one wave per (env, agent i): competitors from the task-major totals,
+// their "other" tasks from topD, then the row (real_constellation_env.py:186-219).
+__global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew) {
+    extern __shared__ unsigned char s_raw[];
+    const int n = st.n, m = st.m, L = st.L, N = st.N, M = st.M, M2 = st.M / 2, MD = st.M + st.M / 2;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    const int64_t e = blockIdx.y;
+    const int i = blockIdx.x * waves + wave;
+    if (i >= n) return;
+    const int osz = M * L + N * M * L + ((N * M) / 2) * L + M;
+    if (knew >= st.T) {  // done: zero observations (:221-224)
+        for (int p = lane; p < osz; p += 64) store_real(bv.obs, foff(bv.obs, e, row, i, 0) + p, 0.0);
+        return;
+    }
+    const size_t per_wave = real_obs_lds_per_wave(n, m, N, M);
+    unsigned char *base = s_raw + per_wave * wave;
+    double *best = reinterpret_cast<double *>(base);             // [n]
+    unsigned char *taken = base + 8 * (size_t)n;                 // [n]
+    int *top = reinterpret_cast<int *>(taken + ((n + 3) & ~3));  // [M]
+    int *topn = top + M;                                         // [N]
+    int *oth = topn + N;                                         // [N][M2], ascending
+    const int *myA = st.topA + (e * n + i) * (int64_t)M;
+    for (int c = lane; c < M; c += 64) top[c] = myA[c];
+    wave_sync();
+    // (b) each agent's best total over agent i's top-M tasks, agent i excluded (:196-198)
+    const double *totT = st.totT + e * (int64_t)n * m;
+    for (int a = lane; a < n; a += 64) {
+        double b = totT[(int64_t)top[0] * n + a];
+        for (int c = 1; c < M; ++c) {
+            const double v = totT[(int64_t)top[c] * n + a];
+            b = v > b ? v : b;
+        }
+        best[a] = a == i ? -INFINITY : b;
+        taken[a] = 0;
+    }
+    wave_sync();
+    // (c) the N strongest competitors (np.argsort(-best)[:N])
+    for (int c = 0; c < N; ++c) {
+        const int a = wave_select<false>(best, taken, n);
+        if (lane == 0) {
+            topn[c] = a;
+            taken[a] = 1;
+        }
+        wave_sync();
+    }
+    // (d) competitor q's M/2 best tasks outside agent i's top M: the first M/2 entries of
+    //     its topD list not in top[], stored ascending (largest picked first)
+    for (int q = lane; q < N; q += 64) {
+        const int *d = st.topD + (e * n + topn[q]) * (int64_t)MD;
+        int got = 0;
+        for (int c = 0; c < MD && got < M2; ++c) {
+            const int j = d[c];
+            bool in_top = false;
+            for (int k = 0; k < M; ++k) in_top |= top[k] == j;
+            if (!in_top) oth[q * M2 + (M2 - 1 - got++)] = j;
+        }
+    }
+    wave_sync();
+    // (e) the observation row: local, neighbouring, neighbouring-other benefits, assigns
+    const double *tab = st.table + e * st.table_env_stride;
+    const int pi = st.prev[e * n + i];
+    const int64_t o0 = foff(bv.obs, e, row, i, 0);
+    const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L;
+    for (int p = lane; p < osz; p += 64) {
+        double v;
+        if (p < r1) {
+            v = real_beta(st, tab, knew, i, top[p / L], p % L);
+        } else if (p < r2) {
+            const int x = p - r1, q = x / (M * L), y = x - q * M * L;
+            v = real_beta(st, tab, knew, topn[q], top[y / L], y % L);
+        } else if (p < r3) {
+            const int x = p - r2, q = x / (M2 * L), y = x - q * M2 * L;
+            v = real_beta(st, tab, knew, topn[q], oth[q * M2 + y / L], y % L);
+        } else {
+            v = top[p - r3] == pi ? 1.0 : 0.0;
+        }
+        store_real(bv.obs, o0 + p, v);
+    }
+}
+
+// host layout [E'][n][m][T] (the reference's sat_prox_mat) -> time-major [E'][T][n][m]
+__global__ void real_table_transpose_kernel(const double *src, double *dst, int64_t count, int n, int m, int T) {
+    const int64_t total = count * n * m * T;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = p / ((int64_t)T * n * m);
+        int64_t r = p - e * (int64_t)T * n * m;
+        const int k = (int)(r / ((int64_t)n * m));
+        r -= (int64_t)k * n * m;
+        const int i = (int)(r / m), j = (int)(r - (int64_t)i * m);
+        dst[p] = src[((e * n + i) * m + j) * T + k];
+    }
+}
+
+}  // namespace asg
+
+using asg::RealState;
+
+struct asg_real_handle {
+    RealState st{};
+    hipStream_t stream = nullptr;
+    int device = 0;
+    int k = 0;
+    bool has_reset = false;
+    bool table_ready = false;
+    double *table_buf = nullptr;
+    std::string err;
+};
+
+namespace {
+
+int rfail(asg_real_handle *h, int code, const std::string &msg) {
+    asg::set_last_error(msg);
+    if (h) h->err = msg;
+    return code;
+}
+int rhip(asg_real_handle *h, hipError_t e, const char *what) {
+    return rfail(h, ASG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct RDeviceGuard {
+    int prev = -1;
+    explicit RDeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~RDeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+bool rfield_ok(const asg_field &f, std::initializer_list<int> ok) {
+    if (!f.ptr) return true;
+    for (int d : ok)
+        if (f.dtype == d) return true;
+    return false;
+}
+
+int rcheck_view(asg_real_handle *h, const asg_batch_view *b, bool step) {
+    if (!b) return rfail(h, ASG_E_INVALID_ARG, "batch view is NULL");
+    if (!b->obs.ptr) return rfail(h, ASG_E_INVALID_ARG, "obs field is required");
+    const bool ok = rfield_ok(b->obs, {ASG_F16, ASG_F32, ASG_F64}) && rfield_ok(b->beta, {ASG_F16, ASG_F32, ASG_F64}) &&
+                    rfield_ok(b->rewards, {ASG_F16, ASG_F32, ASG_F64}) && rfield_ok(b->avail_actions, {ASG_BOOL}) &&
+                    rfield_ok(b->terminated, {ASG_BOOL}) &&
+                    rfield_ok(b->prev_assigns, {ASG_I16, ASG_I32, ASG_I64}) &&
+                    rfield_ok(b->actions_onehot, {ASG_I16, ASG_I32, ASG_I64}) && rfield_ok(b->filled, {ASG_I64});
+    if (!ok) return rfail(h, ASG_E_INVALID_ARG, "batch field dtype does not match the real-env scheme");
+    if (step && (!b->actions.ptr || !rfield_ok(b->actions, {ASG_I16, ASG_I32, ASG_I64})))
+        return rfail(h, ASG_E_INVALID_ARG, "step needs integer actions");
+    return ASG_OK;
+}
+
+int strip_height(const RealState &st) {
+    int S = 16;
+    while (S > 1 && asg::strip_lds(S, st.m) > 64 * 1024) S >>= 1;
+    return S;
+}
+
+// reset: strip + observation passes; step: transition, strip, observation
+hipError_t launch_real(asg_real_handle *h, const asg_batch_view &bv, int ts, bool step) {
+    const RealState &st = h->st;
+    const int knew = step ? h->k + 1 : 0;
+    const int row = step ? ts + 1 : ts;
+    if (step) {
+        hipLaunchKernelGGL(asg::real_transition_kernel, dim3((unsigned)st.E), dim3(256), asg::transition_lds(st.n, st.m),
+                           h->stream, bv, st, ts, h->k);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    const int S = strip_height(st);
+    hipLaunchKernelGGL(asg::real_strip_kernel, dim3((unsigned)((st.n + S - 1) / S), (unsigned)st.E), dim3(64 * S),
+                       asg::strip_lds(S, st.m), h->stream, bv, st, ts, knew, (int)step, S);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t per_wave = asg::real_obs_lds_per_wave(st.n, st.m, st.N, st.M);
+    int waves = 4;
+    while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
+    const dim3 grid((unsigned)((st.n + waves - 1) / waves), (unsigned)st.E);
+    hipLaunchKernelGGL(asg::real_obs_kernel, grid, dim3(64 * waves), per_wave * waves, h->stream, bv, st, row, knew);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, asg_real_handle **out) {
+    if (!cfg || !out) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL config or output");
+    *out = nullptr;
+    const int n = cfg->n, m = cfg->m, T = cfg->T;
+    const int L = cfg->L < T ? cfg->L : T;  // self.L = min(L, T) (:37)
+    if (cfg->num_envs <= 0 || n <= 0 || m <= 0 || T <= 0 || cfg->L <= 0)
+        return rfail(nullptr, ASG_E_INVALID_ARG, "num_envs, n, m, T, L must be positive");
+    if (n > m) return rfail(nullptr, ASG_E_INVALID_ARG, "prev_assigns = arange(n) needs n <= m");
+    if (n > 4096 || m > 4096) return rfail(nullptr, ASG_E_INVALID_ARG, "n, m <= 4096");
+    if (cfg->M <= 0 || cfg->M > m || cfg->M % 2 != 0)
+        return rfail(nullptr, ASG_E_INVALID_ARG, "M must be even and in [2, m] (obs size uses N*M//2)");
+    if (cfg->N <= 0 || cfg->N > n) return rfail(nullptr, ASG_E_INVALID_ARG, "N must be in [1, n]");
+    if (m < cfg->M + cfg->M / 2)
+        return rfail(nullptr, ASG_E_INVALID_ARG, "m must be >= M + M/2 (the competitors' other tasks)");
+    if (asg::real_obs_lds_per_wave(n, m, cfg->N, cfg->M) > 64 * 1024 || asg::strip_lds(1, m) > 64 * 1024)
+        return rfail(nullptr, ASG_E_INVALID_ARG, "n, m, N, M too large for the observation kernels");
+    RDeviceGuard g(device);
+    auto *h = new (std::nothrow) asg_real_handle();
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "out of host memory");
+    h->device = device;
+    h->stream = static_cast<hipStream_t>(hip_stream);
+    RealState &st = h->st;
+    st.E = cfg->num_envs;
+    st.n = n, st.m = m, st.T = T, st.L = L, st.N = cfg->N, st.M = cfg->M;
+    st.lambda_ = cfg->lambda_;
+    hipError_t e = hipSuccess;
+    double *prios = nullptr, *tt = nullptr;
+    e = hipMalloc(&prios, sizeof(double) * m);
+    if (e == hipSuccess) e = hipMalloc(&tt, sizeof(double) * (size_t)m * m);
+    if (e == hipSuccess) e = hipMalloc(&st.prev, sizeof(int) * (size_t)st.E * n);
+    if (e == hipSuccess) e = hipMalloc(&st.returns, sizeof(double) * (size_t)st.E);
+    if (e == hipSuccess) e = hipMalloc(&st.totT, sizeof(double) * (size_t)st.E * n * m);
+    if (e == hipSuccess) e = hipMalloc(&st.topA, sizeof(int) * (size_t)st.E * n * cfg->M);
+    if (e == hipSuccess) e = hipMalloc(&st.topD, sizeof(int) * (size_t)st.E * n * (cfg->M + cfg->M / 2));
+    if (e == hipSuccess) e = hipMalloc(&st.err, sizeof(int));
+    if (e != hipSuccess) {
+        hipFree(prios), hipFree(tt), hipFree(st.prev), hipFree(st.returns), hipFree(st.err);
+        hipFree(st.totT), hipFree(st.topA), hipFree(st.topD);
+        delete h;
+        return rhip(nullptr, e, "asg_real_create: hipMalloc");
+    }
+    std::vector<double> hp(m, 1.0), ht((size_t)m * m);
+    if (cfg->task_prios) std::memcpy(hp.data(), cfg->task_prios, sizeof(double) * m);
+    for (int a = 0; a < m; ++a)
+        for (int b = 0; b < m; ++b) ht[(size_t)a * m + b] = cfg->T_trans ? cfg->T_trans[(size_t)a * m + b] : (a != b);
+    e = hipMemcpy(prios, hp.data(), sizeof(double) * m, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(tt, ht.data(), sizeof(double) * (size_t)m * m, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(st.err, 0, sizeof(int));
+    if (e == hipSuccess) e = hipMemset(st.returns, 0, sizeof(double) * (size_t)st.E);
+    st.prios = prios;
+    st.T_trans = tt;
+    if (e != hipSuccess) {
+        asg_real_destroy(h);
+        return rhip(nullptr, e, "asg_real_create: upload");
+    }
+    *out = h;
+    return ASG_OK;
+}
+
+void asg_real_destroy(asg_real_handle *h) {
+    if (!h) return;
+    RDeviceGuard g(h->device);
+    hipFree(const_cast<double *>(h->st.prios));
+    hipFree(const_cast<double *>(h->st.T_trans));
+    hipFree(h->st.prev);
+    hipFree(h->st.returns);
+    hipFree(h->st.totT);
+    hipFree(h->st.topA);
+    hipFree(h->st.topD);
+    hipFree(h->st.err);
+    hipFree(h->table_buf);
+    delete h;
+}
+
+int asg_real_set_benefits(asg_real_handle *h, const double *table, int64_t count, int on_device) {
+    if (!h || !table) return rfail(h, ASG_E_INVALID_ARG, "NULL handle or table");
+    if (count != 1 && count != h->st.E) return rfail(h, ASG_E_INVALID_ARG, "count must be 1 or num_envs");
+    RDeviceGuard g(h->device);
+    const RealState &st = h->st;
+    const size_t elems = (size_t)count * st.n * st.m * st.T;
+    hipFree(h->table_buf);
+    h->table_buf = nullptr;
+    double *src = nullptr;
+    hipError_t e = hipMalloc(&h->table_buf, sizeof(double) * elems);
+    if (e == hipSuccess && !on_device) {
+        e = hipMalloc(&src, sizeof(double) * elems);
+        if (e == hipSuccess) e = hipMemcpyAsync(src, table, sizeof(double) * elems, hipMemcpyHostToDevice, h->stream);
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(asg::real_table_transpose_kernel, dim3(2048), dim3(256), 0, h->stream,
+                           on_device ? table : src, h->table_buf, (int64_t)count, st.n, st.m, st.T);
+        e = hipGetLastError();
+    }
+    if (src) {
+        const hipError_t e2 = hipStreamSynchronize(h->stream);
+        hipFree(src);
+        if (e == hipSuccess) e = e2;
+    }
+    if (e != hipSuccess) return rhip(h, e, "asg_real_set_benefits");
+    h->st.table = h->table_buf;
+    h->st.table_env_stride = count == 1 ? 0 : (int64_t)st.T * st.n * st.m;
+    h->table_ready = true;
+    return ASG_OK;
+}
+
+int asg_real_set_stream(asg_real_handle *h, void *hip_stream) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    h->stream = static_cast<hipStream_t>(hip_stream);
+    return ASG_OK;
+}
+
+int asg_real_reset(asg_real_handle *h, const asg_batch_view *view, int ts) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (!h->table_ready) return rfail(h, ASG_E_STATE, "asg_real_reset: no benefit table (asg_real_set_benefits)");
+    if (int rc = rcheck_view(h, view, false)) return rc;
+    RDeviceGuard g(h->device);
+    const hipError_t e = launch_real(h, *view, ts, false);
+    if (e != hipSuccess) return rhip(h, e, "asg_real_reset");
+    h->k = 0;
+    h->has_reset = true;
+    return ASG_OK;
+}
+
+int asg_real_step(asg_real_handle *h, const asg_batch_view *view, int ts) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (!h->has_reset) return rfail(h, ASG_E_STATE, "asg_real_step before asg_real_reset");
+    if (h->k >= h->st.T) return rfail(h, ASG_E_STATE, "episode is done: call asg_real_reset");
+    if (int rc = rcheck_view(h, view, true)) return rc;
+    RDeviceGuard g(h->device);
+    const hipError_t e = launch_real(h, *view, ts, true);
+    if (e != hipSuccess) return rhip(h, e, "asg_real_step");
+    h->k += 1;
+    return ASG_OK;
+}
+
+int asg_real_sync_status(asg_real_handle *h) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    RDeviceGuard g(h->device);
+    int code = 0;
+    hipError_t e = hipMemcpyAsync(&code, h->st.err, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return rhip(h, e, "asg_real_sync_status");
+    if (code == ASG_E_ACTION_RANGE) {
+        (void)hipMemsetAsync(h->st.err, 0, sizeof(int), h->stream);
+        return rfail(h, code, "action out of range [0, m)");
+    }
+    return code ? rfail(h, code, "device error") : ASG_OK;
+}
+
+int asg_real_get_returns(asg_real_handle *h, double *out_device) {
+    if (!h || !out_device) return rfail(h, ASG_E_INVALID_ARG, "NULL handle or output");
+    RDeviceGuard g(h->device);
+    const hipError_t e = hipMemcpyAsync(out_device, h->st.returns, sizeof(double) * (size_t)h->st.E,
+                                        hipMemcpyDeviceToDevice, h->stream);
+    return e == hipSuccess ? ASG_OK : rhip(h, e, "asg_real_get_returns");
+}
+
+int asg_real_get_step(const asg_real_handle *h, int *k_out) {
+    if (!h || !k_out) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle or output");
+    *k_out = h->k;
+    return ASG_OK;
+}
+
+int asg_real_obs_size(int N, int M, int L) { return M * L + N * M * L + ((N * M) / 2) * L + M; }
+
+}  // extern "C"

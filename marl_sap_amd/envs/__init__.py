@@ -8,6 +8,7 @@ from functools import partial
 
 from .multiagentenv import MultiAgentEnv
 from .assign_env import AssignEnvBatch, MockConstellationEnv, make_scheme, batch_view
+from .real_env import RealAssignEnvBatch, make_real_scheme
 
 
 def env_fn(env, **kwargs) -> MultiAgentEnv:
@@ -15,4 +16,5 @@ def env_fn(env, **kwargs) -> MultiAgentEnv:
 
 
 REGISTRY = {"mock_constellation_env": partial(env_fn, env=MockConstellationEnv)}
-BATCHED_REGISTRY = {"mock_constellation_env": partial(env_fn, env=AssignEnvBatch)}
+BATCHED_REGISTRY = {"mock_constellation_env": partial(env_fn, env=AssignEnvBatch),
+                    "real_constellation_env": partial(env_fn, env=RealAssignEnvBatch)}

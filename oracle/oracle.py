@@ -64,6 +64,14 @@ def lib():
         L.ora_rollout_random.argtypes = [ctypes.c_int] * 5 + [ctypes.c_double, ctypes.c_uint32,
                                                               ctypes.c_int, ctypes.c_int, _dp]
         L.ora_rollout_random.restype = ctypes.c_double
+        ci = ctypes.c_int
+        L.ora_real_obs_size.argtypes = [ci, ci, ci]
+        L.ora_real_obs_size.restype = ci
+        L.ora_real_beta.argtypes = [_dp, _dp, ci, ci, ci, ci, ci, _dp]
+        L.ora_real_obs.argtypes = [_dp, ci, ci, ci, ci, ci, _i64p, ci, _dp]
+        L.ora_real_reset.argtypes = [_dp, _dp, ci, ci, ci, ci, ci, ci, _dp, _i64p, _dp]
+        L.ora_real_step.argtypes = [_dp, _dp, _dp, ci, ci, ci, ci, ci, ci, ctypes.c_double,
+                                    ctypes.POINTER(ci), _dp, _i64p, _i64p, _dp, ctypes.POINTER(ci), _dp]
         _lib = L
     return _lib
 
@@ -208,6 +216,43 @@ class OracleMockEnv:
 
     def beta_hat(self, beta, prev_assigns):
         return beta_hat(np.asarray(beta), np.asarray(prev_assigns), self.lambda_, self.T_trans)
+
+
+class OracleRealEnv:
+    """RealConstellationEnv with injected benefits (src/envs/real_constellation_env.py,
+    constant-benefit path), arithmetic in asg_real_oracle.c; argsort ties resolved in the
+    stable (lower index first) order."""
+
+    def __init__(self, sat_prox_mat, N, M, L, lambda_, T_trans=None, task_prios=None):
+        self.table = np.ascontiguousarray(sat_prox_mat, dtype=np.float64)
+        self.n, self.m, self.T = self.table.shape
+        self.N, self.M, self.L, self.lambda_ = N, M, min(L, self.T), float(lambda_)
+        self.T_trans = np.ascontiguousarray(
+            T_trans if T_trans is not None else np.ones((self.m, self.m)) - np.eye(self.m), dtype=np.float64)
+        self.prios = np.ascontiguousarray(task_prios if task_prios is not None else np.ones(self.m),
+                                          dtype=np.float64)
+        self.obs_size = lib().ora_real_obs_size(N, M, self.L)
+
+    def reset(self):
+        self.k = 0
+        self.done = False
+        self.beta = np.empty((self.n, self.m, self.L))
+        self.prev_assigns = np.empty(self.n, dtype=np.int64)
+        self.obs = np.empty((self.n, self.obs_size))
+        lib().ora_real_reset(_p(self.table, _dp), _p(self.prios, _dp), self.n, self.m, self.T, self.L, self.N,
+                             self.M, _p(self.beta, _dp), _p(self.prev_assigns, _i64p), _p(self.obs, _dp))
+        return self.obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int64)
+        rewards = np.empty(self.n)
+        k, done = ctypes.c_int(self.k), ctypes.c_int(0)
+        lib().ora_real_step(_p(self.table, _dp), _p(self.prios, _dp), _p(self.T_trans, _dp), self.n, self.m,
+                            self.T, self.L, self.N, self.M, self.lambda_, ctypes.byref(k), _p(self.beta, _dp),
+                            _p(self.prev_assigns, _i64p), _p(a, _i64p), _p(rewards, _dp), ctypes.byref(done),
+                            _p(self.obs, _dp))
+        self.k, self.done = k.value, bool(done.value)
+        return rewards, self.done, {}
 
 
 def rollout_random(E, n, m, T, L, lam, seed, threads, episodes=1):

@@ -19,6 +19,7 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   mock_step.npz       per-step rewards / obs / beta / done for injected tables
   lsa.npz             scipy.optimize.linear_sum_assignment input/output pairs
   runner_dumps.npz    EpisodeRunner / ParallelRunner EpisodeBatch dumps (layout + quirks)
+  real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
 """
 import os
 import sys
@@ -225,6 +226,62 @@ def gen_mock_step():
     np.savez_compressed(os.path.join(OUT, "mock_step.npz"), **out)
 
 
+def gen_real_env():
+    """RealConstellationEnv (constant-benefit path: injected sat_prox_mat + graphs) through
+    reset/step.  Strictly positive tables: no equal totals, so numpy's (unstable) argsort
+    order is the tie-free order the GPU restates."""
+    from envs.real_constellation_env import RealConstellationEnv
+    rng = np.random.RandomState(4321)
+    out = {}
+    # (n, m, T, L, N, M, lambda, prios, T_trans, actions)
+    specs = [(6, 10, 5, 3, 2, 4, 0.5, False, False, "random"),
+             (12, 20, 6, 3, 3, 4, 0.5, True, False, "random"),
+             (9, 16, 8, 2, 4, 6, 0.3, False, True, "collide"),
+             (10, 12, 4, 5, 3, 2, 0.5, True, False, "random"),
+             (8, 30, 7, 3, 7, 8, 0.5, False, False, "collide"),
+             (5, 9, 6, 3, 4, 6, 1.5, True, True, "random")]
+    for idx, (n, m, T, L, N, M, lam, use_prios, use_tt, kind) in enumerate(specs):
+        table = rng.uniform(0.01, 1.0, size=(n, m, T))
+        prios = rng.uniform(0.5, 2.0, size=m) if use_prios else None
+        T_trans = (rng.uniform(size=(m, m)) > 0.4).astype(np.float64) if use_tt else None
+        env = RealConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(), graphs=[None] * T,
+                                   T_trans=None if T_trans is None else T_trans.copy(),
+                                   task_prios=None if prios is None else prios.copy())
+        env.reset()
+        Le = env.L
+        obs0, beta0, prev0 = np.array(env._obs), np.asarray(env.beta).copy(), np.asarray(env.prev_assigns)
+        acts, rews, obs, betas, dones, prevs = [], [], [], [], [], []
+        for t in range(T):
+            if kind == "collide" and t % 2 == 0:
+                a = np.full(n, (3 * t) % m, dtype=np.int64)
+            else:
+                a = rng.randint(0, m, size=n)
+            r, d, info = env.step(list(a))
+            acts.append(a)
+            rews.append(np.asarray(r, dtype=np.float64))
+            obs.append(np.array(env._obs))
+            betas.append(np.asarray(env.beta).copy())
+            dones.append(bool(d))
+            prevs.append(np.asarray(env.prev_assigns, dtype=np.int64))
+        out[f"r{idx}_spec"] = np.array([n, m, T, Le, N, M])
+        out[f"r{idx}_lambda"] = np.array(lam)
+        out[f"r{idx}_table"] = table
+        out[f"r{idx}_prios"] = prios if prios is not None else np.ones(m)
+        out[f"r{idx}_T_trans"] = T_trans if T_trans is not None else np.ones((m, m)) - np.eye(m)
+        out[f"r{idx}_obs_size"] = np.array(env.get_obs_size())
+        out[f"r{idx}_obs0"] = obs0
+        out[f"r{idx}_beta0"] = beta0
+        out[f"r{idx}_prev0"] = prev0.astype(np.int64)
+        out[f"r{idx}_actions"] = np.stack(acts)
+        out[f"r{idx}_rewards"] = np.stack(rews)
+        out[f"r{idx}_obs"] = np.stack(obs)
+        out[f"r{idx}_beta"] = np.stack(betas)
+        out[f"r{idx}_done"] = np.array(dones)
+        out[f"r{idx}_prev"] = np.stack(prevs)
+    out["n_cases"] = np.array(len(specs))
+    np.savez_compressed(os.path.join(OUT, "real_env.npz"), **out)
+
+
 def gen_lsa():
     import scipy.optimize as so
     rng = np.random.RandomState(77)
@@ -353,6 +410,10 @@ def gen_runner_dumps():
 
 if __name__ == "__main__":
     _install_stubs()
+    if sys.argv[1:] == ["real_env"]:  # regenerate only the RealConstellationEnv fixture
+        gen_real_env()
+        sys.exit(0)
+    gen_real_env()
     gen_mt_words()
     gen_mock_reset()
     gen_mock_step()

@@ -95,3 +95,25 @@ def test_lsa(golden, oracle):
         msg = str(g[f"e{e}_msg"])
         with pytest.raises(ValueError, match=msg):
             oracle.lsa(g[f"e{e}_C"], bool(g[f"e{e}_max"]))
+
+
+def test_real_env_oracle_matches_reference_fixture(golden, oracle):
+    """RealConstellationEnv restatement (oracle/asg_real_oracle.c) vs the reference's own
+    reset/step outputs on tie-free injected tables: float64 bit-exact."""
+    d = golden("real_env")
+    for c in range(int(d["n_cases"])):
+        n, m, T, L, N, M = (int(x) for x in d[f"r{c}_spec"])
+        env = oracle.OracleRealEnv(d[f"r{c}_table"], N, M, L, float(d[f"r{c}_lambda"]),
+                                   T_trans=d[f"r{c}_T_trans"], task_prios=d[f"r{c}_prios"])
+        assert env.obs_size == int(d[f"r{c}_obs_size"])
+        obs0 = env.reset()
+        np.testing.assert_array_equal(obs0, d[f"r{c}_obs0"])
+        np.testing.assert_array_equal(env.beta, d[f"r{c}_beta0"])
+        np.testing.assert_array_equal(env.prev_assigns, d[f"r{c}_prev0"])
+        for t in range(T):
+            r, done, _ = env.step(d[f"r{c}_actions"][t])
+            np.testing.assert_array_equal(r, d[f"r{c}_rewards"][t])
+            np.testing.assert_array_equal(env.obs, d[f"r{c}_obs"][t])
+            np.testing.assert_array_equal(env.beta, d[f"r{c}_beta"][t])
+            np.testing.assert_array_equal(env.prev_assigns, d[f"r{c}_prev"][t])
+            assert done == bool(d[f"r{c}_done"][t])
