@@ -237,14 +237,34 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
  * np.argsort ties (unspecified order in numpy) are broken by the lower index. */
 typedef struct asg_real_handle asg_real_handle;
 
+/* env family: RealConstellationEnv (real_constellation_env.py), RealPowerConstellationEnv
+ * (real_power_constellation_env.py: per-satellite power drained 0.2 per meaningful task,
+ * recharged 0.1 otherwise, dead at <= 0; power in state and obs), InterferenceConstellationEnv
+ * (interference_constellation_env.py: the power dynamics plus a beam-interference reward
+ * over satellites sharing a frequency band, :309-353). */
+enum asg_real_variant { ASG_REAL_PLAIN = 0, ASG_REAL_POWER = 1, ASG_REAL_INTERFERENCE = 2 };
+
 typedef struct {
     int64_t num_envs;
     int32_t n, m, T, L;        /* n = num_planes * num_sats_per_plane (n <= m); L = min(L, T) */
-    int32_t N, M;              /* competitors and tasks in the observation; M even */
+    int32_t N, M;              /* competitors and tasks in the observation; M even, m >= 3M/2 */
     double lambda_;
     const double *T_trans;     /* host [m][m] or NULL (= 1 - I) */
     const double *task_prios;  /* host [m] or NULL (= ones) */
+    int32_t variant;           /* asg_real_variant */
+    int32_t pad_;
+    uint64_t seed;             /* power variants: Philox key of the reset assignments ... */
+    int64_t env_index_base;    /* ... per global env index (choice(m, n, replace=False)) */
+    const int32_t *sat_freq_bands;   /* host [n] (interference) */
+    const double *neighbor_matrix;   /* host [m][m] (interference; integer-valued) */
 } asg_real_config;
+
+/* EpisodeBatch view of the real envs: the mock-env fields plus power_states f16 [B, T+1, n]
+ * (power variants; real_power_constellation_env.py:112, NULL ptr = absent) */
+typedef struct {
+    asg_batch_view base;
+    asg_field power_states;
+} asg_real_batch_view;
 
 int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, asg_real_handle **out);
 void asg_real_destroy(asg_real_handle *h);
@@ -252,12 +272,16 @@ int asg_real_set_stream(asg_real_handle *h, void *hip_stream);
 /* sat_prox_mat float64 [count][n][m][T] (reference layout), count = 1 (shared by every
  * env, the reference's constant benefits) or num_envs; host or device memory. */
 int asg_real_set_benefits(asg_real_handle *h, const double *table, int64_t count, int on_device);
-int asg_real_reset(asg_real_handle *h, const asg_batch_view *view, int ts);
-int asg_real_step(asg_real_handle *h, const asg_batch_view *view, int ts);
+/* power variants: the reset's np.random.choice(m, n, replace=False) as given int64
+ * [count][n] (count 1 or num_envs; exact-parity mode); NULL returns to Philox draws */
+int asg_real_set_initial_assignments(asg_real_handle *h, const int64_t *prev0, int64_t count, int on_device);
+int asg_real_reset(asg_real_handle *h, const asg_real_batch_view *view, int ts);
+int asg_real_step(asg_real_handle *h, const asg_real_batch_view *view, int ts);
 int asg_real_sync_status(asg_real_handle *h);
 int asg_real_get_returns(asg_real_handle *h, double *out_device); /* float64 [E] */
 int asg_real_get_step(const asg_real_handle *h, int *k_out);
-/* get_obs_size (:251-253): M*L + N*M*L + (N*M//2)*L + M */
+/* get_obs_size (real_constellation_env.py:251-253): M*L + N*M*L + (N*M//2)*L + M; the
+ * power variants add N + 1 (real_power_constellation_env.py:286-290) */
 int asg_real_obs_size(int N, int M, int L);
 
 #ifdef __cplusplus

@@ -37,7 +37,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_epsilon_greedy",
            "asg_rnn_agent_packed_size", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
            "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
-           "asg_real_set_benefits", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
+           "asg_real_set_benefits", "asg_real_set_initial_assignments", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
            "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size"]
 
 
@@ -67,7 +67,17 @@ class AsgRealConfig(ctypes.Structure):
     _fields_ = [("num_envs", ctypes.c_int64), ("n", ctypes.c_int32), ("m", ctypes.c_int32),
                 ("T", ctypes.c_int32), ("L", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32),
                 ("lambda_", ctypes.c_double), ("T_trans", ctypes.POINTER(ctypes.c_double)),
-                ("task_prios", ctypes.POINTER(ctypes.c_double))]
+                ("task_prios", ctypes.POINTER(ctypes.c_double)), ("variant", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("seed", ctypes.c_uint64), ("env_index_base", ctypes.c_int64),
+                ("sat_freq_bands", ctypes.POINTER(ctypes.c_int32)),
+                ("neighbor_matrix", ctypes.POINTER(ctypes.c_double))]
+
+
+class AsgRealBatchView(ctypes.Structure):
+    _fields_ = [("base", AsgBatchView), ("power_states", AsgField)]
+
+
+ASG_REAL_PLAIN, ASG_REAL_POWER, ASG_REAL_INTERFERENCE = 0, 1, 2
 
 
 _lib = None
@@ -115,8 +125,9 @@ def lib():
         L.asg_real_destroy.restype = None
         L.asg_real_set_stream.argtypes = [vp, vp]
         L.asg_real_set_benefits.argtypes = [vp, vp, i64, i32]
-        L.asg_real_reset.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
-        L.asg_real_step.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
+        L.asg_real_set_initial_assignments.argtypes = [vp, vp, i64, i32]
+        L.asg_real_reset.argtypes = [vp, ctypes.POINTER(AsgRealBatchView), i32]
+        L.asg_real_step.argtypes = [vp, ctypes.POINTER(AsgRealBatchView), i32]
         L.asg_real_sync_status.argtypes = [vp]
         L.asg_real_get_returns.argtypes = [vp, vp]
         L.asg_real_get_step.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]

@@ -47,6 +47,15 @@ struct RealState {
     int *topA;              // [E][n][M]        each agent's top-M tasks, ties -> lower index
     int *topD;              // [E][n][M + M/2]  its top tasks, ties -> higher index
     int *err;
+    int variant;            // asg_real_variant
+    double *power;          // [E][n] power states (power / interference variants)
+    const int *bands;       // [n] frequency band per satellite (interference)
+    const double *nbr;      // [m][m] task neighbour matrix (interference)
+    const int64_t *prev0;   // injected reset assignments [count][n] or nullptr (Philox)
+    int64_t prev0_env_stride;
+    uint64_t seed;
+    int64_t env_base;
+    uint32_t episode;
 };
 
 __device__ __forceinline__ void store_real(const asg_field &f, int64_t off, double v) {
@@ -113,9 +122,9 @@ __device__ __forceinline__ int wave_select(const double *vals, unsigned char *ta
 }
 
 // ---- kernel 1: the transition of each env (step only), one workgroup per env ---------------
-// LDS: actions [n] int, counts [m] int, rewards [n] f64
+// LDS: actions [n] int, counts [m] int, rewards [n] f64, applicable [n] int
 __host__ __device__ __forceinline__ size_t transition_lds(int n, int m) {
-    return (size_t)4 * (n + m + 1) + 8 * (size_t)n + 8;
+    return (size_t)4 * (n + m + 1) + 8 * (size_t)n + 8 + 4 * (size_t)n;  // + applicable [n]
 }
 
 __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv, RealState st, int ts, int k) {
@@ -137,19 +146,64 @@ __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv,
     }
     for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[sa[i]], 1);
+    double *pw = st.power + e * n;
+    int *sapp = reinterpret_cast<int *>(srew + n);  // [n] applicable (interference)
+    if (st.variant == ASG_REAL_INTERFERENCE) {
+        // applicable = alive and on a meaningful task; counts over applicable agents only
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            sapp[i] = (pw[i] <= 0 ? 0 : 1) * (real_beta(st, tab, k, i, sa[i], 0) < 1e-12 ? 0 : 1);
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            if (sapp[i]) atomicAdd(&scnt[sa[i]], 1);
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[sa[i]], 1);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int c = sa[i];
-        double s = real_beta(st, tab, k, i, c, 0);
-        const double b0 = s;
-        for (int l = 1; l < L; ++l) s = s + real_beta(st, tab, k, i, c, l);
-        const double cond = s > 1e-12 ? 1.0 : 0.0;
-        const double pen = st.T_trans[(int64_t)prev[i] * m + c] * cond;
-        const double bh = b0 - st.lambda_ * pen;
-        const double r = bh > 0 ? bh / (double)scnt[c] : bh;
+        double r;
+        if (st.variant == ASG_REAL_INTERFERENCE) {
+            // conflicts = sum over the agents of i's band of nbr[a_i, a_j] * applicable_j - 1
+            // (interference_constellation_env.py:327-331), then 0.5 ** conflicts
+            double conf = 0.0;
+            const int band = st.bands[i];
+            for (int a = 0; a < n; ++a)
+                if (st.bands[a] == band) conf = conf + st.nbr[(int64_t)c * m + sa[a]] * (double)sapp[a];
+            conf = conf - 1.0;
+            r = real_beta(st, tab, k, i, c, 0) * pow(0.5, conf);
+            if (scnt[c] > 0) r = r / (double)scnt[c];
+            if (sapp[i] && prev[i] != c) r = r - st.lambda_;
+        } else if (st.variant == ASG_REAL_POWER && !(pw[i] > 0)) {
+            r = 0.0;  // dead satellite (real_power_constellation_env.py:161-162)
+        } else {
+            double bh;
+            if (st.variant == ASG_REAL_POWER && pw[i] < 1e-12) {
+                bh = 0.0;  // beta_hat zeroed below 1e-12 power (:343-347)
+            } else {
+                double s = real_beta(st, tab, k, i, c, 0);
+                const double b0 = s;
+                for (int l = 1; l < L; ++l) s = s + real_beta(st, tab, k, i, c, l);
+                const double cond = s > 1e-12 ? 1.0 : 0.0;
+                const double pen = st.T_trans[(int64_t)prev[i] * m + c] * cond;
+                bh = b0 - st.lambda_ * pen;
+            }
+            r = bh > 0 ? bh / (double)scnt[c] : bh;
+        }
         srew[i] = r;
         if (bv.rewards.ptr) store_real(bv.rewards, foff(bv.rewards, e, ts, i, 0), r);
+    }
+    if (st.variant != ASG_REAL_PLAIN) {
+        __syncthreads();  // every reader of the old power is done
+        // power update on the pre-step beta (real_power_constellation_env.py:170-178)
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            if (pw[i] > 0) {
+                if (real_beta(st, tab, k, i, sa[i], 0) > 1e-12) {
+                    pw[i] -= 0.2;
+                } else {
+                    const double p = pw[i] + 0.1;
+                    pw[i] = p < 1.0 ? p : 1.0;
+                }
+            }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -159,6 +213,40 @@ __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv,
         if (bv.terminated.ptr) store_int(bv.terminated, foff(bv.terminated, e, ts, 0, 0), k + 1 >= st.T);
     }
     for (int i = threadIdx.x; i < n; i += blockDim.x) prev[i] = sa[i];
+}
+
+// ---- reset: assignments, power, returns (one workgroup per env) -------------------------
+//   plain:          prev_assigns = arange(n)                              (:111)
+//   power variants: np.random.choice(m, n, replace=False) -- the injected assignments, or a
+//                   Philox Fisher-Yates keyed (seed, global env, episode) -- and full power
+__global__ void __launch_bounds__(256) real_reset_kernel(RealState st) {
+    extern __shared__ int s_perm[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m;
+    int *prev = st.prev + e * n;
+    if (st.variant == ASG_REAL_PLAIN) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) prev[i] = i;
+    } else if (st.prev0) {
+        const int64_t *p0 = st.prev0 + e * st.prev0_env_stride;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) prev[i] = (int)p0[i];
+    } else {
+        for (int j = threadIdx.x; j < m; j += blockDim.x) s_perm[j] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const EnvKey key = env_key(st.seed, st.env_base + e);
+            for (int i = m - 1; i >= 1; --i) {
+                const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, 0u, kCtrPerm, st.episode}, key.k0, key.k1);
+                const int jj = (int)(((uint64_t)r.x * (uint64_t)(i + 1)) >> 32);
+                const int t = s_perm[i];
+                s_perm[i] = s_perm[jj];
+                s_perm[jj] = t;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) prev[i] = s_perm[i];
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) st.power[e * n + i] = 1.0;
+    if (threadIdx.x == 0) st.returns[e] = 0.0;
 }
 
 // ---- kernel 2: the pre-transition row and each agent's task ranking, one workgroup per
@@ -175,8 +263,8 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
     return (size_t)S * m * 8 + (size_t)S * ((m + 3) & ~3);
 }
 
-__global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, RealState st, int ts, int knew, int step,
-                                                         int S) {
+__global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
+                                                          int knew, int step, int S) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, M = st.M, MD = st.M + st.M / 2;
     const int64_t e = blockIdx.y;
@@ -187,10 +275,6 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, Rea
     const double *tab = st.table + e * st.table_env_stride;
     int *prev = st.prev + e * n;
     const int row = step ? ts + 1 : ts;
-    if (!step) {
-        for (int r = threadIdx.x; r < rows; r += blockDim.x) prev[i0 + r] = i0 + r;  // np.arange(n) (:111)
-        if (blockIdx.x == 0 && threadIdx.x == 0) st.returns[e] = 0.0;
-    }
     for (int64_t p = threadIdx.x; p < (int64_t)rows * m; p += blockDim.x) {
         const int r = (int)(p / m), j = (int)(p - (int64_t)r * m), i = i0 + r;
         double sum = 0.0;
@@ -206,7 +290,10 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, Rea
     }
     if (bv.prev_assigns.ptr)
         for (int r = threadIdx.x; r < rows; r += blockDim.x)
-            store_int(bv.prev_assigns, foff(bv.prev_assigns, e, row, i0 + r, 0), step ? prev[i0 + r] : i0 + r);
+            store_int(bv.prev_assigns, foff(bv.prev_assigns, e, row, i0 + r, 0), prev[i0 + r]);
+    if (pfield.ptr && st.variant != ASG_REAL_PLAIN)
+        for (int r = threadIdx.x; r < rows; r += blockDim.x)
+            store_real(pfield, foff(pfield, e, row, i0 + r, 0), st.power[e * n + i0 + r]);
     if (blockIdx.x == 0 && threadIdx.x == 0 && bv.filled.ptr) store_int(bv.filled, foff(bv.filled, e, row, 0, 0), 1);
     __syncthreads();
     if (knew >= st.T) return;  // done: no observation pass follows
@@ -262,7 +349,7 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     const int64_t e = blockIdx.y;
     const int i = blockIdx.x * waves + wave;
     if (i >= n) return;
-    const int osz = M * L + N * M * L + ((N * M) / 2) * L + M;
+    const int osz = M * L + N * M * L + ((N * M) / 2) * L + M + (st.variant != ASG_REAL_PLAIN ? N + 1 : 0);
     if (knew >= st.T) {  // done: zero observations (:221-224)
         for (int p = lane; p < osz; p += 64) store_real(bv.obs, foff(bv.obs, e, row, i, 0) + p, 0.0);
         return;
@@ -315,7 +402,8 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     const double *tab = st.table + e * st.table_env_stride;
     const int pi = st.prev[e * n + i];
     const int64_t o0 = foff(bv.obs, e, row, i, 0);
-    const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L;
+    const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L, r4 = r3 + M;
+    const double *pw = st.power + e * n;
     for (int p = lane; p < osz; p += 64) {
         double v;
         if (p < r1) {
@@ -326,8 +414,10 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
         } else if (p < r3) {
             const int x = p - r2, q = x / (M2 * L), y = x - q * M2 * L;
             v = real_beta(st, tab, knew, topn[q], oth[q * M2 + y / L], y % L);
-        } else {
+        } else if (p < r4) {
             v = top[p - r3] == pi ? 1.0 : 0.0;
+        } else {  // [power_i, power[top_n]] (real_power_constellation_env.py:226-229)
+            v = p == r4 ? pw[i] : pw[topn[p - r4 - 1]];
         }
         store_real(bv.obs, o0 + p, v);
     }
@@ -411,21 +501,25 @@ int strip_height(const RealState &st) {
     return S;
 }
 
-// reset: strip + observation passes; step: transition, strip, observation
-hipError_t launch_real(asg_real_handle *h, const asg_batch_view &bv, int ts, bool step) {
+// reset: reset + strip + observation passes; step: transition, strip, observation
+hipError_t launch_real(asg_real_handle *h, const asg_real_batch_view &v, int ts, bool step) {
     const RealState &st = h->st;
+    const asg_batch_view &bv = v.base;
     const int knew = step ? h->k + 1 : 0;
     const int row = step ? ts + 1 : ts;
     if (step) {
         hipLaunchKernelGGL(asg::real_transition_kernel, dim3((unsigned)st.E), dim3(256), asg::transition_lds(st.n, st.m),
                            h->stream, bv, st, ts, h->k);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(asg::real_reset_kernel, dim3((unsigned)st.E), dim3(256), sizeof(int) * (size_t)st.m,
+                           h->stream, st);
     }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     const int S = strip_height(st);
     hipLaunchKernelGGL(asg::real_strip_kernel, dim3((unsigned)((st.n + S - 1) / S), (unsigned)st.E), dim3(64 * S),
-                       asg::strip_lds(S, st.m), h->stream, bv, st, ts, knew, (int)step, S);
-    hipError_t e = hipGetLastError();
+                       asg::strip_lds(S, st.m), h->stream, bv, v.power_states, st, ts, knew, (int)step, S);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t per_wave = asg::real_obs_lds_per_wave(st.n, st.m, st.N, st.M);
     int waves = 4;
@@ -433,6 +527,13 @@ hipError_t launch_real(asg_real_handle *h, const asg_batch_view &bv, int ts, boo
     const dim3 grid((unsigned)((st.n + waves - 1) / waves), (unsigned)st.E);
     hipLaunchKernelGGL(asg::real_obs_kernel, grid, dim3(64 * waves), per_wave * waves, h->stream, bv, st, row, knew);
     return hipGetLastError();
+}
+
+template <class T>
+hipError_t upload(T **dst, const T *src, size_t count) {
+    hipError_t e = hipMalloc(dst, sizeof(T) * count);
+    if (e == hipSuccess) e = hipMemcpy(*dst, src, sizeof(T) * count, hipMemcpyHostToDevice);
+    return e;
 }
 
 }  // namespace
@@ -446,7 +547,11 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
     const int L = cfg->L < T ? cfg->L : T;  // self.L = min(L, T) (:37)
     if (cfg->num_envs <= 0 || n <= 0 || m <= 0 || T <= 0 || cfg->L <= 0)
         return rfail(nullptr, ASG_E_INVALID_ARG, "num_envs, n, m, T, L must be positive");
-    if (n > m) return rfail(nullptr, ASG_E_INVALID_ARG, "prev_assigns = arange(n) needs n <= m");
+    if (cfg->variant < ASG_REAL_PLAIN || cfg->variant > ASG_REAL_INTERFERENCE)
+        return rfail(nullptr, ASG_E_INVALID_ARG, "unknown variant");
+    if (n > m)
+        return rfail(nullptr, ASG_E_INVALID_ARG,
+                     "Cannot take a larger sample than population when 'replace=False' (prev_assigns needs n <= m)");
     if (n > 4096 || m > 4096) return rfail(nullptr, ASG_E_INVALID_ARG, "n, m <= 4096");
     if (cfg->M <= 0 || cfg->M > m || cfg->M % 2 != 0)
         return rfail(nullptr, ASG_E_INVALID_ARG, "M must be even and in [2, m] (obs size uses N*M//2)");
@@ -455,6 +560,8 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
         return rfail(nullptr, ASG_E_INVALID_ARG, "m must be >= M + M/2 (the competitors' other tasks)");
     if (asg::real_obs_lds_per_wave(n, m, cfg->N, cfg->M) > 64 * 1024 || asg::strip_lds(1, m) > 64 * 1024)
         return rfail(nullptr, ASG_E_INVALID_ARG, "n, m, N, M too large for the observation kernels");
+    if (cfg->variant == ASG_REAL_INTERFERENCE && (!cfg->sat_freq_bands || !cfg->neighbor_matrix))
+        return rfail(nullptr, ASG_E_INVALID_ARG, "the interference variant needs sat_freq_bands and neighbor_matrix");
     RDeviceGuard g(device);
     auto *h = new (std::nothrow) asg_real_handle();
     if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "out of host memory");
@@ -464,35 +571,35 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
     st.E = cfg->num_envs;
     st.n = n, st.m = m, st.T = T, st.L = L, st.N = cfg->N, st.M = cfg->M;
     st.lambda_ = cfg->lambda_;
-    hipError_t e = hipSuccess;
-    double *prios = nullptr, *tt = nullptr;
-    e = hipMalloc(&prios, sizeof(double) * m);
-    if (e == hipSuccess) e = hipMalloc(&tt, sizeof(double) * (size_t)m * m);
+    st.variant = cfg->variant;
+    st.seed = cfg->seed;
+    st.env_base = cfg->env_index_base;
+    std::vector<double> hp(m, 1.0), ht((size_t)m * m), hn((size_t)m * m, 0.0);
+    std::vector<int> hb(n, 0);
+    if (cfg->task_prios) std::memcpy(hp.data(), cfg->task_prios, sizeof(double) * m);
+    for (int a = 0; a < m; ++a)
+        for (int b = 0; b < m; ++b) ht[(size_t)a * m + b] = cfg->T_trans ? cfg->T_trans[(size_t)a * m + b] : (a != b);
+    if (cfg->neighbor_matrix) std::memcpy(hn.data(), cfg->neighbor_matrix, sizeof(double) * (size_t)m * m);
+    if (cfg->sat_freq_bands) std::memcpy(hb.data(), cfg->sat_freq_bands, sizeof(int) * n);
+    double *prios = nullptr, *tt = nullptr, *nb = nullptr;
+    int *bands = nullptr;
+    hipError_t e = upload(&prios, hp.data(), hp.size());
+    if (e == hipSuccess) e = upload(&tt, ht.data(), ht.size());
+    if (e == hipSuccess) e = upload(&nb, hn.data(), hn.size());
+    if (e == hipSuccess) e = upload(&bands, hb.data(), hb.size());
+    st.prios = prios, st.T_trans = tt, st.nbr = nb, st.bands = bands;
     if (e == hipSuccess) e = hipMalloc(&st.prev, sizeof(int) * (size_t)st.E * n);
+    if (e == hipSuccess) e = hipMalloc(&st.power, sizeof(double) * (size_t)st.E * n);
     if (e == hipSuccess) e = hipMalloc(&st.returns, sizeof(double) * (size_t)st.E);
     if (e == hipSuccess) e = hipMalloc(&st.totT, sizeof(double) * (size_t)st.E * n * m);
     if (e == hipSuccess) e = hipMalloc(&st.topA, sizeof(int) * (size_t)st.E * n * cfg->M);
     if (e == hipSuccess) e = hipMalloc(&st.topD, sizeof(int) * (size_t)st.E * n * (cfg->M + cfg->M / 2));
     if (e == hipSuccess) e = hipMalloc(&st.err, sizeof(int));
-    if (e != hipSuccess) {
-        hipFree(prios), hipFree(tt), hipFree(st.prev), hipFree(st.returns), hipFree(st.err);
-        hipFree(st.totT), hipFree(st.topA), hipFree(st.topD);
-        delete h;
-        return rhip(nullptr, e, "asg_real_create: hipMalloc");
-    }
-    std::vector<double> hp(m, 1.0), ht((size_t)m * m);
-    if (cfg->task_prios) std::memcpy(hp.data(), cfg->task_prios, sizeof(double) * m);
-    for (int a = 0; a < m; ++a)
-        for (int b = 0; b < m; ++b) ht[(size_t)a * m + b] = cfg->T_trans ? cfg->T_trans[(size_t)a * m + b] : (a != b);
-    e = hipMemcpy(prios, hp.data(), sizeof(double) * m, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(tt, ht.data(), sizeof(double) * (size_t)m * m, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemset(st.err, 0, sizeof(int));
     if (e == hipSuccess) e = hipMemset(st.returns, 0, sizeof(double) * (size_t)st.E);
-    st.prios = prios;
-    st.T_trans = tt;
     if (e != hipSuccess) {
         asg_real_destroy(h);
-        return rhip(nullptr, e, "asg_real_create: upload");
+        return rhip(nullptr, e, "asg_real_create");
     }
     *out = h;
     return ASG_OK;
@@ -503,7 +610,11 @@ void asg_real_destroy(asg_real_handle *h) {
     RDeviceGuard g(h->device);
     hipFree(const_cast<double *>(h->st.prios));
     hipFree(const_cast<double *>(h->st.T_trans));
+    hipFree(const_cast<double *>(h->st.nbr));
+    hipFree(const_cast<int *>(h->st.bands));
+    hipFree(const_cast<int64_t *>(h->st.prev0));
     hipFree(h->st.prev);
+    hipFree(h->st.power);
     hipFree(h->st.returns);
     hipFree(h->st.totT);
     hipFree(h->st.topA);
@@ -511,6 +622,40 @@ void asg_real_destroy(asg_real_handle *h) {
     hipFree(h->st.err);
     hipFree(h->table_buf);
     delete h;
+}
+
+int asg_real_set_initial_assignments(asg_real_handle *h, const int64_t *prev0, int64_t count, int on_device) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    RDeviceGuard g(h->device);
+    hipFree(const_cast<int64_t *>(h->st.prev0));
+    h->st.prev0 = nullptr;
+    if (!prev0) return ASG_OK;  // back to Philox draws
+    if (count != 1 && count != h->st.E) return rfail(h, ASG_E_INVALID_ARG, "count must be 1 or num_envs");
+    const size_t elems = (size_t)count * h->st.n;
+    std::vector<int64_t> host(elems);
+    hipError_t e = hipSuccess;
+    if (on_device) {
+        e = hipMemcpyAsync(host.data(), prev0, sizeof(int64_t) * elems, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    } else {
+        std::memcpy(host.data(), prev0, sizeof(int64_t) * elems);
+    }
+    if (e != hipSuccess) return rhip(h, e, "asg_real_set_initial_assignments");
+    for (size_t c = 0; c < (size_t)count; ++c) {  // choice(m, n, replace=False): distinct tasks in [0, m)
+        std::vector<char> seen(h->st.m, 0);
+        for (int i = 0; i < h->st.n; ++i) {
+            const int64_t v = host[c * h->st.n + i];
+            if (v < 0 || v >= h->st.m || seen[v])
+                return rfail(h, ASG_E_INVALID_ARG, "initial assignments must be distinct tasks in [0, m)");
+            seen[v] = 1;
+        }
+    }
+    int64_t *dev = nullptr;
+    e = upload(&dev, host.data(), elems);
+    if (e != hipSuccess) return rhip(h, e, "asg_real_set_initial_assignments");
+    h->st.prev0 = dev;
+    h->st.prev0_env_stride = count == 1 ? 0 : h->st.n;
+    return ASG_OK;
 }
 
 int asg_real_set_benefits(asg_real_handle *h, const double *table, int64_t count, int on_device) {
@@ -550,11 +695,15 @@ int asg_real_set_stream(asg_real_handle *h, void *hip_stream) {
     return ASG_OK;
 }
 
-int asg_real_reset(asg_real_handle *h, const asg_batch_view *view, int ts) {
+int asg_real_reset(asg_real_handle *h, const asg_real_batch_view *view, int ts) {
     if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (!h->table_ready) return rfail(h, ASG_E_STATE, "asg_real_reset: no benefit table (asg_real_set_benefits)");
-    if (int rc = rcheck_view(h, view, false)) return rc;
+    if (!view) return rfail(h, ASG_E_INVALID_ARG, "batch view is NULL");
+    if (int rc = rcheck_view(h, &view->base, false)) return rc;
+    if (view->power_states.ptr && !rfield_ok(view->power_states, {ASG_F16, ASG_F32, ASG_F64}))
+        return rfail(h, ASG_E_INVALID_ARG, "power_states must be a float field");
     RDeviceGuard g(h->device);
+    if (h->has_reset) h->st.episode += 1;  // Philox counter: a fresh draw every episode
     const hipError_t e = launch_real(h, *view, ts, false);
     if (e != hipSuccess) return rhip(h, e, "asg_real_reset");
     h->k = 0;
@@ -562,11 +711,14 @@ int asg_real_reset(asg_real_handle *h, const asg_batch_view *view, int ts) {
     return ASG_OK;
 }
 
-int asg_real_step(asg_real_handle *h, const asg_batch_view *view, int ts) {
+int asg_real_step(asg_real_handle *h, const asg_real_batch_view *view, int ts) {
     if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (!h->has_reset) return rfail(h, ASG_E_STATE, "asg_real_step before asg_real_reset");
     if (h->k >= h->st.T) return rfail(h, ASG_E_STATE, "episode is done: call asg_real_reset");
-    if (int rc = rcheck_view(h, view, true)) return rc;
+    if (!view) return rfail(h, ASG_E_INVALID_ARG, "batch view is NULL");
+    if (int rc = rcheck_view(h, &view->base, true)) return rc;
+    if (view->power_states.ptr && !rfield_ok(view->power_states, {ASG_F16, ASG_F32, ASG_F64}))
+        return rfail(h, ASG_E_INVALID_ARG, "power_states must be a float field");
     RDeviceGuard g(h->device);
     const hipError_t e = launch_real(h, *view, ts, true);
     if (e != hipSuccess) return rhip(h, e, "asg_real_step");

@@ -8,7 +8,7 @@ from functools import partial
 
 from .multiagentenv import MultiAgentEnv
 from .assign_env import AssignEnvBatch, MockConstellationEnv, make_scheme, batch_view
-from .real_env import RealAssignEnvBatch, make_real_scheme
+from .real_env import InterferenceAssignEnvBatch, RealAssignEnvBatch, RealPowerAssignEnvBatch, make_real_scheme
 
 
 def env_fn(env, **kwargs) -> MultiAgentEnv:
@@ -17,4 +17,6 @@ def env_fn(env, **kwargs) -> MultiAgentEnv:
 
 REGISTRY = {"mock_constellation_env": partial(env_fn, env=MockConstellationEnv)}
 BATCHED_REGISTRY = {"mock_constellation_env": partial(env_fn, env=AssignEnvBatch),
-                    "real_constellation_env": partial(env_fn, env=RealAssignEnvBatch)}
+                    "real_constellation_env": partial(env_fn, env=RealAssignEnvBatch),
+                    "real_power_constellation_env": partial(env_fn, env=RealPowerAssignEnvBatch),
+                    "interference_constellation_env": partial(env_fn, env=InterferenceAssignEnvBatch)}

@@ -1,9 +1,12 @@
-"""Batched RealConstellationEnv on MI355X.
+"""Batched RealConstellationEnv family on MI355X.
 
 `RealAssignEnvBatch` owns E RealConstellationEnv episodes (src/envs/real_constellation_env.py)
 on one GPU behind one `asg_real_*` C-ABI handle (include/asg.h): reset / step / the
 top-M / top-N observation builder run as HIP kernels writing straight into an
-EpisodeBatch with the reference's float16 / int16 scheme.
+EpisodeBatch with the reference's float16 / int16 scheme.  `RealPowerAssignEnvBatch`
+(real_power_constellation_env.py) adds per-satellite power states;
+`InterferenceAssignEnvBatch` (interference_constellation_env.py) adds the beam
+interference reward over satellites sharing a frequency band.
 
 Benefits: the constant-benefit path of the reference (sat_prox_mat + graphs injected,
 :55-61) — the orbital simulator that would draw new tasks per reset
@@ -22,15 +25,17 @@ from .assign_env import batch_view
 from .multiagentenv import MultiAgentEnv
 
 
-def obs_size(N, M, L):
-    """RealConstellationEnv.get_obs_size (:251-253)."""
-    return M * L + N * M * L + (N * M // 2) * L + M
+def obs_size(N, M, L, power=False):
+    """get_obs_size (real_constellation_env.py:251-253; + N + 1 power observations in
+    real_power_constellation_env.py:286-290)."""
+    return M * L + N * M * L + (N * M // 2) * L + M + ((N + 1) if power else 0)
 
 
-def make_real_scheme(n, m, L, N, M):
-    """Scheme + preprocess (real_constellation_env.py:74-97): half precision."""
+def make_real_scheme(n, m, L, N, M, power=False):
+    """Scheme + preprocess (real_constellation_env.py:74-97, real_power_constellation_env.py:
+    95-116): half precision; the power variants add power_states."""
     scheme = {
-        "obs": {"vshape": obs_size(N, M, L), "group": "agents", "dtype": torch.float16},
+        "obs": {"vshape": obs_size(N, M, L, power), "group": "agents", "dtype": torch.float16},
         "actions": {"vshape": (1,), "group": "agents", "dtype": torch.int16},
         "avail_actions": {"vshape": (m,), "group": "agents", "dtype": torch.bool},
         "rewards": {"vshape": (n,), "dtype": torch.float16},
@@ -38,16 +43,30 @@ def make_real_scheme(n, m, L, N, M):
         "prev_assigns": {"vshape": (n,), "dtype": torch.int16, "part_of_state": True},
         "beta": {"vshape": (n, m, L), "dtype": torch.float16, "part_of_state": True},
     }
+    if power:
+        scheme["power_states"] = {"vshape": (n,), "dtype": torch.float16, "part_of_state": True}
     preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=m)])}
     return scheme, preprocess
+
+
+def real_batch_view(data):
+    """asg_real_batch_view over an EpisodeBatch (or a dict of its transition tensors)."""
+    td = data.data.transition_data if hasattr(data, "data") else data
+    v = _lib.AsgRealBatchView()
+    v.base = batch_view(td)
+    v.power_states = _lib.field(td.get("power_states"))
+    return v
 
 
 class RealAssignEnvBatch(MultiAgentEnv):
     """E RealConstellationEnv episodes on one GPU, stepped in lockstep by HIP kernels."""
 
+    VARIANT = _lib.ASG_REAL_PLAIN
+
     def __init__(self, num_planes, num_sats_per_plane, m, T, N, M, L, lambda_, sat_prox_mat=None, graphs=None,
                  bids_as_actions=False, seed=None, T_trans=None, task_prios=None, num_envs=1, env_index_base=0,
-                 device=None, rng=None, quirks=()):
+                 device=None, rng=None, quirks=(), sat_freq_bands=None, neighbor_matrix=None,
+                 initial_assignments=None):
         if not torch.cuda.is_available():
             raise RuntimeError("RealAssignEnvBatch needs a ROCm GPU (HIP path only, no CPU fallback)")
         if sat_prox_mat is None:
@@ -72,10 +91,17 @@ class RealAssignEnvBatch(MultiAgentEnv):
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.T_trans = (np.ones((self.m, self.m)) - np.eye(self.m) if T_trans is None
                         else np.ascontiguousarray(T_trans, dtype=np.float64))
+        power = self.VARIANT != _lib.ASG_REAL_PLAIN
+        if task_prios is None and power:
+            # the reference draws choice([1, 1, 1, 5], m) from numpy's global stream
+            task_prios = np.random.RandomState(0 if seed is None else int(seed)).choice([1, 1, 1, 5], size=self.m)
         self.task_prios = (np.ones(self.m) if task_prios is None
                            else np.ascontiguousarray(task_prios, dtype=np.float64))
-        self.obs_space_size = obs_size(self.N, self.M, self.L)
-        self.scheme, self.preprocess = make_real_scheme(self.n, self.m, self.L, self.N, self.M)
+        self.sat_freq_bands = None if sat_freq_bands is None else np.ascontiguousarray(sat_freq_bands, dtype=np.int32)
+        self.neighbor_matrix = (None if neighbor_matrix is None
+                                else np.ascontiguousarray(neighbor_matrix, dtype=np.float64))
+        self.obs_space_size = obs_size(self.N, self.M, self.L, power)
+        self.scheme, self.preprocess = make_real_scheme(self.n, self.m, self.L, self.N, self.M, power)
         self.k = 0
         cfg = _lib.AsgRealConfig()
         cfg.num_envs, cfg.n, cfg.m, cfg.T, cfg.L = self.num_envs, self.n, self.m, self.T, int(L)
@@ -83,6 +109,13 @@ class RealAssignEnvBatch(MultiAgentEnv):
         dp = ctypes.POINTER(ctypes.c_double)
         cfg.T_trans = self.T_trans.ctypes.data_as(dp)
         cfg.task_prios = self.task_prios.ctypes.data_as(dp)
+        cfg.variant = self.VARIANT
+        cfg.seed = (0 if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF
+        cfg.env_index_base = self.env_index_base
+        if self.sat_freq_bands is not None:
+            cfg.sat_freq_bands = self.sat_freq_bands.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        if self.neighbor_matrix is not None:
+            cfg.neighbor_matrix = self.neighbor_matrix.ctypes.data_as(dp)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().asg_real_create(ctypes.byref(cfg), self.device.index,
@@ -90,6 +123,18 @@ class RealAssignEnvBatch(MultiAgentEnv):
         self._h = h
         t = table.to(self.device).contiguous()
         self._call("asg_real_set_benefits", ctypes.c_void_p(t.data_ptr()), t.shape[0], 1)
+        if initial_assignments is not None:
+            self.set_initial_assignments(initial_assignments)
+
+    def set_initial_assignments(self, prev0):
+        """Power variants: use these reset assignments ([n] or [E, n]) instead of Philox
+        draws -- the reference's np.random.choice(m, n, replace=False); None: Philox."""
+        if prev0 is None:
+            self._call("asg_real_set_initial_assignments", None, 0, 0)
+            return
+        p = np.ascontiguousarray(prev0, dtype=np.int64)
+        p2 = p.reshape(1 if p.ndim == 1 else p.shape[0], self.n)
+        self._call("asg_real_set_initial_assignments", p2.ctypes.data_as(ctypes.c_void_p), p2.shape[0], 0)
 
     def _call(self, fn, *args):
         L = _lib.lib()
@@ -112,13 +157,13 @@ class RealAssignEnvBatch(MultiAgentEnv):
     # ------------------------------------------------------------------ hot path
     def reset(self, batch, ts=0):
         """New episode for every env (k = 0, prev_assigns = arange(n)); writes row ts."""
-        self._call("asg_real_reset", ctypes.byref(batch_view(batch)), int(ts))
+        self._call("asg_real_reset", ctypes.byref(real_batch_view(batch)), int(ts))
         self.k = 0
 
     def step(self, batch, ts):
         """Reads actions at row ts; writes rewards / terminated / actions_onehot at ts and
         the next pre-transition row (obs, beta, avail, prev_assigns, filled) at ts + 1."""
-        self._call("asg_real_step", ctypes.byref(batch_view(batch)), int(ts))
+        self._call("asg_real_step", ctypes.byref(real_batch_view(batch)), int(ts))
         self.k += 1
         return self.k >= self.T
 
@@ -163,3 +208,40 @@ class RealAssignEnvBatch(MultiAgentEnv):
 
     def render(self):
         pass
+
+
+class RealPowerAssignEnvBatch(RealAssignEnvBatch):
+    """RealPowerConstellationEnv (real_power_constellation_env.py) batched: power states
+    drained 0.2 per meaningful task, recharged 0.1 otherwise (capped at 1), dead at <= 0;
+    beta_hat zeroed below 1e-12 power; reset assignments are choice(m, n, replace=False)
+    (Philox per global env, or `initial_assignments` for exact parity)."""
+
+    VARIANT = _lib.ASG_REAL_POWER
+
+    def beta_hat(self, beta, prev_assigns, power_states=None):
+        out = super().beta_hat(beta, prev_assigns)
+        if power_states is not None:
+            dead = torch.as_tensor(power_states, device=self.device) < 1e-12
+            out = torch.where(dead[..., None, None], torch.zeros_like(out), out)
+        return out
+
+
+class InterferenceAssignEnvBatch(RealPowerAssignEnvBatch):
+    """InterferenceConstellationEnv (interference_constellation_env.py) batched: the power
+    dynamics plus reward = beta[i, a_i, 0] * 0.5 ** conflicts with the conflicts counted
+    over satellites of the same frequency band through the task neighbour matrix
+    (:309-353).  The orbital simulator that produces sat_prox_mat / neighbor_matrix for
+    coverage tasks is not part of this build: pass them in (constant setup)."""
+
+    VARIANT = _lib.ASG_REAL_INTERFERENCE
+
+    def __init__(self, num_planes, num_sats_per_plane, res=None, T=None, N=None, M=None, L=None, lambda_=None,
+                 task_prios=None, sat_freq_bands=None, bids_as_actions=False, seed=None, sat_prox_mat=None,
+                 neighbor_matrix=None, **kw):
+        if sat_prox_mat is None or neighbor_matrix is None or sat_freq_bands is None:
+            raise ValueError("InterferenceAssignEnvBatch needs sat_prox_mat, neighbor_matrix and sat_freq_bands")
+        tab = np.asarray(sat_prox_mat) if not torch.is_tensor(sat_prox_mat) else sat_prox_mat
+        super().__init__(num_planes, num_sats_per_plane, tab.shape[-2], T, N, M, L, lambda_, sat_prox_mat=sat_prox_mat,
+                         bids_as_actions=bids_as_actions, seed=seed, task_prios=task_prios,
+                         sat_freq_bands=sat_freq_bands, neighbor_matrix=neighbor_matrix, **kw)
+        self.res = res

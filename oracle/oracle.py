@@ -72,6 +72,12 @@ def lib():
         L.ora_real_reset.argtypes = [_dp, _dp, ci, ci, ci, ci, ci, ci, _dp, _i64p, _dp]
         L.ora_real_step.argtypes = [_dp, _dp, _dp, ci, ci, ci, ci, ci, ci, ctypes.c_double,
                                     ctypes.POINTER(ci), _dp, _i64p, _i64p, _dp, ctypes.POINTER(ci), _dp]
+        L.ora_realx_obs_size.argtypes = [ci, ci, ci, ci]
+        L.ora_realx_obs_size.restype = ci
+        L.ora_realx_reset.argtypes = [ci, _dp, _dp, ci, ci, ci, ci, ci, ci, _i64p, _dp, _i64p, _dp, _dp]
+        L.ora_realx_step.argtypes = [ci, _dp, _dp, _dp, ctypes.POINTER(ci), _dp, ci, ci, ci, ci, ci, ci,
+                                     ctypes.c_double, ctypes.POINTER(ci), _dp, _i64p, _dp, _i64p, _dp,
+                                     ctypes.POINTER(ci), _dp]
         _lib = L
     return _lib
 
@@ -251,6 +257,48 @@ class OracleRealEnv:
                             self.T, self.L, self.N, self.M, self.lambda_, ctypes.byref(k), _p(self.beta, _dp),
                             _p(self.prev_assigns, _i64p), _p(a, _i64p), _p(rewards, _dp), ctypes.byref(done),
                             _p(self.obs, _dp))
+        self.k, self.done = k.value, bool(done.value)
+        return rewards, self.done, {}
+
+
+class OracleRealVariantEnv(OracleRealEnv):
+    """RealPowerConstellationEnv (kind "power", real_power_constellation_env.py) and
+    InterferenceConstellationEnv (kind "interference", interference_constellation_env.py)
+    with constant setup; `prev0` plays the reset's np.random.choice(m, n, replace=False)."""
+
+    VARIANTS = {"real": 0, "power": 1, "interference": 2}
+
+    def __init__(self, kind, sat_prox_mat, N, M, L, lambda_, task_prios, prev0, bands=None, neighbor_matrix=None,
+                 T_trans=None):
+        super().__init__(sat_prox_mat, N, M, L, lambda_, T_trans=T_trans, task_prios=task_prios)
+        self.variant = self.VARIANTS[kind]
+        self.prev0 = np.ascontiguousarray(prev0, dtype=np.int64)
+        self.bands = np.ascontiguousarray(bands if bands is not None else np.zeros(self.n), dtype=np.int32)
+        self.nbr = np.ascontiguousarray(neighbor_matrix if neighbor_matrix is not None else np.eye(self.m),
+                                        dtype=np.float64)
+        self.obs_size = lib().ora_realx_obs_size(self.variant, N, M, self.L)
+
+    def reset(self):
+        self.k = 0
+        self.done = False
+        self.beta = np.empty((self.n, self.m, self.L))
+        self.prev_assigns = np.empty(self.n, dtype=np.int64)
+        self.power_states = np.empty(self.n)
+        self.obs = np.empty((self.n, self.obs_size))
+        lib().ora_realx_reset(self.variant, _p(self.table, _dp), _p(self.prios, _dp), self.n, self.m, self.T, self.L,
+                              self.N, self.M, _p(self.prev0, _i64p), _p(self.beta, _dp), _p(self.prev_assigns, _i64p),
+                              _p(self.power_states, _dp), _p(self.obs, _dp))
+        return self.obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int64)
+        rewards = np.empty(self.n)
+        k, done = ctypes.c_int(self.k), ctypes.c_int(0)
+        lib().ora_realx_step(self.variant, _p(self.table, _dp), _p(self.prios, _dp), _p(self.T_trans, _dp),
+                             self.bands.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _p(self.nbr, _dp), self.n,
+                             self.m, self.T, self.L, self.N, self.M, self.lambda_, ctypes.byref(k), _p(self.beta, _dp),
+                             _p(self.prev_assigns, _i64p), _p(self.power_states, _dp), _p(a, _i64p),
+                             _p(rewards, _dp), ctypes.byref(done), _p(self.obs, _dp))
         self.k, self.done = k.value, bool(done.value)
         return rewards, self.done, {}
 

@@ -20,6 +20,7 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   lsa.npz             scipy.optimize.linear_sum_assignment input/output pairs
   runner_dumps.npz    EpisodeRunner / ParallelRunner EpisodeBatch dumps (layout + quirks)
   real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
+  real_variants.npz   RealPowerConstellationEnv / InterferenceConstellationEnv reset/step
 """
 import os
 import sys
@@ -282,6 +283,89 @@ def gen_real_env():
     np.savez_compressed(os.path.join(OUT, "real_env.npz"), **out)
 
 
+def gen_real_variants():
+    """RealPowerConstellationEnv (injected benefits) and InterferenceConstellationEnv
+    (constructed without the orbital simulator: object.__new__ + the attributes its
+    __init__ would have derived from it -- sat_prox_mat, neighbor_matrix -- then the
+    reference's own reset/step).  Strictly positive tables (tie-free orders); power
+    drains over T >= 8 steps so dead agents are exercised."""
+    from collections import defaultdict
+    from envs.real_power_constellation_env import RealPowerConstellationEnv
+    from envs.interference_constellation_env import InterferenceConstellationEnv
+    rng = np.random.RandomState(8765)
+    out = {}
+    specs = [  # (variant, n, m, T, L, N, M, lambda, sparse)
+        ("power", 8, 14, 9, 3, 3, 4, 0.5, False), ("power", 10, 16, 10, 2, 4, 6, 0.3, True),
+        ("interference", 9, 15, 9, 3, 3, 4, 0.5, False), ("interference", 12, 18, 10, 3, 4, 4, 0.4, True)]
+    for idx, (kind, n, m, T, L, N, M, lam, sparse) in enumerate(specs):
+        table = rng.uniform(0.01, 1.0, size=(n, m, T))
+        if sparse:  # some exact zeros (non-meaningful tasks) without creating equal totals
+            table[:, ::5, :] = 0.0
+            table[::3, 1::5, :2] = 0.0
+        prios = rng.choice([1.0, 1.0, 1.0, 5.0], size=m)
+        np.random.seed(500 + idx)
+        if kind == "power":
+            env = RealPowerConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(), graphs=[None] * T,
+                                            task_prios=prios.copy())
+            bands = np.zeros(n, dtype=np.int64)
+            nbr = np.eye(m, dtype=np.int64)
+        else:
+            env = object.__new__(InterferenceConstellationEnv)
+            env.n, env.m, env.T, env.N, env.M, env.L = n, m, T, N, M, min(L, T)
+            env.lambda_, env.beam_types, env.bids_as_actions = lam, 7, False
+            env.k, env.done, env.constant_setup = 0, False, True
+            env.sat_prox_mat = table.copy()
+            nbr = (rng.uniform(size=(m, m)) > 0.7).astype(np.int64)
+            nbr = np.maximum(nbr, nbr.T)
+            np.fill_diagonal(nbr, 1)
+            env.neighbor_matrix = nbr
+            bands = rng.randint(0, 3, size=n)
+            env.sat_freq_bands = bands
+            env.sat_freq_band_dict = defaultdict(list)
+            for i, b in enumerate(bands):
+                env.sat_freq_band_dict[b].append(i)
+            env.task_prios = np.repeat(np.tile(prios, (n, 1))[:, :, np.newaxis], env.L, axis=-1)
+            env.power_states = np.ones(n)
+        env.reset()
+        Le = env.L
+        obs0, beta0 = np.array(env._obs), np.asarray(env.beta).copy()
+        prev0 = np.asarray(env.prev_assigns, dtype=np.int64).copy()
+        acts, rews, obs, betas, dones, prevs, powers = [], [], [], [], [], [], []
+        for t in range(T):
+            if t % 3 == 1:  # crowd a few tasks: collisions and (for interference) neighbours
+                a = rng.randint(0, min(3, m), size=n)
+            else:
+                a = rng.randint(0, m, size=n)
+            r, d, info = env.step(list(a))
+            acts.append(a)
+            rews.append(np.asarray(r, dtype=np.float64))
+            obs.append(np.array(env._obs))
+            betas.append(np.asarray(env.beta).copy())
+            dones.append(bool(d))
+            prevs.append(np.asarray(env.prev_assigns, dtype=np.int64))
+            powers.append(np.asarray(env.power_states, dtype=np.float64).copy())
+        out[f"v{idx}_kind"] = np.array(kind)
+        out[f"v{idx}_spec"] = np.array([n, m, T, Le, N, M])
+        out[f"v{idx}_lambda"] = np.array(lam)
+        out[f"v{idx}_table"] = table
+        out[f"v{idx}_prios"] = prios
+        out[f"v{idx}_bands"] = np.asarray(bands, dtype=np.int64)
+        out[f"v{idx}_nbr"] = np.asarray(nbr, dtype=np.float64)
+        out[f"v{idx}_obs_size"] = np.array(env.get_obs_size())
+        out[f"v{idx}_obs0"] = obs0
+        out[f"v{idx}_beta0"] = beta0
+        out[f"v{idx}_prev0"] = prev0
+        out[f"v{idx}_actions"] = np.stack(acts)
+        out[f"v{idx}_rewards"] = np.stack(rews)
+        out[f"v{idx}_obs"] = np.stack(obs)
+        out[f"v{idx}_beta"] = np.stack(betas)
+        out[f"v{idx}_done"] = np.array(dones)
+        out[f"v{idx}_prev"] = np.stack(prevs)
+        out[f"v{idx}_power"] = np.stack(powers)
+    out["n_cases"] = np.array(len(specs))
+    np.savez_compressed(os.path.join(OUT, "real_variants.npz"), **out)
+
+
 def gen_lsa():
     import scipy.optimize as so
     rng = np.random.RandomState(77)
@@ -410,10 +494,12 @@ def gen_runner_dumps():
 
 if __name__ == "__main__":
     _install_stubs()
-    if sys.argv[1:] == ["real_env"]:  # regenerate only the RealConstellationEnv fixture
+    if sys.argv[1:] == ["real_env"]:  # regenerate only the RealConstellationEnv fixtures
         gen_real_env()
+        gen_real_variants()
         sys.exit(0)
     gen_real_env()
+    gen_real_variants()
     gen_mt_words()
     gen_mock_reset()
     gen_mock_step()

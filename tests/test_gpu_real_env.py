@@ -140,3 +140,77 @@ def test_gpu_runner_drives_real_env():
     assert runner.t_env == E * T
     ret = batch["rewards"][:, :T].double().sum((1, 2)).cpu()
     np.testing.assert_allclose(runner.last_returns.cpu().numpy(), ret.numpy(), rtol=5e-3, atol=5e-3)
+
+
+def _variant_env(kind, table, N, M, L, lam, prios, E, bands=None, nbr=None, prev0=None, seed=0):
+    from marl_sap_amd.envs import InterferenceAssignEnvBatch, RealPowerAssignEnvBatch
+    n, m, T = table.shape[-3:]
+    if kind == "power":
+        return RealPowerAssignEnvBatch(1, n, m, T, N, M, L, lam, sat_prox_mat=table, graphs=[None] * T,
+                                       task_prios=prios, num_envs=E, initial_assignments=prev0, seed=seed,
+                                       device=DEV)
+    return InterferenceAssignEnvBatch(1, n, None, T, N, M, L, lam, task_prios=prios, sat_freq_bands=bands,
+                                      sat_prox_mat=table, neighbor_matrix=nbr, num_envs=E,
+                                      initial_assignments=prev0, seed=seed, device=DEV)
+
+
+def test_real_variants_match_reference_fixture(golden):
+    """RealPowerConstellationEnv / InterferenceConstellationEnv outputs of the reference
+    itself (power drain and death, band conflicts), float16 scheme incl. power_states."""
+    d = golden("real_variants")
+    for c in range(int(d["n_cases"])):
+        n, m, T, L, N, M = (int(x) for x in d[f"v{c}_spec"])
+        env = _variant_env(str(d[f"v{c}_kind"]), d[f"v{c}_table"], N, M, L, float(d[f"v{c}_lambda"]),
+                           d[f"v{c}_prios"], 2, bands=d[f"v{c}_bands"], nbr=d[f"v{c}_nbr"], prev0=d[f"v{c}_prev0"])
+        assert env.obs_space_size == int(d[f"v{c}_obs_size"]) and "power_states" in env.scheme
+        b = new_batch(env, 2)
+        env.reset(b, 0)
+        for e in range(2):
+            check_row(b, e, 0, d[f"v{c}_obs0"], d[f"v{c}_beta0"], d[f"v{c}_prev0"])
+            assert torch.equal(b["power_states"][e, 0].cpu(), f16(np.ones(n)))
+        for t in range(T):
+            b["actions"][:, t, :, 0] = torch.from_numpy(d[f"v{c}_actions"][t]).to(torch.int16).to(DEV)
+            env.step(b, t)
+            for e in range(2):
+                assert torch.equal(b["rewards"][e, t].cpu(), f16(d[f"v{c}_rewards"][t])), (c, t)
+                check_row(b, e, t + 1, d[f"v{c}_obs"][t], d[f"v{c}_beta"][t], d[f"v{c}_prev"][t])
+                assert torch.equal(b["power_states"][e, t + 1].cpu(), f16(d[f"v{c}_power"][t]))
+        env.sync()
+
+
+@pytest.mark.parametrize("kind,n,m,T,L,N,M", [("power", 14, 24, 9, 3, 4, 6), ("interference", 20, 30, 8, 2, 5, 4),
+                                             ("interference", 33, 50, 7, 3, 6, 8)])
+def test_real_variants_match_oracle(oracle, kind, n, m, T, L, N, M):
+    """Per-env sparse tables (equal totals), Philox reset assignments read back from the
+    batch and replayed on the oracle; integer-valued neighbour matrix with self loops."""
+    E = 4
+    rng = np.random.RandomState(n + m)
+    tables = rng.uniform(0.0, 1.0, size=(E, n, m, T)) * (rng.uniform(size=(E, n, m, 1)) > 0.6)
+    prios = rng.choice([1.0, 1.0, 1.0, 5.0], size=m)
+    bands = rng.randint(0, 4, size=n)
+    nbr = (rng.uniform(size=(m, m)) > 0.75).astype(np.float64)
+    nbr = np.maximum(nbr, nbr.T)
+    np.fill_diagonal(nbr, 1.0)
+    env = _variant_env(kind, tables, N, M, L, 0.5, prios, E, bands=bands, nbr=nbr, seed=11)
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    prev0 = b["prev_assigns"][:, 0].cpu().numpy().astype(np.int64)
+    assert all(len(set(p)) == n and p.min() >= 0 and p.max() < m for p in prev0)  # choice(m, n, replace=False)
+    refs = [oracle.OracleRealVariantEnv(kind, tables[e], N, M, L, 0.5, prios, prev0[e], bands=bands,
+                                        neighbor_matrix=nbr) for e in range(E)]
+    for e, r in enumerate(refs):
+        r.reset()
+        check_row(b, e, 0, r.obs, r.beta, r.prev_assigns)
+    for t in range(T):
+        acts = np.where(rng.uniform(size=(E, n)) < 0.3, rng.randint(0, 3, size=(E, n)), rng.randint(0, m, size=(E, n)))
+        b["actions"][:, t, :, 0] = torch.from_numpy(acts).to(torch.int16).to(DEV)
+        env.step(b, t)
+        for e, r in enumerate(refs):
+            rew, _, _ = r.step(acts[e])
+            assert torch.equal(b["rewards"][e, t].cpu(), f16(rew)), (e, t)
+            check_row(b, e, t + 1, r.obs, r.beta, r.prev_assigns)
+            assert torch.equal(b["power_states"][e, t + 1].cpu(), f16(r.power_states))
+    env.sync()
+    # a second episode draws new assignments
+    env.reset(b, 0)
+    assert not np.array_equal(b["prev_assigns"][:, 0].cpu().numpy(), prev0)

@@ -117,3 +117,25 @@ def test_real_env_oracle_matches_reference_fixture(golden, oracle):
             np.testing.assert_array_equal(env.beta, d[f"r{c}_beta"][t])
             np.testing.assert_array_equal(env.prev_assigns, d[f"r{c}_prev"][t])
             assert done == bool(d[f"r{c}_done"][t])
+
+
+def test_real_variant_oracle_matches_reference_fixture(golden, oracle):
+    """RealPowerConstellationEnv / InterferenceConstellationEnv restatement vs the
+    reference's own outputs (power drain and death, band conflicts, handovers)."""
+    d = golden("real_variants")
+    for c in range(int(d["n_cases"])):
+        n, m, T, L, N, M = (int(x) for x in d[f"v{c}_spec"])
+        env = oracle.OracleRealVariantEnv(str(d[f"v{c}_kind"]), d[f"v{c}_table"], N, M, L, float(d[f"v{c}_lambda"]),
+                                          d[f"v{c}_prios"], d[f"v{c}_prev0"], bands=d[f"v{c}_bands"],
+                                          neighbor_matrix=d[f"v{c}_nbr"])
+        assert env.obs_size == int(d[f"v{c}_obs_size"])
+        np.testing.assert_array_equal(env.reset(), d[f"v{c}_obs0"])
+        np.testing.assert_array_equal(env.beta, d[f"v{c}_beta0"])
+        for t in range(T):
+            r, done, _ = env.step(d[f"v{c}_actions"][t])
+            np.testing.assert_array_equal(r, d[f"v{c}_rewards"][t])
+            np.testing.assert_array_equal(env.power_states, d[f"v{c}_power"][t])
+            np.testing.assert_array_equal(env.obs, d[f"v{c}_obs"][t])
+            np.testing.assert_array_equal(env.beta, d[f"v{c}_beta"][t])
+            np.testing.assert_array_equal(env.prev_assigns, d[f"v{c}_prev"][t])
+            assert done == bool(d[f"v{c}_done"][t])
