@@ -121,6 +121,79 @@ __device__ __forceinline__ int wave_select(const double *vals, unsigned char *ta
     return key;
 }
 
+// Top-K of vals[0..len) in the same order as K successive wave_select calls, for short
+// lists (len <= 64 * CAP): every lane sorts its own CAP candidates (j = lane + 64 c) once
+// in registers, then each pick is two wave reductions over the lanes' list heads and a
+// register shift in the winning lane -- no rescans, no LDS round trips.
+template <int CAP, bool HIGHER_TIES>
+__device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int K, int *out) {
+    const int lane = threadIdx.x & 63;
+    double v[CAP];
+    int id[CAP];
+#pragma unroll
+    for (int c = 0; c < CAP; ++c) {
+        const int j = lane + 64 * c;
+        v[c] = j < len ? vals[j] : -INFINITY;
+        id[c] = j < len ? j : -1;  // -1: no candidate (sorts last, never wins)
+    }
+    auto before = [](double va, int ia, double vb, int ib) {
+        if (ia < 0) return false;
+        if (ib < 0) return true;
+        return va > vb || (va == vb && (HIGHER_TIES ? ia > ib : ia < ib));
+    };
+#pragma unroll
+    for (int pass = 0; pass < CAP; ++pass)  // odd-even transposition sort, fully unrolled
+#pragma unroll
+        for (int c = pass & 1; c + 1 < CAP; c += 2)
+            if (before(v[c + 1], id[c + 1], v[c], id[c])) {
+                const double tv = v[c];
+                v[c] = v[c + 1];
+                v[c + 1] = tv;
+                const int ti = id[c];
+                id[c] = id[c + 1];
+                id[c + 1] = ti;
+            }
+    for (int k = 0; k < K; ++k) {
+        const bool has = id[0] >= 0;
+        const double vmax =
+            wave_allreduce(has ? v[0] : -INFINITY, [](double a, double b) { return a > b ? a : b; });
+        const bool cand = has && v[0] == vmax;
+        const int win = HIGHER_TIES ? wave_max_i32(cand ? id[0] : -1) : -wave_max_i32(cand ? -id[0] : -0x7fffffff);
+        if (lane == 0) out[k] = win;
+        if (id[0] == win) {
+#pragma unroll
+            for (int c = 0; c + 1 < CAP; ++c) {
+                v[c] = v[c + 1];
+                id[c] = id[c + 1];
+            }
+            v[CAP - 1] = -INFINITY;
+            id[CAP - 1] = -1;
+        }
+    }
+}
+
+// top-K: register heads when len <= 64 * CAP (CAP > 0, chosen per kernel instance so each
+// gets its own register budget), else K rescans (CAP = 0; taken: [len] scratch)
+template <int CAP, bool HIGHER_TIES>
+__device__ __forceinline__ void wave_topk(const double *vals, int len, int K, int *out, unsigned char *taken) {
+    if constexpr (CAP > 0) {
+        wave_topk_heads<CAP, HIGHER_TIES>(vals, len, K, out);
+    } else {
+        const int lane = threadIdx.x & 63;
+        for (int j = lane; j < len; j += 64) taken[j] = 0;
+        wave_sync();
+        for (int c = 0; c < K; ++c) {
+            const int j = wave_select<HIGHER_TIES>(vals, taken, len);
+            if (lane == 0) {
+                out[c] = j;
+                taken[j] = 1;
+            }
+            wave_sync();
+        }
+    }
+    wave_sync();
+}
+
 // ---- kernel 1: the transition of each env (step only), one workgroup per env ---------------
 // LDS: actions [n] int, counts [m] int, rewards [n] f64, applicable [n] int
 __host__ __device__ __forceinline__ size_t transition_lds(int n, int m) {
@@ -263,6 +336,7 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
     return (size_t)S * m * 8 + (size_t)S * ((m + 3) & ~3);
 }
 
+template <int CAP>
 __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
                                                           int knew, int step, int S) {
     extern __shared__ unsigned char s_raw[];
@@ -275,18 +349,54 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
     const double *tab = st.table + e * st.table_env_stride;
     int *prev = st.prev + e * n;
     const int row = step ? ts + 1 : ts;
-    for (int64_t p = threadIdx.x; p < (int64_t)rows * m; p += blockDim.x) {
-        const int r = (int)(p / m), j = (int)(p - (int64_t)r * m), i = i0 + r;
-        double sum = 0.0;
-        for (int l = 0; l < L; ++l) {
-            const double b = real_beta(st, tab, knew, i, j, l);
-            sum = l == 0 ? b : sum + b;
-            if (bv.beta.ptr) store_real(bv.beta, foff(bv.beta, e, row, i, j) + l, b);
+    // one wave per agent row of the strip, lanes along the tasks: per row the field bases
+    // are computed once; the scheme's own dtypes (f16 beta, bool avail, i16 one-hot) take
+    // typed stores, anything else the generic ones
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    const bool fast = bv.beta.dtype == ASG_F16 && bv.avail_actions.dtype == ASG_BOOL &&
+                      (!step || bv.actions_onehot.dtype == ASG_I16) && bv.beta.ptr && bv.avail_actions.ptr &&
+                      (!step || bv.actions_onehot.ptr);
+    for (int r = wave; r < rows; r += waves) {
+        const int i = i0 + r;
+        const double *t0 = tab + ((int64_t)knew * n + i) * m;  // slice knew, row i
+        const int64_t slice = (int64_t)n * m;
+        int eff = st.T - knew < L ? st.T - knew : L;
+        eff = eff < 0 ? 0 : eff;
+        const int pa = prev[i];
+        double *trow = tl + (int64_t)r * m;
+        if (fast) {
+            __half *bb = reinterpret_cast<__half *>(bv.beta.ptr) + foff(bv.beta, e, row, i, 0);
+            uint8_t *ab = reinterpret_cast<uint8_t *>(bv.avail_actions.ptr) + foff(bv.avail_actions, e, row, i, 0);
+            int16_t *ob = step ? reinterpret_cast<int16_t *>(bv.actions_onehot.ptr) + foff(bv.actions_onehot, e, ts, i, 0)
+                               : nullptr;
+            const int64_t bs3 = bv.beta.stride[3], as3 = bv.avail_actions.stride[3];
+            const int64_t os3 = step ? bv.actions_onehot.stride[3] : 0;
+            for (int j = lane; j < m; j += 64) {
+                const double pr = st.prios[j];
+                double sum = 0.0;
+                for (int l = 0; l < L; ++l) {
+                    const double b = (l < eff ? t0[l * slice + j] : 0.0) * pr;
+                    sum = l == 0 ? b : sum + b;
+                    bb[j * bs3 + l] = __float2half((float)b);
+                }
+                trow[j] = sum;
+                ab[j * as3] = 1;
+                if (step) ob[j * os3] = (int16_t)(pa == j);
+            }
+        } else {
+            for (int j = lane; j < m; j += 64) {
+                double sum = 0.0;
+                for (int l = 0; l < L; ++l) {
+                    const double b = real_beta(st, tab, knew, i, j, l);
+                    sum = l == 0 ? b : sum + b;
+                    if (bv.beta.ptr) store_real(bv.beta, foff(bv.beta, e, row, i, j) + l, b);
+                }
+                trow[j] = sum;
+                if (bv.avail_actions.ptr) store_int(bv.avail_actions, foff(bv.avail_actions, e, row, i, j), 1);
+                if (step && bv.actions_onehot.ptr)
+                    store_int(bv.actions_onehot, foff(bv.actions_onehot, e, ts, i, j), pa == j);
+            }
         }
-        tl[p] = sum;
-        if (bv.avail_actions.ptr) store_int(bv.avail_actions, foff(bv.avail_actions, e, row, i, j), 1);
-        if (step && bv.actions_onehot.ptr)
-            store_int(bv.actions_onehot, foff(bv.actions_onehot, e, ts, i, j), step ? prev[i] == j : 0);
     }
     if (bv.prev_assigns.ptr)
         for (int r = threadIdx.x; r < rows; r += blockDim.x)
@@ -303,33 +413,12 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
         totT[(int64_t)j * n + i0 + r] = tl[(int64_t)r * m + j];
     }
     // rank each agent row of the strip, one wave per row
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
     unsigned char *taken = taken_all + (size_t)wave * ((m + 3) & ~3);
     for (int r = wave; r < rows; r += waves) {
         const double *vals = tl + (int64_t)r * m;
         const int a = i0 + r;
-        for (int j = lane; j < m; j += 64) taken[j] = 0;
-        wave_sync();
-        int *outA = st.topA + (e * n + a) * (int64_t)M;
-        for (int c = 0; c < M; ++c) {
-            const int j = wave_select<false>(vals, taken, m);
-            if (lane == 0) {
-                outA[c] = j;
-                taken[j] = 1;
-            }
-            wave_sync();
-        }
-        for (int j = lane; j < m; j += 64) taken[j] = 0;
-        wave_sync();
-        int *outD = st.topD + (e * n + a) * (int64_t)MD;
-        for (int c = 0; c < MD; ++c) {
-            const int j = wave_select<true>(vals, taken, m);
-            if (lane == 0) {
-                outD[c] = j;
-                taken[j] = 1;
-            }
-            wave_sync();
-        }
+        wave_topk<CAP, false>(vals, m, M, st.topA + (e * n + a) * (int64_t)M, taken);
+        wave_topk<CAP, true>(vals, m, MD, st.topD + (e * n + a) * (int64_t)MD, taken);
     }
 }
 
@@ -342,13 +431,18 @@ __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, i
 
 // Observation pass, one wave per (env, agent i): competitors from the task-major totals,
 // their "other" tasks from topD, then the row (real_constellation_env.py:186-219).
-__global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew) {
+// XCD-aware grid: workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD
+// b % 8), so block b serves env 8 * ((b / 8) / G) + b % 8: all G workgroups of an env
+// land on one XCD and its [m][n] totals are fetched into one L2, not eight.
+template <int CAP>
+__global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, N = st.N, M = st.M, M2 = st.M / 2, MD = st.M + st.M / 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
-    const int64_t e = blockIdx.y;
-    const int i = blockIdx.x * waves + wave;
-    if (i >= n) return;
+    const int64_t k = blockIdx.x / 8;
+    const int64_t e = (int64_t)(blockIdx.x % 8) + 8 * (k / G);
+    const int i = (int)(k % G) * waves + wave;
+    if (e >= st.E || i >= n) return;
     const int osz = M * L + N * M * L + ((N * M) / 2) * L + M + (st.variant != ASG_REAL_PLAIN ? N + 1 : 0);
     if (knew >= st.T) {  // done: zero observations (:221-224)
         for (int p = lane; p < osz; p += 64) store_real(bv.obs, foff(bv.obs, e, row, i, 0) + p, 0.0);
@@ -377,14 +471,7 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     }
     wave_sync();
     // (c) the N strongest competitors (np.argsort(-best)[:N])
-    for (int c = 0; c < N; ++c) {
-        const int a = wave_select<false>(best, taken, n);
-        if (lane == 0) {
-            topn[c] = a;
-            taken[a] = 1;
-        }
-        wave_sync();
-    }
+    wave_topk<CAP, false>(best, n, N, topn, taken);
     // (d) competitor q's M/2 best tasks outside agent i's top M: the first M/2 entries of
     //     its topD list not in top[], stored ascending (largest picked first)
     for (int q = lane; q < N; q += 64) {
@@ -404,22 +491,43 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     const int64_t o0 = foff(bv.obs, e, row, i, 0);
     const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L, r4 = r3 + M;
     const double *pw = st.power + e * n;
+    // benefit entries are copied from the batch's beta row just written by the strip
+    // kernel when it holds the same element type (the stored value is the same rounding
+    // of the same float64: 3 L-contiguous elements per (agent, task) instead of 3 table
+    // lines); otherwise recomputed from the table
+    const bool copy = bv.beta.ptr && bv.beta.dtype == bv.obs.dtype;
+    const int64_t b0 = copy ? foff(bv.beta, e, row, 0, 0) : 0;
+    auto bval = [&](int a, int j, int l, int p) {
+        if (copy) {
+            const int64_t src = b0 + a * bv.beta.stride[2] + j * bv.beta.stride[3] + l;
+            switch (bv.obs.dtype) {
+                case ASG_F16:
+                    reinterpret_cast<uint16_t *>(bv.obs.ptr)[o0 + p] = reinterpret_cast<const uint16_t *>(bv.beta.ptr)[src];
+                    return;
+                case ASG_F32:
+                    reinterpret_cast<float *>(bv.obs.ptr)[o0 + p] = reinterpret_cast<const float *>(bv.beta.ptr)[src];
+                    return;
+                default:
+                    reinterpret_cast<double *>(bv.obs.ptr)[o0 + p] = reinterpret_cast<const double *>(bv.beta.ptr)[src];
+                    return;
+            }
+        }
+        store_real(bv.obs, o0 + p, real_beta(st, tab, knew, a, j, l));
+    };
     for (int p = lane; p < osz; p += 64) {
-        double v;
         if (p < r1) {
-            v = real_beta(st, tab, knew, i, top[p / L], p % L);
+            bval(i, top[p / L], p % L, p);
         } else if (p < r2) {
             const int x = p - r1, q = x / (M * L), y = x - q * M * L;
-            v = real_beta(st, tab, knew, topn[q], top[y / L], y % L);
+            bval(topn[q], top[y / L], y % L, p);
         } else if (p < r3) {
             const int x = p - r2, q = x / (M2 * L), y = x - q * M2 * L;
-            v = real_beta(st, tab, knew, topn[q], oth[q * M2 + y / L], y % L);
+            bval(topn[q], oth[q * M2 + y / L], y % L, p);
         } else if (p < r4) {
-            v = top[p - r3] == pi ? 1.0 : 0.0;
+            store_real(bv.obs, o0 + p, top[p - r3] == pi ? 1.0 : 0.0);
         } else {  // [power_i, power[top_n]] (real_power_constellation_env.py:226-229)
-            v = p == r4 ? pw[i] : pw[topn[p - r4 - 1]];
+            store_real(bv.obs, o0 + p, p == r4 ? pw[i] : pw[topn[p - r4 - 1]]);
         }
-        store_real(bv.obs, o0 + p, v);
     }
 }
 
@@ -495,6 +603,12 @@ int rcheck_view(asg_real_handle *h, const asg_batch_view *b, bool step) {
     return ASG_OK;
 }
 
+// candidates per lane of a top-K over `len` values: 1, 2, 4, 8, 16, or 0 (> 1024: rescans)
+int cap_of(int len) {
+    const int c = (len + 63) / 64;
+    return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : c <= 8 ? 8 : c <= 16 ? 16 : 0;
+}
+
 int strip_height(const RealState &st) {
     int S = 16;
     while (S > 1 && asg::strip_lds(S, st.m) > 64 * 1024) S >>= 1;
@@ -517,15 +631,39 @@ hipError_t launch_real(asg_real_handle *h, const asg_real_batch_view &v, int ts,
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int S = strip_height(st);
-    hipLaunchKernelGGL(asg::real_strip_kernel, dim3((unsigned)((st.n + S - 1) / S), (unsigned)st.E), dim3(64 * S),
-                       asg::strip_lds(S, st.m), h->stream, bv, v.power_states, st, ts, knew, (int)step, S);
+    const dim3 sgrid((unsigned)((st.n + S - 1) / S), (unsigned)st.E);
+    const size_t slds = asg::strip_lds(S, st.m);
+#define STRIP_(CAP) \
+    hipLaunchKernelGGL(asg::real_strip_kernel<CAP>, sgrid, dim3(64 * S), slds, h->stream, bv, v.power_states, st, ts, \
+                       knew, (int)step, S)
+    switch (cap_of(st.m)) {
+        case 1: STRIP_(1); break;
+        case 2: STRIP_(2); break;
+        case 4: STRIP_(4); break;
+        case 8: STRIP_(8); break;
+        case 16: STRIP_(16); break;
+        default: STRIP_(0); break;
+    }
+#undef STRIP_
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t per_wave = asg::real_obs_lds_per_wave(st.n, st.m, st.N, st.M);
     int waves = 4;
     while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
-    const dim3 grid((unsigned)((st.n + waves - 1) / waves), (unsigned)st.E);
-    hipLaunchKernelGGL(asg::real_obs_kernel, grid, dim3(64 * waves), per_wave * waves, h->stream, bv, st, row, knew);
+    const int G = (st.n + waves - 1) / waves;
+    const dim3 grid((unsigned)(8 * ((st.E + 7) / 8) * G));
+#define OBS_(CAP)                                                                                                 \
+    hipLaunchKernelGGL(asg::real_obs_kernel<CAP>, grid, dim3(64 * waves), per_wave * waves, h->stream, bv, st, row, \
+                       knew, G)
+    switch (cap_of(st.n)) {
+        case 1: OBS_(1); break;
+        case 2: OBS_(2); break;
+        case 4: OBS_(4); break;
+        case 8: OBS_(8); break;
+        case 16: OBS_(16); break;
+        default: OBS_(0); break;
+    }
+#undef OBS_
     return hipGetLastError();
 }
 
