@@ -104,3 +104,33 @@ def test_cpu_baseline_runs():
     from oracle.cpu_parallel_runner import run_parallel_baseline
     rate, steps, secs = run_parallel_baseline(n=4, m=4, T=3, L=1, workers=2, episodes=1)
     assert steps == 6 and rate > 0
+
+
+def test_real_env_schemes_match_reference_sizes(golden):
+    """RealConstellationEnv-family schemes (real_constellation_env.py:74-97,
+    real_power_constellation_env.py:95-116): float16 obs of get_obs_size(), int16
+    actions / prev_assigns, [n, m, L] beta, power_states only for the power variants."""
+    import torch
+    from marl_sap_amd.envs.real_env import make_real_scheme, obs_size
+    d = golden("real_env")
+    for c in range(int(d["n_cases"])):
+        n, m, T, L, N, M = (int(x) for x in d[f"r{c}_spec"])
+        scheme, pre = make_real_scheme(n, m, L, N, M)
+        assert scheme["obs"]["vshape"] == obs_size(N, M, L) == int(d[f"r{c}_obs_size"]) == d[f"r{c}_obs0"].shape[1]
+        assert scheme["obs"]["dtype"] == torch.float16 and scheme["actions"]["dtype"] == torch.int16
+        assert scheme["beta"]["vshape"] == (n, m, L) and "power_states" not in scheme
+        assert pre["actions"][0] == "actions_onehot"
+    v = golden("real_variants")
+    for c in range(int(v["n_cases"])):
+        n, m, T, L, N, M = (int(x) for x in v[f"v{c}_spec"])
+        scheme, _ = make_real_scheme(n, m, L, N, M, power=True)
+        assert scheme["obs"]["vshape"] == int(v[f"v{c}_obs_size"]) == v[f"v{c}_obs0"].shape[1]
+        assert scheme["power_states"]["vshape"] == (n,) and scheme["power_states"]["dtype"] == torch.float16
+
+
+def test_bench_accounting():
+    """The algorithmic figures bench.py divides by."""
+    import bench
+    assert bench.step_bytes(64, 64, 3) == 120073
+    assert bench.step_bytes(16, 16, 3) == 16 * 16 * 29 + 16 * 20 + 9
+    assert bench.agent_flops(64, 64, 3) == 90112  # 2 * (256*64 + 2*3*64*64 + 64*64)
