@@ -359,7 +359,7 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
 }
 
 static bool agent_shape_ok(int K, int hidden, int n_out) {
-    return hidden == 64 && n_out > 0 && n_out <= 256 && n_out % 16 == 0 && K > 0 && K % 4 == 0;
+    return hidden == 64 && n_out > 0 && n_out <= 512 && K > 0;
 }
 
 int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn) {
@@ -373,7 +373,7 @@ int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, co
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_pack: NULL weight or output");
     if (!agent_shape_ok(K, hidden, n_out))
         return fail(nullptr, ASG_E_INVALID_ARG,
-                    "asg_rnn_agent_pack: needs hidden == 64, n_out a multiple of 16 up to 256, K % 4 == 0");
+                    "asg_rnn_agent_pack: needs hidden == 64, 1 <= n_out <= 512, K >= 1");
     hipError_t e = asg::launch_rnn_agent_pack(W1, W_ih, W_hh, W2, K, n_out, use_rnn, static_cast<float4 *>(packed),
                                               static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_pack");
@@ -384,11 +384,11 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
                           int hidden, int n_out, int use_rnn, float *h_out, float *q_out, void *hip_stream) {
     if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !q_out || R < 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: bad arguments");
-    if (!agent_shape_ok(K, hidden, n_out) || x_stride % 4 != 0 || h_stride % 4 != 0 ||
-        (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
+    if (!agent_shape_ok(K, hidden, n_out) || x_stride < K || h_stride % 4 != 0 ||
+        (reinterpret_cast<uintptr_t>(x) % 4) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG,
-                    "asg_rnn_agent_forward: needs hidden == 64, n_out a multiple of 16 up to 256, K % 4 == 0 and 16-B "
-                    "aligned rows");
+                    "asg_rnn_agent_forward: needs hidden == 64, 1 <= n_out <= 512, x_stride >= K and 16-B aligned "
+                    "h rows");
     if (R == 0) return ASG_OK;
     hipError_t e = asg::launch_rnn_agent_fwd(x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed),
                                              b1, b_ih, b_hh, b2, n_out, use_rnn, h_out, q_out, nullptr,
@@ -404,8 +404,8 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
     if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !avail || !avail_strides || !out || !out_strides ||
         !status || R < 0 || n <= 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: bad arguments");
-    if (!agent_shape_ok(K, hidden, n_out) || x_stride % 4 != 0 || h_stride % 4 != 0 ||
-        (reinterpret_cast<uintptr_t>(x) % 16) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
+    if (!agent_shape_ok(K, hidden, n_out) || x_stride < K || h_stride % 4 != 0 ||
+        (reinterpret_cast<uintptr_t>(x) % 4) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: unsupported shape / alignment");
     if (!(epsilon >= 0.0 && epsilon <= 1.0))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: epsilon must be in [0, 1]");

@@ -57,22 +57,24 @@ __device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
 // (t, ct) holds, for lane l, W[16 ct + (l & 15)][16 t + 4 (l >> 4) .. + 3] as one float4,
 // so one wave loads a whole MFMA B-operand chunk as 1 KiB of contiguous memory.  K is
 // zero-padded to a multiple of 16.  Offsets (in float4) of the four matrices:
-//   W1: [K16/16][4][64]; W_ih: [4][12][64]; W_hh: [4][12][64] (GRU) ; W2: [4][nq][64]
+//   W1: [K16/16][4][64]; W_ih: [4][12][64]; W_hh: [4][12][64] (GRU) ; W2: [4][nq][64],
+//   nq = ceil(n_out / 16) (zero rows pad the last output tile)
 __device__ __forceinline__ int64_t pk(int t, int ct, int nct, int lane) { return ((int64_t)t * nct + ct) * 64 + lane; }
 
 __global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
-    const int nct = C / 16, nt = (K + 15) / 16;
+    const int nct = (C + 15) / 16, nt = (K + 15) / 16;  // rows >= C (the n_out tail) are zero
     const int64_t total = (int64_t)nt * nct * 64;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int lane = (int)(i & 63);
         const int ct = (int)((i >> 6) % nct);
         const int t = (int)((i >> 6) / nct);
         const int row = 16 * ct + (lane & 15), k = 16 * t + 4 * (lane >> 4);
+        const bool okr = row < C;
         float4 v;
-        v.x = k + 0 < K ? W[(int64_t)row * K + k + 0] : 0.f;
-        v.y = k + 1 < K ? W[(int64_t)row * K + k + 1] : 0.f;
-        v.z = k + 2 < K ? W[(int64_t)row * K + k + 2] : 0.f;
-        v.w = k + 3 < K ? W[(int64_t)row * K + k + 3] : 0.f;
+        v.x = okr && k + 0 < K ? W[(int64_t)row * K + k + 0] : 0.f;
+        v.y = okr && k + 1 < K ? W[(int64_t)row * K + k + 1] : 0.f;
+        v.z = okr && k + 2 < K ? W[(int64_t)row * K + k + 2] : 0.f;
+        v.w = okr && k + 3 < K ? W[(int64_t)row * K + k + 3] : 0.f;
         out[i] = v;
     }
 }
@@ -88,9 +90,14 @@ __global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
 // t = mt, so activations go from layer to layer in registers: no LDS, no transposes, no
 // barriers.  One wave owns 32 rows (nt = 0, 1); lane (r, q) = (l & 15, l >> 4).
 // ---------------------------------------------------------------------------------
-// n_out <= 256 (checked by the ABI): a lane keeps 4 availability bits per output tile in a u64
+// GEN = false: the bench shapes (K % 4 == 0 with 16-B aligned rows, n_out % 16 == 0, n_out
+// <= 256).  GEN = true: any K, any n_out <= 512 (checked by the ABI): guarded scalar row
+// loads, and the last output tile partial when n_out % 16 != 0 (zero weight rows, masked
+// bias / Q / availability).  A lane keeps 4 availability bits per output tile in two u64
+// (tiles 0-15, 16-31; the second only with GEN).  The general path costs ~3 % at the
+// bench shape, hence the two instantiations.
 
-template <bool RNN, bool SEL>
+template <bool RNN, bool SEL, bool GEN>
 __device__ __forceinline__ void agent_rows(
     int64_t row0, const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
@@ -119,12 +126,24 @@ __device__ __forceinline__ void agent_rows(
         }
         const float *xr[2] = {X + (ok[0] ? rows[0] : 0) * xs, X + (ok[1] ? rows[1] : 0) * xs};
         const int nk = (K + 15) / 16;
+        // float4 row loads when K, the row stride and X are 16-B aligned; else guarded scalars
+        const bool xvec = !GEN || (((K | xs) & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0);
         float4 a0[2], w0[4], a1[2], w1[4];
         auto load = [&](int t, float4 (&a4)[2], float4 (&w4)[4]) {
             const int k = 16 * t + 4 * q;
-            const bool okk = k < K;  // K % 4 == 0 (checked on the host)
+            if (xvec) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && okk);
+                for (int nt = 0; nt < 2; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && k < K);
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    const float *p = xr[nt] + k;
+                    a4[nt].x = ok[nt] && k + 0 < K ? p[0] : 0.f;
+                    a4[nt].y = ok[nt] && k + 1 < K ? p[1] : 0.f;
+                    a4[nt].z = ok[nt] && k + 2 < K ? p[2] : 0.f;
+                    a4[nt].w = ok[nt] && k + 3 < K ? p[3] : 0.f;
+                }
+            }
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) w4[mt] = W1p[pk(t, mt, 4, lane)];
         };
@@ -245,7 +264,7 @@ __device__ __forceinline__ void agent_rows(
     bool av4 = false;
     float best[2] = {-__builtin_inff(), -__builtin_inff()};
     int bj[2] = {0x7fffffff, 0x7fffffff};
-    uint64_t amask[2] = {0, 0};  // bit 4c + v <-> task 16 c + 4 q + v
+    uint64_t amask[2][2] = {{0, 0}, {0, 0}};  // [row][c >> 4] bit 4 (c & 15) + v <-> task 16 c + 4 q + v
     int64_t oidx[2] = {0, 0};
     if (SEL) {
         const int64_t b0 = row0 / sel.n;
@@ -265,16 +284,22 @@ __device__ __forceinline__ void agent_rows(
     }
 
     // ---- fc2 one 16-output tile at a time: q^T = W2 h'^T + b2; Q store and/or argmax ----
-    const int nct = nout / 16;
+    const int nct = (nout + 15) / 16;
+    const bool qvec = !GEN || (nout & 3) == 0;
     for (int c = 0; c < nct; ++c) {
+        const bool full = !GEN || 16 * c + 16 <= nout;  // wave-uniform: only the last tile can be partial
+        const int j0 = 16 * c + 4 * q;          // this lane's first task of the tile
         uint32_t av[2] = {0u, 0u};  // 4 availability bits of this lane's tasks, per row
         if (SEL) {
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) {
-                const uint8_t *ap = arow[nt] + 16 * c + 4 * q;
+                const uint8_t *ap = arow[nt] + j0;
                 uint32_t w = 0;
                 if (ok[nt]) {
-                    if (av4) {
+                    if (!full) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) w |= j0 + e < nout ? (uint32_t)ap[e] << (8 * e) : 0u;
+                    } else if (av4) {
                         w = *reinterpret_cast<const uint32_t *>(ap);
                     } else {
                         w = (uint32_t)ap[0] | ((uint32_t)ap[1] << 8) | ((uint32_t)ap[2] << 16) | ((uint32_t)ap[3] << 24);
@@ -284,7 +309,15 @@ __device__ __forceinline__ void agent_rows(
                          ((w >> 24) != 0) << 3;
             }
         }
-        const float4 bq = *reinterpret_cast<const float4 *>(b2 + 16 * c + 4 * q);
+        float4 bq;
+        if (full) {
+            bq = *reinterpret_cast<const float4 *>(b2 + j0);
+        } else {
+            bq.x = j0 + 0 < nout ? b2[j0 + 0] : 0.f;
+            bq.y = j0 + 1 < nout ? b2[j0 + 1] : 0.f;
+            bq.z = j0 + 2 < nout ? b2[j0 + 2] : 0.f;
+            bq.w = j0 + 3 < nout ? b2[j0 + 3] : 0.f;
+        }
         f32x4 a2[2] = {f32x4{bq.x, bq.y, bq.z, bq.w}, f32x4{bq.x, bq.y, bq.z, bq.w}};
         float4 w2[4];
 #pragma unroll
@@ -297,19 +330,28 @@ __device__ __forceinline__ void agent_rows(
                 for (int nt = 0; nt < 2; ++nt) a2[nt] = mfma4(comp(w2[t], e), hp[t][nt][e], a2[nt]);
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
-            if (Q && ok[nt])
-                *reinterpret_cast<float4 *>(Q + rows[nt] * nout + 16 * c + 4 * q) =
-                    make_float4(a2[nt][0], a2[nt][1], a2[nt][2], a2[nt][3]);
+            if (Q && ok[nt]) {
+                float *qp = Q + rows[nt] * nout + j0;
+                if (full && qvec) {
+                    *reinterpret_cast<float4 *>(qp) = make_float4(a2[nt][0], a2[nt][1], a2[nt][2], a2[nt][3]);
+                } else {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (j0 + v < nout) qp[v] = a2[nt][v];
+                }
+            }
             if (SEL) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
-                    const int j = 16 * c + 4 * q + v;
+                    const int j = j0 + v;
                     const float x = ((av[nt] >> v) & 1u) ? a2[nt][v] : -__builtin_inff();
                     const bool b = better(x, j, best[nt], bj[nt]);
                     best[nt] = b ? x : best[nt];
                     bj[nt] = b ? j : bj[nt];
                 }
-                amask[nt] |= (uint64_t)av[nt] << (4 * c);
+                const uint64_t bits = (uint64_t)av[nt] << (4 * (c & 15));
+                if (!GEN || c < 16) amask[nt][0] |= bits;
+                else amask[nt][1] |= bits;
             }
         }
     }
@@ -353,7 +395,7 @@ __device__ __forceinline__ void agent_rows(
         int target = -1, found = -1;
         for (int ntt = 0; ntt < 2; ++ntt) {
             const bool mine_row = explore && nt == ntt;
-            int cnt = __popcll(amask[ntt]);
+            int cnt = __popcll(amask[ntt][0]) + (GEN ? __popcll(amask[ntt][1]) : 0);
             {
                 const SwapPair c16 = swap16((uint32_t)cnt);
                 const SwapPair c32 = swap32(c16.a + c16.b);
@@ -364,7 +406,7 @@ __device__ __forceinline__ void agent_rows(
                 else target = (int)(((uint64_t)rr.y * (uint64_t)cnt) >> 32);
             }
             for (int w = 0; w < nwin; ++w) {
-                const uint32_t mine = (uint32_t)(amask[ntt] >> (16 * w)) & 0xFFFFu;
+                const uint32_t mine = (uint32_t)(((GEN && w >= 4) ? amask[ntt][1] : amask[ntt][0]) >> (16 * (w & 3))) & 0xFFFFu;
                 uint32_t lo = 0, hi = 0;  // this lane's tasks of the window, in task order
 #pragma unroll
                 for (int c = 0; c < 2; ++c) lo |= ((mine >> (4 * c)) & 0xFu) << (16 * c + 4 * q);
@@ -400,7 +442,7 @@ __device__ __forceinline__ void agent_rows(
 }
 
 // One wave per 32 rows, weights read through L1/L2 (any n_out).
-template <bool RNN, bool SEL>
+template <bool RNN, bool SEL, bool GEN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AGENT_WAVES))) rnn_agent_fwd_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
@@ -408,14 +450,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AG
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
     float *__restrict__ Q, SelectArgs sel) {
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
-    agent_rows<RNN, SEL>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel);
+    agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel);
 }
 
 // Persistent variant: one 512-thread workgroup per CU copies the recurrent and output
 // weights (packed fragments) into LDS once, then its 8 waves walk 256-row tiles; the
 // gate and fc2 A operands become conflict-free ds_read_b128 instead of L2 round trips.
 constexpr int kLdsWaves = 8;
-template <bool RNN, bool SEL>
+template <bool RNN, bool SEL, bool GEN>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rnn_agent_lds_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
@@ -430,7 +472,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
-        agent_rows<RNN, SEL>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel);
+        agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel);
     }
 }
 
@@ -438,7 +480,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
     const int64_t w1 = (int64_t)((K + 15) / 16) * 4 * 64;
     const int64_t wr = use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64;
-    const int64_t w2 = 4 * (int64_t)(nout / 16) * 64;
+    const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
     return w1 + wr + w2;
 }
 
@@ -446,7 +488,7 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
                                  int use_rnn, float4 *packed, hipStream_t s) {
     float4 *p = packed;
     auto one = [&](const float *W, int C, int KK) {
-        const int64_t n = (int64_t)((KK + 15) / 16) * (C / 16) * 64;
+        const int64_t n = (int64_t)((KK + 15) / 16) * ((C + 15) / 16) * 64;
         hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, C, KK, p);
         p += n;
     };
@@ -482,32 +524,39 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
     const SelectArgs sa = sel ? *sel : SelectArgs{};
     // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU)
-    const int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)(nout / 16) * 64;
+    const int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)((nout + 15) / 16) * 64;
     const size_t lds = (size_t)nrf4 * sizeof(float4);
+    const bool gen = ((K | xs) & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 || nout > 256;
     if (use_lds_weights() && lds <= 160 * 1024) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
-#define LL_(RNN, SEL)                                                                                              \
-    hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, Hin, \
-                       hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa)
+#define LL_(RNN, SEL, GEN)                                                                                   \
+    hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL, GEN>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, \
+                       Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa)
+#define LG_(RNN, SEL) \
+    if (gen) LL_(RNN, SEL, true); else LL_(RNN, SEL, false)
         if (use_rnn) {
-            if (sel) LL_(true, true); else LL_(true, false);
+            if (sel) { LG_(true, true); } else { LG_(true, false); }
         } else {
-            if (sel) LL_(false, true); else LL_(false, false);
+            if (sel) { LG_(false, true); } else { LG_(false, false); }
         }
+#undef LG_
 #undef LL_
         return hipGetLastError();
     }
-#define L_(RNN, SEL)                                                                                          \
-    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, SEL>), dim3(blocks), dim3(256), 0, s, X, xs, R, K, Hin, hs, \
+#define L_(RNN, SEL, GEN)                                                                                    \
+    hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, SEL, GEN>), dim3(blocks), dim3(256), 0, s, X, xs, R, K, Hin, hs, \
                        W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa)
+#define LG_(RNN, SEL) \
+    if (gen) L_(RNN, SEL, true); else L_(RNN, SEL, false)
     if (use_rnn) {
-        if (sel) L_(true, true); else L_(true, false);
+        if (sel) { LG_(true, true); } else { LG_(true, false); }
     } else {
-        if (sel) L_(false, true); else L_(false, false);
+        if (sel) { LG_(false, true); } else { LG_(false, false); }
     }
+#undef LG_
 #undef L_
     return hipGetLastError();
 }

@@ -37,19 +37,18 @@ class RNNAgent(nn.Module):
 class RNNFusedAgent(RNNAgent):
     """RNNAgent with the same parameters / state_dict, whose inference forward (no autograd:
     the rollout's action selection) is one fused HIP kernel (asg_rnn_agent_forward: f32
-    MFMA, fc1 + GRUCell + fc2 with every intermediate in registers; hidden 64, n_out a
-    multiple of 16 up to 256).  With autograd enabled
+    MFMA, fc1 + GRUCell + fc2 with every intermediate in registers; hidden 64, any input
+    size, n_out = m up to 512 -- the real envs' m = 450 included).  With autograd enabled
     (learner training) it is the plain PyTorch module, so gradients are unchanged."""
 
     def __init__(self, input_shape, args):
         super().__init__(input_shape, args)
-        if args.hidden_dim != 64 or args.m % 16 != 0 or args.m > 256 or input_shape % 4 != 0:
-            raise ValueError("rnn_fused needs hidden_dim == 64, m a multiple of 16 up to 256 and an input size "
-                             "divisible by 4; use agent 'rnn'")
+        if args.hidden_dim != 64 or not 1 <= args.m <= 512 or input_shape < 1:
+            raise ValueError("rnn_fused needs hidden_dim == 64 and 1 <= m <= 512; use agent 'rnn'")
 
     def _prep(self, inputs, hidden_state):
         x = inputs
-        if x.dtype != torch.float32 or x.stride(-1) != 1 or x.stride(0) % 4 != 0 or x.data_ptr() % 16 != 0:
+        if x.dtype != torch.float32 or x.stride(-1) != 1 or x.stride(0) < x.shape[1]:
             x = x.float().contiguous()
         H = self.args.hidden_dim
         h = hidden_state

@@ -21,6 +21,7 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   runner_dumps.npz    EpisodeRunner / ParallelRunner EpisodeBatch dumps (layout + quirks)
   real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
   real_variants.npz   RealPowerConstellationEnv / InterferenceConstellationEnv reset/step
+  real_runner_dumps.npz  EpisodeRunner + BasicMAC EpisodeBatch dumps over RealConstellationEnv
 """
 import os
 import sys
@@ -492,11 +493,63 @@ def gen_runner_dumps():
     np.savez_compressed(os.path.join(OUT, "runner_dumps.npz"), **out)
 
 
+def gen_real_runner_dumps():
+    """EpisodeRunner + BasicMAC over RealConstellationEnv (constant benefits injected
+    through env_args: sat_prox_mat + graphs), greedy epsilon-greedy and SAP selectors.
+    Strictly positive tables, so the env's argsorts are tie-free."""
+    import torch as th
+    th.set_num_threads(1)
+    from runners.episode_runner import EpisodeRunner
+    from controllers import REGISTRY as mac_REGISTRY
+
+    out = {}
+    runs = [  # (tag, n, m, T, N, M, L, lambda, selector, use_rnn, prios)
+        ("real_eg_16", 12, 16, 6, 3, 4, 3, 0.5, "epsilon_greedy", True, False),
+        ("real_sap_16", 10, 16, 5, 2, 4, 2, 0.5, "sap", True, True),
+        ("real_eg_32", 20, 32, 5, 4, 6, 3, 0.3, "epsilon_greedy", False, True),
+    ]
+    for ri, (tag, n, m, T, N, M, L, lam, sel, use_rnn, use_prios) in enumerate(runs):
+        seed = 40 + ri
+        rng = np.random.RandomState(seed)
+        table = rng.uniform(0.01, 1.0, size=(n, m, T))
+        prios = rng.uniform(0.5, 2.0, size=m) if use_prios else None
+        np.random.seed(seed)
+        th.manual_seed(seed)
+        env_args = dict(num_planes=1, num_sats_per_plane=n, m=m, T=T, N=N, M=M, L=L, lambda_=lam,
+                        sat_prox_mat=table.copy(), graphs=[None] * T,
+                        task_prios=None if prios is None else prios.copy())
+        args = _args(env="real_constellation_env", env_args=env_args, action_selector=sel, use_rnn=use_rnn)
+        runner = EpisodeRunner(args, _Logger())
+        env = runner.get_env()
+        args.n, args.m, args.T = env.n, env.m, env.T
+        mac = mac_REGISTRY["basic_mac"](env.scheme, {"agents": n}, args)
+        g = th.Generator().manual_seed(2000 + ri)
+        with th.no_grad():
+            for p in mac.agent.parameters():
+                p.copy_(th.randn(p.shape, generator=g) * 0.3)
+        mac.update_action_selector_agent()
+        runner.setup(scheme=env.scheme, groups={"agents": n}, preprocess=env.preprocess, mac=mac)
+        batch = runner.run(test_mode=False)
+        for k, v in batch.data.transition_data.items():
+            out[f"{tag}__{k}"] = v.numpy()
+        for k, v in mac.agent.state_dict().items():
+            out[f"{tag}__w__{k}"] = v.numpy()
+        out[f"{tag}__returns"] = np.asarray(runner.train_returns, dtype=np.float64)
+        out[f"{tag}__t_env"] = np.array(runner.t_env)
+        out[f"{tag}__cfg"] = np.array([n, m, T, N, M, L, int(use_rnn)])
+        out[f"{tag}__lambda"] = np.array(lam)
+        out[f"{tag}__table"] = table
+        out[f"{tag}__prios"] = prios if prios is not None else np.ones(m)
+        out[f"{tag}__names"] = np.array([sel])
+    np.savez_compressed(os.path.join(OUT, "real_runner_dumps.npz"), **out)
+
+
 if __name__ == "__main__":
     _install_stubs()
     if sys.argv[1:] == ["real_env"]:  # regenerate only the RealConstellationEnv fixtures
         gen_real_env()
         gen_real_variants()
+        gen_real_runner_dumps()
         sys.exit(0)
     gen_real_env()
     gen_real_variants()
@@ -505,6 +558,7 @@ if __name__ == "__main__":
     gen_mock_step()
     gen_lsa()
     gen_runner_dumps()
+    gen_real_runner_dumps()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -18,7 +18,10 @@ DEV = torch.device("cuda", 0)
 @pytest.mark.parametrize("R,K,m,use_rnn,hidden", [
     (64 * 256, 256, 64, True, "zero"), (4096 + 37, 256, 64, True, "dense"), (1000, 68, 16, True, "dense"),
     (513, 256, 48, False, "zero"), (2048, 128, 32, False, "dense"), (31, 20, 64, True, "dense"),
-    (2000 + 5, 1024, 256, True, "dense"), (777, 512, 128, False, "dense"), (96, 1024, 256, True, "zero")])
+    (2000 + 5, 1024, 256, True, "dense"), (777, 512, 128, False, "dense"), (96, 1024, 256, True, "zero"),
+    # any input size / n_out: the real envs' obs sizes (70, 490) and m (20, 450), n_out > 256
+    (1000, 70, 16, True, "dense"), (517, 490, 450, True, "dense"), (300, 37, 20, False, "dense"),
+    (129, 132, 500, True, "zero"), (65, 3, 1, True, "dense"), (200, 130, 512, False, "dense")])
 def test_fused_agent_matches_pytorch(R, K, m, use_rnn, hidden):
     torch.manual_seed(R + K)
     args = SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m)
@@ -64,7 +67,9 @@ def test_fused_agent_reads_time_major_obs_slab():
 
 @pytest.mark.parametrize("eps,B,n,m,K,use_rnn", [
     (0.0, 300, 64, 64, 256, True), (0.3, 300, 64, 64, 256, True), (0.5, 37, 5, 48, 192, False),
-    (0.4, 50, 8, 256, 1024, True), (1.0, 21, 3, 16, 64, True), (0.3, 40, 7, 144, 576, True)])
+    (0.4, 50, 8, 256, 1024, True), (1.0, 21, 3, 16, 64, True), (0.3, 40, 7, 144, 576, True),
+    (0.3, 20, 12, 450, 490, True), (0.5, 30, 9, 20, 70, True), (0.0, 16, 20, 500, 132, False),
+    (1.0, 25, 6, 300, 33, True), (0.2, 9, 11, 512, 64, True)])
 def test_fused_select_equals_forward_then_selector(eps, B, n, m, K, use_rnn):
     """asg_rnn_agent_select == asg_rnn_agent_forward followed by asg_epsilon_greedy with
     the same Philox (seed, counter): same actions, same hidden state (ragged row counts,

@@ -214,3 +214,44 @@ def test_real_variants_match_oracle(oracle, kind, n, m, T, L, N, M):
     # a second episode draws new assignments
     env.reset(b, 0)
     assert not np.array_equal(b["prev_assigns"][:, 0].cpu().numpy(), prev0)
+
+
+REAL_RUNNER_TAGS = ["real_eg_16", "real_sap_16", "real_eg_32"]
+
+
+@pytest.mark.parametrize("agent", ["rnn", "rnn_fused"])
+@pytest.mark.parametrize("tag", REAL_RUNNER_TAGS)
+def test_runner_matches_reference_real_dump(golden, tag, agent):
+    """The "episode" runner + BasicMAC over the batched RealConstellationEnv against the
+    reference EpisodeRunner's EpisodeBatch (tests/golden/real_runner_dumps.npz): same
+    weights, greedy epsilon-greedy / SAP actions, every scheme field and the return."""
+    from types import SimpleNamespace
+    from marl_sap_amd.controllers import REGISTRY as mac_REGISTRY
+    from marl_sap_amd.runners import REGISTRY as r_REGISTRY
+    g = golden("real_runner_dumps")
+    n, m, T, N, M, L, use_rnn = [int(x) for x in g[f"{tag}__cfg"]]
+    sel = str(g[f"{tag}__names"][0])
+    args = SimpleNamespace(
+        batch_size_run=1, env="real_constellation_env",
+        env_args=dict(num_planes=1, num_sats_per_plane=n, m=m, T=T, N=N, M=M, L=L, lambda_=float(g[f"{tag}__lambda"]),
+                      sat_prox_mat=g[f"{tag}__table"], graphs=[None] * T, task_prios=g[f"{tag}__prios"], seed=0),
+        runner_protocol="episode", test_nepisode=1, runner_log_interval=10 ** 9, n=n, m=m, T=T, hidden_dim=64,
+        use_rnn=bool(use_rnn), obs_last_action=False, obs_agent_id=False, agent_output_type="q",
+        action_selector=sel, agent=agent, epsilon_start=0.0, epsilon_finish=0.0, epsilon_anneal_time=1000,
+        evaluation_epsilon=0.0, mac="basic_mac")
+    runner = r_REGISTRY["episode"](args, None)
+    env = runner.get_env()
+    mac = mac_REGISTRY["basic_mac"](env.scheme, {"agents": n}, args)
+    mac.agent.load_state_dict({k[len(tag) + 5:]: torch.as_tensor(g[k]) for k in g.files
+                               if k.startswith(f"{tag}__w__")})
+    mac.to(DEV)
+    runner.setup(env.scheme, {"agents": n}, env.preprocess, mac)
+    batch = runner.run(test_mode=False)
+    td = {k: v.cpu().numpy() for k, v in batch.data.transition_data.items()}
+    for k in ["obs", "beta", "rewards", "actions", "actions_onehot", "avail_actions", "terminated", "filled",
+              "prev_assigns"]:
+        ref = g[f"{tag}__{k}"]
+        assert td[k].dtype == ref.dtype, k
+        np.testing.assert_array_equal(td[k], ref, err_msg=f"{tag}:{k}")
+    np.testing.assert_allclose(np.array(runner.train_returns), g[f"{tag}__returns"], rtol=1e-5, atol=1e-6)
+    assert runner.t_env == int(g[f"{tag}__t_env"])

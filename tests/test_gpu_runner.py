@@ -46,8 +46,6 @@ def test_runner_matches_reference_dump(golden, tag, agent):
     g = golden("runner_dumps")
     n, m, T, B, seed, use_rnn = [int(x) for x in g[f"{tag}__cfg"]]
     rname, sel, macname = [str(x) for x in g[f"{tag}__names"]]
-    if agent == "rnn_fused" and m % 16:
-        pytest.skip("fused agent needs m % 16 == 0")
     args = _args(n, m, T, B, seed, use_rnn, rname, sel, macname)
     args.agent = agent
     runner = r_REGISTRY[rname](args, _Logger())

@@ -1,0 +1,43 @@
+"""Time the fused agent+select kernel at the bench shape with whichever library
+ASG_LIB_PATH names (A/B of kernel variants: run alternately per library, one process each).
+Prints one line: lib, median ms over `rounds` rounds of `iters` launches."""
+import os
+import sys
+from types import SimpleNamespace
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector  # noqa: E402
+from marl_sap_amd.modules.agents import RNNFusedAgent  # noqa: E402
+
+
+def main(E=16384, n=64, m=64, K=256, rounds=7, iters=30):
+    dev = torch.device("cuda", 0)
+    args = SimpleNamespace(hidden_dim=64, use_rnn=True, m=m, epsilon_start=0.05, epsilon_finish=0.05,
+                           epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=0)
+    fused = RNNFusedAgent(K, args).to(dev)
+    x = torch.randn((E * n, K), device=dev)
+    h = torch.randn((E * n, 64), device=dev)
+    avail = torch.ones((E, n, m), dtype=torch.bool, device=dev)
+    out = torch.empty((E, n), dtype=torch.int64, device=dev)
+    sel = EpsilonGreedyActionSelector(args)
+    res = []
+    with torch.no_grad():
+        for r in range(rounds + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(iters):
+                e, s, c, st = sel.fused_params(0, False, dev)
+                fused.forward_select(x, h, avail, n, e, s, c, out, st)
+            b.record()
+            torch.cuda.synchronize()
+            if r:
+                res.append(a.elapsed_time(b) / iters)
+    res.sort()
+    print(f"{os.environ.get('ASG_LIB_PATH', 'default')} K={K} m={m} median {res[len(res) // 2]:.4f} ms "
+          f"min {res[0]:.4f}", flush=True)
+
+
+if __name__ == "__main__":
+    main(*[int(a) for a in sys.argv[1:]])
