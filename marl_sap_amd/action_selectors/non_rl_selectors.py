@@ -8,7 +8,7 @@ import ctypes
 import torch
 
 from .. import _lib
-from .lsa import DeferredStatus
+from .lsa import DeferredStatus, raise_on_status
 
 REGISTRY = {}
 
@@ -36,21 +36,34 @@ class HAASelector:
         prev = batch["prev_assigns"][:, 0]
         if beta.dim() == 4:  # L-deep beta of the real env: use the current step only
             beta = beta[..., 0]
-        B, n, m = beta.shape
-        if beta.dtype != torch.float32:
-            beta = beta.float()
         lam, tt = self._env_params()
-        tt_dev = None if tt is None else tt.to(beta.device).contiguous()
-        out = torch.empty((B, n), dtype=torch.float32, device=beta.device)
-        status = torch.empty((B,), dtype=torch.int32, device=beta.device)
-        with torch.cuda.device(beta.device):
-            _lib.check(_lib.lib().asg_haa_select(
-                ctypes.c_void_p(beta.data_ptr()), _lib.i64arr(beta.stride()), ctypes.c_void_p(prev.data_ptr()),
-                _lib.i64arr(prev.stride()), B, n, m,
-                ctypes.c_void_p(tt_dev.data_ptr()) if tt_dev is not None else None, lam,
-                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(beta.device)))
+        out, status = haa_select_batched(beta, prev, lam, tt, return_status=True)
         self.status.add(status)
         return out
+
+
+def haa_select_batched(beta, prev, lambda_, T_trans=None, return_status=False):
+    """float32 [B, n] task ids = LSA(beta_hat(beta[b], prev[b]), maximize)[1] for every env
+    (non_rl_selectors.py:36-47), one asg_haa_select launch.  beta: [B, n, m] CUDA tensor,
+    prev: [B, n] int64, T_trans: None (the default 1 - I) or [m, m]."""
+    B, n, m = beta.shape
+    if beta.dtype != torch.float32:
+        beta = beta.float()
+    if prev.dtype != torch.int64:
+        prev = prev.long()
+    tt_dev = None if T_trans is None else torch.as_tensor(T_trans, dtype=torch.float64).to(beta.device).contiguous()
+    out = torch.empty((B, n), dtype=torch.float32, device=beta.device)
+    status = torch.empty((B,), dtype=torch.int32, device=beta.device)
+    with torch.cuda.device(beta.device):
+        _lib.check(_lib.lib().asg_haa_select(
+            ctypes.c_void_p(beta.data_ptr()), _lib.i64arr(beta.stride()), ctypes.c_void_p(prev.data_ptr()),
+            _lib.i64arr(prev.stride()), B, n, m,
+            ctypes.c_void_p(tt_dev.data_ptr()) if tt_dev is not None else None, float(lambda_),
+            ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(beta.device)))
+    if return_status:
+        return out, status
+    raise_on_status(status)
+    return out
 
 
 REGISTRY["haa_selector"] = HAASelector

@@ -174,21 +174,31 @@ __device__ __forceinline__ int wave_or_i32(int v) {
 
 // uniform read of a lane-distributed register array: element idx lives in lane idx % 64,
 // slot idx / 64 (idx wave-uniform)
+// (one v_readlane per slot, then scalar selects: the compiler must not turn the slot pick
+// into a dynamically indexed private array, which would live in scratch)
 template <int N, class T>
 __device__ __forceinline__ T lane_get(const T (&x)[N], int idx) {
     static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit values");
     const int slot = idx >> 6, src = idx & 63;
-    T sel = x[0];
-#pragma unroll
-    for (int c = 1; c < N; ++c)
-        if (c == slot) sel = x[c];
     if constexpr (sizeof(T) == 4) {
-        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sel), src));
+        int sel = __builtin_amdgcn_readlane(__builtin_bit_cast(int, x[0]), src);
+#pragma unroll
+        for (int c = 1; c < N; ++c) {
+            const int t = __builtin_amdgcn_readlane(__builtin_bit_cast(int, x[c]), src);
+            sel = (c == slot) ? t : sel;
+        }
+        return __builtin_bit_cast(T, sel);
     } else {
-        const uint64_t u = __builtin_bit_cast(uint64_t, sel);
-        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, src);
-        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
-        return __builtin_bit_cast(T, (uint64_t)lo | ((uint64_t)hi << 32));
+        uint64_t sel = 0;
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const uint64_t u = __builtin_bit_cast(uint64_t, x[c]);
+            const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, src);
+            const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), src);
+            const uint64_t t = (uint64_t)lo | ((uint64_t)hi << 32);
+            sel = (c == 0 || c == slot) ? t : sel;
+        }
+        return __builtin_bit_cast(T, sel);
     }
 }
 template <int N, class T>
@@ -196,8 +206,7 @@ __device__ __forceinline__ void lane_set(T (&x)[N], int idx, T val) {
     const int slot = idx >> 6, dst = idx & 63;
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int c = 0; c < N; ++c)
-        if (c == slot && lane == dst) x[c] = val;
+    for (int c = 0; c < N; ++c) x[c] = (c == slot && lane == dst) ? val : x[c];
 }
 
 // wave-scope barrier with LDS/global ordering (a workgroup may hold other waves that do

@@ -4,6 +4,8 @@
 // (L2-resident for the row sweeps).
 // Reference call sites: sap_selectors.py:32,90 (SAP selectors on Q-values),
 // non_rl_selectors.py:36-47 (HAA: beta_hat + LSA), mock_constellation_env.py:228-274.
+#include <type_traits>
+
 #include "asg_device.h"
 #include "asg_internal.h"
 #include "lsa_wave.h"
@@ -99,13 +101,45 @@ __global__ void __launch_bounds__(64) lsa_batched_kernel(const IT *C, int64_t s0
 
 static size_t lsa_scratch_bytes(int nr0) { return sizeof(int) * nr0 + 64; }
 
+// float32 problems up to 64 x 64 (working orientation): the working matrix lives in the
+// wave's registers (RegCostF32), so residency is set by registers alone (no LDS)
+__global__ void __launch_bounds__(64) lsa_reg_kernel(const float *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
+                                                     int nc0, int maximize, int64_t *row_out, int64_t *col_out,
+                                                     int32_t *status_out) {
+    __shared__ int mark[64];
+    const int64_t b = blockIdx.x;
+    const bool tr = nc0 < nr0;
+    const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;
+    const int k = nr;
+    int64_t *ro = row_out ? row_out + b * k : nullptr;
+    int64_t *co = col_out ? col_out + b * k : nullptr;
+    RegCostF32 rc;
+    int status = lsa_stage_regs<float>(C + b * s0, s1, s2, nr0, nc0, maximize != 0, rc);
+    if (status == ASG_OK) {
+        int c4r[1];
+        status = lsa_solve_wave<1>(rc, nr, nc, c4r);
+        if (status == ASG_OK) lsa_emit_wave(c4r, nr0, nc0, mark, ro, co, nullptr);
+    }
+    const int lane = threadIdx.x;
+    if (status != ASG_OK) {
+        for (int r = lane; r < k; r += kWave) {
+            if (ro) ro[r] = -1;
+            if (co) co[r] = -1;
+        }
+    }
+    if (lane == 0 && status_out) status_out[b] = status;
+}
+
 template <typename IT, typename CT>
 static hipError_t launch_lsa_t(const IT *C, const int64_t st[3], int64_t B, int nr0, int nc0, int maximize,
                                int64_t *row_out, int64_t *col_out, int32_t *status_out, hipStream_t s) {
     const int nr = nc0 < nr0 ? nc0 : nr0, nc = nc0 < nr0 ? nr0 : nc0;
     const size_t cost_bytes = ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
     const size_t scratch = lsa_scratch_bytes(nr0);
-    if (cost_bytes <= kLdsCostBudget) {
+    if (std::is_same<IT, float>::value && nc <= 64) {
+        hipLaunchKernelGGL(lsa_reg_kernel, dim3(B), dim3(64), 0, s, reinterpret_cast<const float *>(C), st[0], st[1],
+                           st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+    } else if (cost_bytes <= kLdsCostBudget) {
 #define L_(CPL)                                                                                                   \
     hipLaunchKernelGGL((lsa_batched_kernel<CPL, IT, CT, true>), dim3(B), dim3(64), cost_bytes + scratch, s, C, \
                        st[0], st[1], st[2], nr0, nc0, maximize, row_out, col_out, status_out)
@@ -221,12 +255,61 @@ __global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64
     if (lane == 0 && status_out) status_out[b] = status;
 }
 
+// m <= 64: the beta column of the lane's task and prev_assigns of the lane's agent stay
+// in registers; -beta_hat(i, j) is formed per relaxed entry
+struct HaaRegCost {
+    RegCostF32 beta;  // beta[i][lane], not sign-flipped
+    int prev;         // prev_assigns[lane]
+    const double *T_trans;
+    double lambda_;
+    int m;
+    __device__ double operator()(int i, int j) const {
+        const double x = (double)beta.get(i);
+        const int p = __builtin_amdgcn_readlane(prev, i);
+        const double tt = T_trans ? T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+        return -(x - lambda_ * (tt * (x > 1e-12 ? 1.0 : 0.0)));
+    }
+};
+
+__global__ void __launch_bounds__(64) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
+                                                     const int64_t *prev, int64_t p0, int64_t p1, int n, int m,
+                                                     const double *T_trans, double lambda_, float *col_out,
+                                                     int32_t *status_out) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    HaaRegCost acc;
+    // beta_hat is not negated here (the accessor does it): stage with maximize = false,
+    // which also rejects NaN; +inf beta (-inf cost) is rejected below
+    int status = lsa_stage_regs<float>(beta + b * b0, b1, b2, n, m, false, acc.beta);
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+        bad |= (acc.beta.lo[i] == __builtin_inff()) | (acc.beta.hi[i] == __builtin_inff());
+    if (wave_or_i32(bad)) status = ASG_E_LSA_INVALID;
+    acc.prev = lane < n ? (int)prev[b * p0 + lane * p1] : 0;
+    acc.T_trans = T_trans;
+    acc.lambda_ = lambda_;
+    acc.m = m;
+    float *co = col_out + b * n;
+    if (status == ASG_OK) {
+        int c4r[1];
+        status = lsa_solve_wave<1>(acc, n, m, c4r);
+        if (status == ASG_OK) lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co);
+    }
+    if (status != ASG_OK)
+        for (int i = lane; i < n; i += kWave) co[i] = -1.0f;
+    if (lane == 0 && status_out) status_out[b] = status;
+}
+
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s) {
     const size_t cost = ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
     const size_t rest = ((sizeof(int) * n + 15) / 16) * 16 + 64;
-    if (cost <= kLdsCostBudget) {
+    if (m <= 64) {
+        hipLaunchKernelGGL(haa_reg_kernel, dim3(B), dim3(64), 0, s, beta, bs[0], bs[1], bs[2], prev, ps[0], ps[1], n,
+                           m, T_trans, lambda_, col_out, status_out);
+    } else if (cost <= kLdsCostBudget) {
 #define L_(CPL)                                                                                                 \
     hipLaunchKernelGGL((haa_select_kernel<CPL, true>), dim3(B), dim3(64), cost + rest, s, beta, bs[0], bs[1], bs[2], \
                        prev, ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out)

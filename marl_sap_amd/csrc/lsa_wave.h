@@ -13,8 +13,9 @@
 // `remaining` positions are tracked per column (pos), including scipy's
 // swap-with-last removal, so ties resolve exactly as in the sequential code.
 //
-// The cost matrix lives in LDS (or global memory for large problems) already
-// transposed (nr <= nc) and sign-flipped for maximize, as scipy does before solving.
+// The working matrix (already transposed so nr <= nc, and sign-flipped for maximize, as
+// scipy does before solving) lives in registers for float32 problems up to 64 x 64
+// (RegCostF32), else in LDS, else (large problems) is read in place from global memory.
 #pragma once
 #include "asg_device.h"
 
@@ -28,13 +29,77 @@ struct DenseCost {
     __device__ double operator()(int i, int j) const { return (double)c[(size_t)i * nc + j]; }
 };
 
+// Register-resident working matrix of at most 64 x 64 float32 entries: lane l holds
+// working column l (rows 0..31 in `lo`, 32..63 in `hi`).  A row index is wave-uniform,
+// so the read is two s_set_gpr_idx moves and a select -- no LDS, no memory latency, and
+// no LDS budget capping the problems resident per CU.
+typedef float f32x32 __attribute__((ext_vector_type(32)));
+struct RegCostF32 {
+    f32x32 lo, hi;
+    __device__ __forceinline__ float get(int i) const {
+        const int ii = __builtin_amdgcn_readfirstlane(i);
+        const float x0 = lo[ii & 31], x1 = hi[ii & 31];
+        return ii < 32 ? x0 : x1;
+    }
+    __device__ __forceinline__ double operator()(int i, int) const { return (double)get(i); }
+};
+
+// Load the lane's working column (scipy orientation: transposed when nr0 > nc0, negated
+// for maximize) into registers.  Returns ASG_E_LSA_INVALID (wave uniform) when an entry
+// is NaN or -inf after the sign flip.
+template <typename IT>
+__device__ int lsa_stage_regs(const IT *C, int64_t rs, int64_t cs, int nr0, int nc0, bool maximize,
+                              RegCostF32 &rc) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool tr = nc0 < nr0;
+    const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;
+    const int64_t istride = tr ? cs : rs, jstride = tr ? rs : cs;
+    const IT *col = C + (int64_t)lane * jstride;
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        float a = 0.0f, b = 0.0f;
+        if (lane < nc && i < nr) a = (float)col[i * istride];
+        if (lane < nc && i + 32 < nr) b = (float)col[(i + 32) * istride];
+        if (maximize) {
+            a = -a;
+            b = -b;
+        }
+        bad |= (a != a) | (b != b) | (a == -__builtin_inff()) | (b == -__builtin_inff());
+        rc.lo[i] = a;
+        rc.hi[i] = b;
+    }
+    return wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
+}
+
+// Order-preserving int32 key of a float64 rounded to float32: x <= y implies
+// key(x) <= key(y) (rounding is monotone; -0 is folded onto +0 so equal doubles get equal
+// keys).  A column whose key is the unique wave minimum therefore holds the unique
+// float64 minimum; equal keys (float64 ties, or values closer than float32 resolves)
+// fall back to the exact float64 selection.
+__device__ __forceinline__ int f32_key(double x) {
+    int b = __float_as_int((float)x);
+    b = (b == (int)0x80000000) ? 0 : b;
+    return b < 0 ? (b ^ 0x7fffffff) : b;
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+    return wave_allreduce(v, [](int a, int b) { return a < b ? a : b; });
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return wave_allreduce(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+}
+
 // Solve on the working matrix acc(i, j), i < nr <= nc <= 64*CPL (scipy's orientation).
 // All per-row and per-column state lives in registers, distributed over the lanes
-// (column j / row r in lane j%64, slot j/64); only the cost matrix is in memory.  The
-// per-iteration reductions are VALU butterflies (DPP + permlane swaps) and the uniform
-// reads are v_readlane, so the serial augmenting-path loop has no LDS round trip except
-// the cost-row read.  Returns 0 or ASG_E_LSA_INFEASIBLE; col4row[c] holds the column
-// assigned to row lane + 64c.  All 64 lanes must call it with identical arguments.
+// (column j / row r in lane j%64, slot j/64); only the cost matrix may be in memory.
+// Each augmenting-path step is: relax the lane's columns in float64 (scipy's operation
+// order), one int32 min-reduction of the float32-rounded keys plus a ballot -- which
+// settles the step whenever a single column attains the minimum key -- and otherwise the
+// exact float64 minimum and scipy's tie rule by packed-key reduction.  Control flow is
+// wave-uniform throughout (row, column and position indices are scalars).
+// Returns 0 or ASG_E_LSA_INFEASIBLE; col4row[c] holds the column assigned to row
+// lane + 64c.  All 64 lanes must call it with identical arguments.
 template <int CPL, class Acc>
 __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL]) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -62,58 +127,105 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
         int nrem = nc;
         double minv = 0.0;
         int i = cur, sink = -1;
-        while (sink == -1) {
+        bool infeasible = false;
+        do {
+            i = __builtin_amdgcn_readfirstlane(i);
             const double ui = lane_get(u, i);
-            double lo = __builtin_inf();
+            int key[CPL];
+            int kl = 0x7fffffff;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const int j = lane + kWave * c;
-                if (pos[c] >= 0) {
-                    const double r = ((minv + acc(i, j)) - ui) - v[c];
-                    if (r < spc[c]) {
-                        spc[c] = r;
-                        path[c] = i;
-                    }
-                    lo = fmin(lo, spc[c]);
-                }
+                // branch-free over the lane's columns: scanned / absent ones are relaxed
+                // too but neither updated nor keyed
+                const bool rem = pos[c] >= 0;
+                const double cij = j < nc ? acc(i, j) : 0.0;  // never read past the matrix
+                const double r = ((minv + cij) - ui) - v[c];
+                const bool upd = rem && r < spc[c];
+                spc[c] = upd ? r : spc[c];
+                path[c] = upd ? i : path[c];
+                key[c] = rem ? f32_key(spc[c]) : 0x7fffffff;
+                kl = key[c] < kl ? key[c] : kl;
             }
-            const double lowest = wave_min_f64(lo);
-            if (lowest == __builtin_inf()) return ASG_E_LSA_INFEASIBLE;  // uniform branch
-            // candidates (remaining columns at the minimum): one ballot per slot.  With a
-            // single candidate (the common case for float data) it is the selection;
-            // ties fall back to the packed-key reduction below.
+            const int kmin = wave_min_i32(kl);
             int total = 0, jsel = -1, psel = -1;
+            double lowest = 0.0;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const uint64_t msk = __ballot(pos[c] >= 0 && spc[c] == lowest);
+                const uint64_t msk = __ballot(key[c] == kmin);
                 const int cnt = __popcll(msk);
                 if (cnt == 1 && total == 0) {
                     const int src = __builtin_ctzll(msk);
                     jsel = src + kWave * c;
                     psel = __builtin_amdgcn_readlane(pos[c], src);
+                    const uint64_t sb = __builtin_bit_cast(uint64_t, spc[c]);
+                    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, src);
+                    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src);
+                    lowest = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
                 }
                 total += cnt;
             }
             if (total != 1) {
-                // packed selection key, reduced with max:
-                //   bit 63      : candidate is unassigned
-                //   bits 62..32 : unassigned ? pos : (2^30 - pos)   (largest pos vs smallest pos)
-                //   bits 31..0  : column index
-                uint64_t key = 0;
+                // Several columns share the minimum key.  Usually they hold exactly equal
+                // float64 values (scipy's tie case, frequent with correlated Q-values):
+                // check that against the first candidate's value, then apply scipy's tie
+                // rule with one 32-bit max-reduction.  Otherwise (distinct float64 values
+                // that round to one float32) take the exact float64 minimum first.
+                int src0 = -1, c0 = 0;
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
-                    const int j = lane + kWave * c;
-                    if (pos[c] >= 0 && spc[c] == lowest) {
-                        const uint64_t k = (r4c[c] == -1)
-                                               ? ((1ull << 63) | ((uint64_t)pos[c] << 32) | (uint32_t)j)
-                                               : (((uint64_t)((1u << 30) - (uint32_t)pos[c]) << 32) | (uint32_t)j);
-                        key = k > key ? k : key;
+                    const uint64_t msk = __ballot(key[c] == kmin);
+                    if (src0 < 0 && msk != 0) {
+                        src0 = __builtin_ctzll(msk);
+                        c0 = c;
                     }
                 }
-                key = wave_max_u64(key);
-                const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
-                jsel = __builtin_amdgcn_readfirstlane((uint32_t)key);
-                psel = (khi >> 31) ? (int)(khi & 0x7fffffffu) : (int)((1u << 30) - khi);
+                double val0 = 0.0;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    if (c == c0) {
+                        const uint64_t sb = __builtin_bit_cast(uint64_t, spc[c]);
+                        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);
+                        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src0);
+                        val0 = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+                    }
+                }
+                bool all_equal = true;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) all_equal &= __ballot(key[c] == kmin && spc[c] != val0) == 0;
+                if (all_equal) {
+                    lowest = val0;
+                } else {
+                    // exact float64 minimum over the remaining columns
+                    double lo = __builtin_inf();
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c)
+                        if (pos[c] >= 0) lo = spc[c] < lo ? spc[c] : lo;
+                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));  // uniform: pin to SGPRs
+                    const uint32_t l0 = __builtin_amdgcn_readfirstlane((uint32_t)lb);
+                    const uint32_t l1 = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
+                    lowest = __builtin_bit_cast(double, (uint64_t)l0 | ((uint64_t)l1 << 32));
+                }
+                // scipy's tie rule as a max-reduced 32-bit key over the candidates
+                // (remaining columns at `lowest`):
+                //   unassigned: 2^31 | pos        (the LARGEST position wins)
+                //   assigned:   2^30 - pos        (else the SMALLEST position)
+                uint32_t tk = 0;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const bool cand = pos[c] >= 0 && spc[c] == lowest;
+                    const uint32_t k = (r4c[c] == -1) ? (0x80000000u | (uint32_t)pos[c])
+                                                      : ((1u << 30) - (uint32_t)pos[c]);
+                    tk = (cand && k > tk) ? k : tk;
+                }
+                tk = __builtin_amdgcn_readfirstlane(wave_max_u32(tk));
+                psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
+                // positions are distinct over the remaining columns: the owner is unique
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint64_t msk = __ballot(pos[c] == psel);
+                    if (msk != 0) jsel = __builtin_ctzll(msk) + kWave * c;
+                }
             }
             const int last = nrem - 1;
             // remaining[index] = remaining[--num_remaining]
@@ -128,8 +240,11 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
             --nrem;
             minv = lowest;
             const int owner = lane_get(r4c, jsel);
-            if (owner == -1) sink = jsel; else i = owner;
-        }
+            infeasible = lowest == __builtin_inf();  // scipy: minVal == INFINITY
+            if (owner == -1) sink = jsel;
+            i = owner;
+        } while (sink == -1 && !infeasible);
+        if (infeasible) return ASG_E_LSA_INFEASIBLE;
         // dual update (scipy: u[cur] += minv; u[r] += minv - spc[col4row[r]] for the
         // other visited rows; v[j] -= minv - spc[j] for the scanned columns).  A row
         // r != cur was visited iff its matched column col4row[r] was scanned.

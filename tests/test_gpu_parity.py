@@ -50,11 +50,23 @@ def test_lsa_golden(golden):
     ((512, 64, 64), "normal", np.float32), ((256, 64, 64), "int3", np.float32),
     ((128, 16, 16), "int2", np.float64), ((64, 20, 37), "round1", np.float64),
     ((64, 37, 20), "round1", np.float64), ((32, 100, 130), "normal", np.float64),
-    ((8, 256, 256), "int3", np.float32), ((4, 300, 300), "normal", np.float64)])
+    ((8, 256, 256), "int3", np.float32), ((4, 300, 300), "normal", np.float64),
+    # float32 <= 64 x 64 runs register-resident (both orientations, degenerate shapes)
+    ((256, 64, 48), "normal", np.float32), ((256, 48, 64), "normal", np.float32),
+    ((64, 1, 64), "normal", np.float32), ((64, 64, 1), "normal", np.float32),
+    ((256, 33, 40), "int2", np.float32), ((256, 64, 64), "corr", np.float32),
+    # float32 keys collide while float64 values differ (the exact selection path)
+    ((256, 64, 64), "near64", np.float64), ((256, 40, 64), "near32", np.float32)])
 def test_lsa_random_batches_vs_oracle(shape, kind, dtype):
-    rng = np.random.RandomState(hash((shape, kind)) % 2**31)
+    rng = np.random.RandomState(sum(shape) * 31 + len(kind))
     if kind == "normal":
         C = rng.normal(size=shape)
+    elif kind == "corr":  # SAP-like Q-values: shared task profile + small per-agent term
+        C = rng.normal(size=(shape[0], 1, shape[2])) + 0.05 * rng.normal(size=shape)
+    elif kind == "near64":
+        C = 1.0 + rng.randint(0, 1000, size=shape) * 2.0 ** -40
+    elif kind == "near32":
+        C = 1.0 + rng.randint(0, 8, size=shape) * 2.0 ** -23
     elif kind == "int3":
         C = rng.randint(0, 3, size=shape).astype(np.float64)
     elif kind == "int2":
@@ -83,6 +95,23 @@ def test_lsa_strided_and_status():
     _, col, status = linear_sum_assignment_batched(bad, return_status=True)
     assert status.cpu().tolist() == [0, -4, 0]
     assert (col[1] == -1).all()
+
+
+def test_lsa_register_path_status():
+    """float32 <= 64 x 64 (register-resident working matrix): scipy's errors per matrix."""
+    C = torch.as_tensor(np.random.RandomState(3).normal(size=(5, 6, 6)), device=DEV, dtype=torch.float32)
+    C[1, 2, 3] = float("nan")                # invalid
+    C[2, 0, :] = float("inf")                # row 0 has no finite entry: infeasible
+    C[3, 4, 1] = -float("inf")               # invalid when minimizing
+    C[4, 5, 5] = float("inf")                # feasible: +inf is only avoided
+    _, col, status = linear_sum_assignment_batched(C, return_status=True)
+    assert status.cpu().tolist() == [0, -4, -5, -4, 0]
+    for b in (0, 4):
+        assert np.array_equal(col[b].cpu().numpy(), ora.lsa(C[b].cpu().numpy().astype(np.float64))[1])
+    _, _, st_max = linear_sum_assignment_batched(C[4:5], maximize=True, return_status=True)
+    assert st_max.cpu().tolist() == [-4]     # +inf becomes -inf under maximize
+    with pytest.raises(ValueError, match="infeasible"):
+        linear_sum_assignment_batched(C[2:3])
 
 
 # ------------------------------------------------------------------------------ beta_hat / HAA
