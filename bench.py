@@ -63,7 +63,8 @@ def agent_roofline(a, E, sel_ms):
     tfs = flops / (sel_ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
             "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "traffic": None,
-            "kernel": "asg::rnn_agent_lds_kernel" if a.agent == "rnn_fused" else "torch agent + selector",
+            "kernel": ("asg::rnn_agent_lds_kernel" if a.agent == "rnn_fused" else "torch agent + selector")
+            if a.selector == "eps" else f"{a.agent} forward + asg::sap_select_kernel (whole selection)",
             "kernel_ms": round(sel_ms, 4), "flops_per_launch": flops}
 
 

@@ -30,6 +30,8 @@
  *                              mock_constellation_env.py:122, action_selectors/sap_selectors.py:32,90,
  *                              action_selectors/non_rl_selectors.py:47
  *   asg_haa_select             HAASelector.select_action (action_selectors/non_rl_selectors.py:19-50)
+ *   asg_sap_select             SequentialAssignmentProblemSelector.select_action
+ *                              (action_selectors/sap_selectors.py:52-98): noise + LSA per env
  *   asg_epsilon_greedy         EpsilonGreedyActionSelector.select_action
  *                              (action_selectors/classic_selectors.py:28-54)
  *   asg_rnn_agent_forward      RNNAgent.forward (modules/agents/rnn_agent.py:23-31) as called by
@@ -182,6 +184,18 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
                    const int64_t prev_strides[2], int64_t B, int n, int m,
                    const double *T_trans_dev, double lambda_, float *col_out,
                    int32_t *status_out, void *hip_stream);
+
+/* SequentialAssignmentProblemSelector (sap_selectors.py:52-98) for n <= m <= 64, fused:
+ * per env b, std = mean(|Q[b]|) * epsilon * 2 (float32), Q' = Q[b] + N(0, std^2) noise
+ * (Philox keyed by (seed, env_index_base + b, counter), Box-Muller; exactly zero noise when
+ * epsilon == 0), col_out[b] = LSA(Q', maximize)[1] as float32 task ids (the selector's
+ * float picked_actions).  Q [B][n][m] f32, any strides.  status_out [B] int32 (0,
+ * ASG_E_LSA_INVALID for NaN / +inf entries, ASG_E_LSA_INFEASIBLE), may be NULL; failed envs
+ * get -1 rows.  ASG_E_INVALID_ARG when n > m or m > 64 (the Python selector then adds the
+ * noise with torch and calls asg_lsa_batched). */
+int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
+                   double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
+                   float *col_out, int32_t *status_out, void *hip_stream);
 
 /* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
  * per row, with probability epsilon a uniformly random available action, else the first

@@ -1,8 +1,11 @@
 """Sequential-assignment selectors (reference: action_selectors/sap_selectors.py:7-98).
 The per-env scipy loop becomes one batched HIP LSA over all envs (lsa.py)."""
+import ctypes
+
 import numpy as np
 import torch
 
+from .. import _lib
 from ..components.epsilon_schedules import DecayThenFlatSchedule
 from .lsa import DeferredStatus, linear_sum_assignment_batched
 
@@ -15,7 +18,11 @@ def _lsa_actions(q, status_sink):
 
 
 class SequentialAssignmentProblemSelector:
-    """REDA selector: Gaussian noise of std 2*eps*mean|Q| per env, then LSA(maximize)."""
+    """REDA selector: Gaussian noise of std 2*eps*mean|Q| per env, then LSA(maximize).
+
+    n <= m <= 64: one fused HIP kernel (asg_sap_select: noise drawn in registers from
+    Philox keyed by (seed, global env index, call counter), register-resident LSA).
+    Larger problems: the noise from torch, then asg_lsa_batched."""
 
     def __init__(self, args):
         self.args = args
@@ -23,12 +30,32 @@ class SequentialAssignmentProblemSelector:
                                               decay="linear")
         self.epsilon = self.schedule.eval(0)
         self.status = DeferredStatus()
+        self.seed = int(getattr(args, "seed", 0) or 0) * 0x9E3779B1 + torch.initial_seed()
+        self.calls = 0
+        self.envs = None  # set by the runner (reference: run.py sets action_selector.envs)
+
+    def _env_index_base(self):
+        return int(getattr(self.envs, "env_index_base", getattr(self.args, "env_index_base", 0)) or 0)
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None):
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:
             self.epsilon = self.args.evaluation_epsilon
         q = agent_inputs.detach()
+        B, n, m = q.shape
+        if n <= m <= 64 and q.is_cuda:
+            if q.dtype != torch.float32:
+                q = q.float()
+            out = torch.empty((B, n), dtype=torch.float32, device=q.device)
+            status = torch.empty((B,), dtype=torch.int32, device=q.device)
+            self.calls += 1
+            with torch.cuda.device(q.device):
+                _lib.check(_lib.lib().asg_sap_select(
+                    ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), B, n, m, float(self.epsilon),
+                    self.seed & 0xFFFFFFFFFFFFFFFF, self.calls, self._env_index_base(),
+                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(q.device)))
+            self.status.add(status)
+            return out
         if self.epsilon > 0:
             avg = q.abs().mean(dim=(1, 2), keepdim=True)
             q = q + torch.randn_like(q) * (avg * self.epsilon * 2)

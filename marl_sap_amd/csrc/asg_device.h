@@ -49,7 +49,8 @@ __device__ __forceinline__ double bump_value(double scale, double center, double
 }
 
 // purposes of Philox counters (counter.z); counter.w = episode
-enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u };
+enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u,
+                  kCtrSapNoise = 7u };
 
 // "a beats b" in torch.max order: NaN wins, then larger value, then smaller index.
 // Branch-free (bitwise on the predicates) so it lowers to compares + v_cndmask.

@@ -206,18 +206,23 @@ __global__ void __launch_bounds__(64) bids_assign_kernel(asg_batch_view bv, EnvS
     extern __shared__ double s_lsa[];
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m;
-    float *cost = reinterpret_cast<float *>(s_lsa);  // [n][m]
+    float *cost = reinterpret_cast<float *>(s_lsa);  // [n][m] (m > 64)
     const float *bids = fptr<float>(bv.actions, e, ts, 0, 0);
-    int status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, cost);
+    int c4r[CPL];
+    int status;
+    if constexpr (CPL == 1) {  // m <= 64: the working matrix stays in registers
+        RegCostF32 rc;
+        status = lsa_stage_regs<float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, rc);
+        if (status == ASG_OK) status = lsa_solve_wave<1>(rc, n, m, c4r);
+    } else {
+        status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, cost);
+        if (status == ASG_OK) status = lsa_solve_wave<CPL>(DenseCost<float>{cost, m}, n, m, c4r);
+    }
     if (status == ASG_OK) {
-        int c4r[CPL];
-        status = lsa_solve_wave<CPL>(DenseCost<float>{cost, m}, n, m, c4r);
-        if (status == ASG_OK) {
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int i = (int)threadIdx.x + kWave * c;
-                if (i < n) st.assign[e * n + i] = c4r[c];
-            }
+        for (int c = 0; c < CPL; ++c) {
+            const int i = (int)threadIdx.x + kWave * c;
+            if (i < n) st.assign[e * n + i] = c4r[c];
         }
     }
     if (status != ASG_OK) {

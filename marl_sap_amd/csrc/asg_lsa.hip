@@ -17,6 +17,7 @@ constexpr size_t kLdsCostBudget = 48 * 1024;
 // working matrix read in place: transposed when nr0 > nc0, negated for maximize
 template <typename IT>
 struct GlobalCost {
+    static constexpr bool kInMemory = true;
     const IT *C;
     int64_t rs, cs;
     bool tr, neg;
@@ -166,6 +167,85 @@ hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3]
 }
 
 // ------------------------------------------------------------------------------------
+// SequentialAssignmentProblemSelector (sap_selectors.py:52-98), n <= m <= 64, fused:
+// noise of std mean|Q| * eps * 2 added in registers while the column is staged, then the
+// register-resident LSA (maximize).  The reference runs, per env on the host: abs, mean,
+// ones * avg * eps * 2, torch.normal, +=, scipy.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
+                                                        int m, float epsilon, uint64_t seed, uint32_t counter,
+                                                        int64_t env_base, float *col_out, int32_t *status_out) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float *col = q + b * q0 + (int64_t)lane * q2;
+    f32x32 lo, hi;
+    float asum = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        float a = 0.0f, c = 0.0f;
+        if (lane < m && i < n) a = col[i * q1];
+        if (lane < m && i + 32 < n) c = col[(i + 32) * q1];
+        asum += __builtin_fabsf(a);
+        asum += __builtin_fabsf(c);
+        lo[i] = a;
+        hi[i] = c;
+    }
+    // th.mean(th.abs(Q)) (float32; summation order differs from torch's, the noise is
+    // random either way), stds = avg * eps * 2
+    const float avg = wave_allreduce(asum, [](float x, float y) { return x + y; }) / (float)(n * m);
+    const float stdv = avg * epsilon * 2.0f;
+    if (epsilon > 0.0f) {
+        const EnvKey key = env_key(seed, env_base + b);
+        constexpr float k2m24 = 5.9604644775390625e-08f;  // 2^-24
+        constexpr float k2pi = 6.283185307179586f;
+#pragma unroll
+        for (int i4 = 0; i4 < 16; ++i4) {  // rows 4*i4 .. 4*i4+3 of this column
+            const u32x4 r = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)i4, kCtrSapNoise, counter}, key.k0, key.k1);
+            const float u1a = (float)((r.x >> 8) + 1u) * k2m24, u2a = (float)(r.y >> 8) * k2m24;
+            const float u1b = (float)((r.z >> 8) + 1u) * k2m24, u2b = (float)(r.w >> 8) * k2m24;
+            const float ra = __builtin_sqrtf(-2.0f * __logf(u1a)), rb = __builtin_sqrtf(-2.0f * __logf(u1b));
+            const float z[4] = {ra * __cosf(k2pi * u2a), ra * __sinf(k2pi * u2a), rb * __cosf(k2pi * u2b),
+                                rb * __sinf(k2pi * u2b)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = 4 * i4 + k;  // torch.normal(0, std) = 0 + std * z, then Q += noise
+                if (i < 32) lo[i] = lo[i] + stdv * z[k];
+                else hi[i - 32] = hi[i - 32] + stdv * z[k];
+            }
+        }
+    }
+    RegCostF32 rc;
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        // scipy on the noisy float64 matrix: NaN or +inf (-inf once negated) is invalid
+        const bool va = lane < m && i < n, vb = lane < m && i + 32 < n;
+        bad |= va & ((lo[i] != lo[i]) | (lo[i] == __builtin_inff()));
+        bad |= vb & ((hi[i] != hi[i]) | (hi[i] == __builtin_inff()));
+        rc.lo[i] = va ? -lo[i] : 0.0f;
+        rc.hi[i] = vb ? -hi[i] : 0.0f;
+    }
+    int status = wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
+    float *co = col_out + b * n;
+    if (status == ASG_OK) {
+        int c4r[1];
+        status = lsa_solve_wave<1>(rc, n, m, c4r);
+        if (status == ASG_OK) lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co);
+    }
+    if (status != ASG_OK)
+        for (int i = lane; i < n; i += kWave) co[i] = -1.0f;
+    if (lane == 0 && status_out) status_out[b] = status;
+}
+
+hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
+                             uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(sap_select_kernel, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon, seed,
+                       counter, env_base, col_out, status_out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
 // beta_hat = beta - lambda * T_trans[prev_i, j] * (beta > 1e-12)   (mock :250-270)
 // ------------------------------------------------------------------------------------
 template <typename BT>
@@ -207,6 +287,7 @@ hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], con
 // a 64x64 problem needs 16 KiB of LDS instead of 32.
 // ------------------------------------------------------------------------------------
 struct HaaCost {
+    static constexpr bool kInMemory = true;
     const float *beta;  // [n][m] in LDS (rs = m, cs = 1) or in place in global memory
     int64_t rs, cs;
     const int *prev;    // LDS [n]
@@ -258,6 +339,7 @@ __global__ void __launch_bounds__(64) haa_select_kernel(const float *beta, int64
 // m <= 64: the beta column of the lane's task and prev_assigns of the lane's agent stay
 // in registers; -beta_hat(i, j) is formed per relaxed entry
 struct HaaRegCost {
+    static constexpr bool kInMemory = false;  // T_trans reads are guarded below
     RegCostF32 beta;  // beta[i][lane], not sign-flipped
     int prev;         // prev_assigns[lane]
     const double *T_trans;
@@ -266,7 +348,7 @@ struct HaaRegCost {
     __device__ double operator()(int i, int j) const {
         const double x = (double)beta.get(i);
         const int p = __builtin_amdgcn_readlane(prev, i);
-        const double tt = T_trans ? T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+        const double tt = T_trans ? (j < m ? T_trans[(int64_t)p * m + j] : 0.0) : (j == p ? 0.0 : 1.0);
         return -(x - lambda_ * (tt * (x > 1e-12 ? 1.0 : 0.0)));
     }
 };

@@ -24,6 +24,7 @@ namespace asg {
 // Row-major cost matrix in LDS (already transposed / sign-flipped)
 template <typename CT>
 struct DenseCost {
+    static constexpr bool kInMemory = true;
     const CT *c;
     int nc;
     __device__ double operator()(int i, int j) const { return (double)c[(size_t)i * nc + j]; }
@@ -35,6 +36,7 @@ struct DenseCost {
 // no LDS budget capping the problems resident per CU.
 typedef float f32x32 __attribute__((ext_vector_type(32)));
 struct RegCostF32 {
+    static constexpr bool kInMemory = false;
     f32x32 lo, hi;
     __device__ __forceinline__ float get(int i) const {
         const int ii = __builtin_amdgcn_readfirstlane(i);
@@ -72,19 +74,30 @@ __device__ int lsa_stage_regs(const IT *C, int64_t rs, int64_t cs, int nr0, int 
     return wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
 }
 
-// Order-preserving int32 key of a float64 rounded to float32: x <= y implies
-// key(x) <= key(y) (rounding is monotone; -0 is folded onto +0 so equal doubles get equal
-// keys).  A column whose key is the unique wave minimum therefore holds the unique
-// float64 minimum; equal keys (float64 ties, or values closer than float32 resolves)
-// fall back to the exact float64 selection.
-__device__ __forceinline__ int f32_key(double x) {
-    int b = __float_as_int((float)x);
-    b = (b == (int)0x80000000) ? 0 : b;
-    return b < 0 ? (b ^ 0x7fffffff) : b;
-}
-
-__device__ __forceinline__ int wave_min_i32(int v) {
-    return wave_allreduce(v, [](int a, int b) { return a < b ? a : b; });
+// wave64 minimum of a float32 that is never NaN, as one block of DPP-fused v_min_f32
+// (fminf on DPP operands would add a canonicalising v_max per step).  s_nop 1 covers the
+// VALU-write -> DPP/permlane-read hazard.  Call in wave-uniform control flow.
+__device__ __forceinline__ float wave_min_f32_nonan(float x) {
+    float y, t;
+    asm("s_nop 1\n\t"
+        "v_min_f32_dpp %0, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32 %1, %0\n\t"
+        "s_nop 1\n\t"
+        "v_permlane16_swap_b32 %0, %1\n\t"
+        "v_min_f32 %0, %0, %1\n\t"
+        "v_mov_b32 %1, %0\n\t"
+        "s_nop 1\n\t"
+        "v_permlane32_swap_b32 %0, %1\n\t"
+        "v_min_f32 %0, %0, %1"
+        : "=&v"(y), "=&v"(t)
+        : "v"(x));
+    return y;
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return wave_allreduce(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
@@ -115,13 +128,11 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
     }
     for (int cur = 0; cur < nr; ++cur) {
         double spc[CPL];
-        int pos[CPL];
-        bool sc[CPL];
+        int pos[CPL];  // position in scipy's `remaining`, -1 once scanned (or absent)
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int j = lane + kWave * c;
             spc[c] = __builtin_inf();
-            sc[c] = false;
             pos[c] = (j < nc) ? (nc - 1 - j) : -1;  // remaining[it] = nc - it - 1
         }
         int nrem = nc;
@@ -131,72 +142,66 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
         do {
             i = __builtin_amdgcn_readfirstlane(i);
             const double ui = lane_get(u, i);
-            int key[CPL];
-            int kl = 0x7fffffff;
+            float key[CPL];
+            float kl = __builtin_inff();
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const int j = lane + kWave * c;
                 // branch-free over the lane's columns: scanned / absent ones are relaxed
-                // too but neither updated nor keyed
+                // too but neither updated nor keyed (+inf keys: a remaining column at
+                // +inf ties with them and takes the exact path)
                 const bool rem = pos[c] >= 0;
-                const double cij = j < nc ? acc(i, j) : 0.0;  // never read past the matrix
+                // never read past a matrix in memory; register columns are always valid
+                const double cij = (!Acc::kInMemory || j < nc) ? acc(i, j) : 0.0;
                 const double r = ((minv + cij) - ui) - v[c];
                 const bool upd = rem && r < spc[c];
                 spc[c] = upd ? r : spc[c];
                 path[c] = upd ? i : path[c];
-                key[c] = rem ? f32_key(spc[c]) : 0x7fffffff;
-                kl = key[c] < kl ? key[c] : kl;
+                key[c] = rem ? (float)spc[c] : __builtin_inff();
+                kl = c == 0 ? key[0] : __builtin_fminf(kl, key[c]);
             }
-            const int kmin = wave_min_i32(kl);
-            int total = 0, jsel = -1, psel = -1;
-            double lowest = 0.0;
+            const float kmin = wave_min_f32_nonan(kl);
+            uint64_t cmsk[CPL];
+            int total = 0;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const uint64_t msk = __ballot(key[c] == kmin);
-                const int cnt = __popcll(msk);
-                if (cnt == 1 && total == 0) {
-                    const int src = __builtin_ctzll(msk);
-                    jsel = src + kWave * c;
-                    psel = __builtin_amdgcn_readlane(pos[c], src);
-                    const uint64_t sb = __builtin_bit_cast(uint64_t, spc[c]);
-                    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, src);
-                    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src);
-                    lowest = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
-                }
-                total += cnt;
+                cmsk[c] = __ballot(key[c] == kmin);
+                total += __popcll(cmsk[c]);
             }
+            // first candidate (the selection when it is the only one)
+            int src0 = 0, c0 = 0;
+#pragma unroll
+            for (int c = CPL - 1; c >= 0; --c) {
+                if (cmsk[c] != 0) {
+                    src0 = __builtin_ctzll(cmsk[c]);
+                    c0 = c;
+                }
+            }
+            double val0 = 0.0;
+            int pos0 = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                if (c == c0) {
+                    const uint64_t sb = __builtin_bit_cast(uint64_t, spc[c]);
+                    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);
+                    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src0);
+                    val0 = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+                    pos0 = __builtin_amdgcn_readlane(pos[c], src0);
+                }
+            }
+            double lowest = val0;
+            int jsel = src0 + kWave * c0, psel = pos0;
             if (total != 1) {
                 // Several columns share the minimum key.  Usually they hold exactly equal
-                // float64 values (scipy's tie case, frequent with correlated Q-values):
-                // check that against the first candidate's value, then apply scipy's tie
-                // rule with one 32-bit max-reduction.  Otherwise (distinct float64 values
-                // that round to one float32) take the exact float64 minimum first.
-                int src0 = -1, c0 = 0;
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    const uint64_t msk = __ballot(key[c] == kmin);
-                    if (src0 < 0 && msk != 0) {
-                        src0 = __builtin_ctzll(msk);
-                        c0 = c;
-                    }
-                }
-                double val0 = 0.0;
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    if (c == c0) {
-                        const uint64_t sb = __builtin_bit_cast(uint64_t, spc[c]);
-                        const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);
-                        const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src0);
-                        val0 = __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
-                    }
-                }
+                // float64 values (scipy's tie case: zero reduced costs, frequent with
+                // correlated Q-values): check that against the first candidate's value,
+                // then apply scipy's tie rule with one 32-bit max-reduction.  Otherwise
+                // (distinct float64 values that round to one float32) take the exact
+                // float64 minimum first.
                 bool all_equal = true;
 #pragma unroll
-                for (int c = 0; c < CPL; ++c) all_equal &= __ballot(key[c] == kmin && spc[c] != val0) == 0;
-                if (all_equal) {
-                    lowest = val0;
-                } else {
-                    // exact float64 minimum over the remaining columns
+                for (int c = 0; c < CPL; ++c) all_equal &= (__ballot(spc[c] != val0) & cmsk[c]) == 0;
+                if (!all_equal) {
                     double lo = __builtin_inf();
 #pragma unroll
                     for (int c = 0; c < CPL; ++c)
@@ -213,7 +218,7 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
                 uint32_t tk = 0;
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
-                    const bool cand = pos[c] >= 0 && spc[c] == lowest;
+                    const bool cand = all_equal ? ((cmsk[c] >> lane) & 1) != 0 : (pos[c] >= 0 && spc[c] == lowest);
                     const uint32_t k = (r4c[c] == -1) ? (0x80000000u | (uint32_t)pos[c])
                                                       : ((1u << 30) - (uint32_t)pos[c]);
                     tk = (cand && k > tk) ? k : tk;
@@ -230,17 +235,13 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
             const int last = nrem - 1;
             // remaining[index] = remaining[--num_remaining]
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                if (pos[c] == last) pos[c] = psel;
-                if (lane + kWave * c == jsel) {
-                    pos[c] = -1;
-                    sc[c] = true;
-                }
-            }
+            for (int c = 0; c < CPL; ++c)
+                pos[c] = (lane + kWave * c == jsel) ? -1 : (pos[c] == last ? psel : pos[c]);
             --nrem;
             minv = lowest;
             const int owner = lane_get(r4c, jsel);
-            infeasible = lowest == __builtin_inf();  // scipy: minVal == INFINITY
+            // scipy: minVal == INFINITY (compared on the bits: a scalar compare)
+            infeasible = __builtin_bit_cast(uint64_t, lowest) == 0x7ff0000000000000ull;
             if (owner == -1) sink = jsel;
             i = owner;
         } while (sink == -1 && !infeasible);
@@ -252,13 +253,14 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
         for (int c = 0; c < CPL; ++c) {
             const int r = lane + kWave * c;
             const int jm = col4row[c];
-            // gather (sc, spc) of column jm from its owner lane
+            // gather (scanned, spc) of column jm from its owner lane; a column of the
+            // matrix was scanned iff it left `remaining` (pos == -1)
             double spc_j = 0.0;
             int sc_j = 0;
 #pragma unroll
             for (int c2 = 0; c2 < CPL; ++c2) {
                 const double sv = __shfl(spc[c2], jm & 63, kWave);
-                const int sb = __shfl((int)sc[c2], jm & 63, kWave);
+                const int sb = __shfl(pos[c2], jm & 63, kWave) < 0;
                 if (jm >= 0 && (jm >> 6) == c2) {
                     spc_j = sv;
                     sc_j = sb;
@@ -271,7 +273,7 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
         }
 #pragma unroll
         for (int c = 0; c < CPL; ++c)
-            if (sc[c]) v[c] -= minv - spc[c];
+            if (pos[c] < 0 && lane + kWave * c < nc) v[c] -= minv - spc[c];
         // augment along path back to cur (uniform loop of lane reads/writes)
         int j = sink;
         while (true) {
