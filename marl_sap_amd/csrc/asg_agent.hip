@@ -457,8 +457,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AG
 // weights (packed fragments) into LDS once, then its 8 waves walk 256-row tiles; the
 // gate and fc2 A operands become conflict-free ds_read_b128 instead of L2 round trips.
 constexpr int kLdsWaves = 8;
+// ASG_AGENT_NUM_VGPR: cap of the persistent kernel's unified (arch + acc) VGPRs, e.g. 224
+// (amdgpu_num_vgpr counts half the unified file on gfx950) to leave room for a co-resident
+// env-step wave on the same SIMD; default: the compiler's choice under 2 waves/SIMD.
+#ifdef ASG_AGENT_NUM_VGPR
+#define ASG_AGENT_VGPR_ATTR __attribute__((amdgpu_num_vgpr(ASG_AGENT_NUM_VGPR / 2)))
+#else
+#define ASG_AGENT_VGPR_ATTR
+#endif
 template <bool RNN, bool SEL, bool GEN>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rnn_agent_lds_kernel(
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) ASG_AGENT_VGPR_ATTR
+rnn_agent_lds_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
     const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,

@@ -234,8 +234,14 @@ __global__ void __launch_bounds__(64) bids_assign_kernel(asg_batch_view bv, EnvS
 // ------------------------------------------------------------------------------------
 // step (mock_constellation_env.py:116-162 plus the runner's batch updates)
 // ------------------------------------------------------------------------------------
+#ifdef ASG_STEP_WAVES_PER_EU
+#define ASG_STEP_VGPR_ATTR __attribute__((amdgpu_waves_per_eu(ASG_STEP_WAVES_PER_EU)))
+#else
+#define ASG_STEP_VGPR_ATTR
+#endif
 template <int VEC, class Src, bool BIDS>
-__global__ void __launch_bounds__(256) step_kernel(Src src, asg_batch_view bv, EnvState st, int ts, int k) {
+__global__ void __launch_bounds__(256) ASG_STEP_VGPR_ATTR step_kernel(Src src, asg_batch_view bv, EnvState st, int ts,
+                                                                     int k) {
     extern __shared__ int s_dyn[];
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m, T = st.T, L = st.L;

@@ -65,10 +65,20 @@ def cases(dev, g):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--scan", action="store_true", help="sap64_corr at 1..16 problems per SIMD (latency vs occupancy)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     g = torch.Generator(device=dev).manual_seed(0)
+    if a.scan:
+        prof = torch.randn((16384, 1, 64), generator=g, device=dev)
+        q = prof + 0.05 * torch.randn((16384, 64, 64), generator=g, device=dev)
+        res = {}
+        for B in (256, 1024, 2048, 4096, 5120, 8192, 16384):
+            ms = timed(lambda: linear_sum_assignment_batched(q[:B], maximize=True, return_status=True), a.iters)
+            res[B] = round(ms, 4)
+        print(json.dumps({"scan_sap64_corr_ms": res}))
+        return
     out = {"lib": os.environ.get("ASG_LIB_PATH", "in-tree")}
     for name, C, maximize in cases(dev, g):
         _, col = linear_sum_assignment_batched(C, maximize=maximize)
