@@ -25,7 +25,13 @@ namespace asg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kRowsPerWave = 32;
+// row tiles of 16 per wave (ASG_AGENT_NT = 2: 32 rows per wave at 2 waves per SIMD;
+// 1: 16 rows per wave, fewer registers, more waves per SIMD)
+#ifndef ASG_AGENT_NT
+#define ASG_AGENT_NT 2
+#endif
+constexpr int kNT = ASG_AGENT_NT;
+constexpr int kRowsPerWave = 16 * kNT;
 #ifndef ASG_AGENT_WAVES
 #define ASG_AGENT_WAVES 2  // waves per SIMD the register budget is fitted to
 #endif
@@ -106,37 +112,39 @@ __device__ __forceinline__ void agent_rows(
     float *__restrict__ Q, const SelectArgs &sel) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= R) return;  // whole wave idle
-    int64_t rows[2];
-    bool ok[2];
+    int64_t rows[kNT];
+    bool ok[kNT];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < kNT; ++nt) {
         rows[nt] = row0 + 16 * nt + r;
         ok[nt] = rows[nt] < R;
     }
 
     // ---- fc1: x^T = relu(W1 X^T + b1), X rows streamed from HBM, 2 chunks in flight ----
-    f32x4 xB[4][2];
+    f32x4 xB[4][kNT];
     {
-        f32x4 acc[4][2];  // start from the bias (C layout: unit 16 mt + 4 q + v)
+        f32x4 acc[4][kNT];  // start from the bias (C layout: unit 16 mt + 4 q + v)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const float4 bb = *reinterpret_cast<const float4 *>(b1 + 16 * mt + 4 * q);
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{bb.x, bb.y, bb.z, bb.w};
+            for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f32x4{bb.x, bb.y, bb.z, bb.w};
         }
-        const float *xr[2] = {X + (ok[0] ? rows[0] : 0) * xs, X + (ok[1] ? rows[1] : 0) * xs};
+        const float *xr[kNT];
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) xr[nt] = X + (ok[nt] ? rows[nt] : 0) * xs;
         const int nk = (K + 15) / 16;
         // float4 row loads when K, the row stride and X are 16-B aligned; else guarded scalars
         const bool xvec = !GEN || (((K | xs) & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0);
-        float4 a0[2], w0[4], a1[2], w1[4];
-        auto load = [&](int t, float4 (&a4)[2], float4 (&w4)[4]) {
+        float4 a0[kNT], w0[4], a1[kNT], w1[4];
+        auto load = [&](int t, float4 (&a4)[kNT], float4 (&w4)[4]) {
             const int k = 16 * t + 4 * q;
             if (xvec) {
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && k < K);
+                for (int nt = 0; nt < kNT; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && k < K);
             } else {
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) {
+                for (int nt = 0; nt < kNT; ++nt) {
                     const float *p = xr[nt] + k;
                     a4[nt].x = ok[nt] && k + 0 < K ? p[0] : 0.f;
                     a4[nt].y = ok[nt] && k + 1 < K ? p[1] : 0.f;
@@ -150,10 +158,12 @@ __device__ __forceinline__ void agent_rows(
         load(0, a0, w0);
         if (nk > 1) load(1, a1, w1);
         for (int t = 0; t < nk; ++t) {
-            float4 a4[2] = {a0[0], a0[1]};
+            float4 a4[kNT];
+#pragma unroll
+            for (int i = 0; i < kNT; ++i) a4[i] = a0[i];
             float4 w4[4] = {w0[0], w0[1], w0[2], w0[3]};
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a0[i] = a1[i];
+            for (int i = 0; i < kNT; ++i) a0[i] = a1[i];
 #pragma unroll
             for (int i = 0; i < 4; ++i) w0[i] = w1[i];
             if (t + 2 < nk) load(t + 2, a1, w1);
@@ -162,27 +172,27 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                    for (int nt = 0; nt < 2; ++nt)
+                    for (int nt = 0; nt < kNT; ++nt)
                         acc[mt][nt] = mfma4(comp(w4[mt], e), comp(a4[nt], e), acc[mt][nt]);
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
+            for (int nt = 0; nt < kNT; ++nt)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v], 0.f);
     }
 
     // ---- h_in fragments (B operand of W_hh, and h of the GRU update), issued first -----
-    float4 hB[4][2];
+    float4 hB[4][kNT];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < kNT; ++nt)
             hB[t][nt] = ldg4(Hin + (ok[nt] ? rows[nt] : 0) * hs + 16 * t + 4 * q, RNN && Hin && ok[nt]);
 
     // ---- recurrent layer -> h'^T in registers (hp[hb] = B operand of fc2's chunk hb) ----
-    f32x4 hp[4][2];
+    f32x4 hp[4][kNT];
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb) {
         if (RNN) {
@@ -198,9 +208,9 @@ __device__ __forceinline__ void agent_rows(
             const float4 bhn = *reinterpret_cast<const float4 *>(bhh + 2 * kHid + u);
             const f32x4 r0 = {bir.x + bhr.x, bir.y + bhr.y, bir.z + bhr.z, bir.w + bhr.w};
             const f32x4 z0 = {biz.x + bhz.x, biz.y + bhz.y, biz.z + bhz.z, biz.w + bhz.w};
-            f32x4 gr[2], gz[2], gni[2], gnh[2];
+            f32x4 gr[kNT], gz[kNT], gni[kNT], gnh[kNT];
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
+            for (int nt = 0; nt < kNT; ++nt) {
                 gr[nt] = r0;
                 gz[nt] = z0;
                 gni[nt] = f32x4{bin.x, bin.y, bin.z, bin.w};
@@ -217,7 +227,7 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int nt = 0; nt < 2; ++nt) {
+                    for (int nt = 0; nt < kNT; ++nt) {
                         gr[nt] = mfma4(comp(wc[0], e), xB[t][nt][e], gr[nt]);
                         gz[nt] = mfma4(comp(wc[1], e), xB[t][nt][e], gz[nt]);
                         gni[nt] = mfma4(comp(wc[2], e), xB[t][nt][e], gni[nt]);
@@ -227,7 +237,7 @@ __device__ __forceinline__ void agent_rows(
                     }
             }
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
+            for (int nt = 0; nt < kNT; ++nt)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     const float rg = sigmoidf_(gr[nt][v]);
@@ -237,40 +247,50 @@ __device__ __forceinline__ void agent_rows(
                 }
         } else {
             const float4 bb = *reinterpret_cast<const float4 *>(bih + 16 * hb + 4 * q);
-            f32x4 a2[2] = {f32x4{bb.x, bb.y, bb.z, bb.w}, f32x4{bb.x, bb.y, bb.z, bb.w}};
+            f32x4 a2[kNT];
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt) a2[nt] = f32x4{bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const float4 w = Wihp[pk(t, hb, 4, lane)];
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int nt = 0; nt < 2; ++nt) a2[nt] = mfma4(comp(w, e), xB[t][nt][e], a2[nt]);
+                    for (int nt = 0; nt < kNT; ++nt) a2[nt] = mfma4(comp(w, e), xB[t][nt][e], a2[nt]);
             }
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt)
+            for (int nt = 0; nt < kNT; ++nt)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) hp[hb][nt][v] = fmaxf(a2[nt][v], 0.f);
         }
         // h' block -> HBM (the new hidden state), one float4 per lane and row
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
+        for (int nt = 0; nt < kNT; ++nt)
             if (ok[nt])
                 *reinterpret_cast<float4 *>(Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
                     make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
     }
 
     // ---- selection state: (env, agent) of each row, running argmax, availability bits ----
-    const uint8_t *arow[2] = {nullptr, nullptr};
+    const uint8_t *arow[kNT];
     bool av4 = false;
-    float best[2] = {-__builtin_inff(), -__builtin_inff()};
-    int bj[2] = {0x7fffffff, 0x7fffffff};
-    uint64_t amask[2][2] = {{0, 0}, {0, 0}};  // [row][c >> 4] bit 4 (c & 15) + v <-> task 16 c + 4 q + v
-    int64_t oidx[2] = {0, 0};
+    float best[kNT];
+    int bj[kNT];
+    uint64_t amask[kNT][2];  // [row][c >> 4] bit 4 (c & 15) + v <-> task 16 c + 4 q + v
+    int64_t oidx[kNT];
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) {
+        arow[nt] = nullptr;
+        best[nt] = -__builtin_inff();
+        bj[nt] = 0x7fffffff;
+        amask[nt][0] = amask[nt][1] = 0;
+        oidx[nt] = 0;
+    }
     if (SEL) {
         const int64_t b0 = row0 / sel.n;
         const int i0 = (int)(row0 - b0 * sel.n);
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+        for (int nt = 0; nt < kNT; ++nt) {
             int64_t b = b0;
             int i = i0 + 16 * nt + r;
             while (i >= sel.n) {
@@ -289,10 +309,12 @@ __device__ __forceinline__ void agent_rows(
     for (int c = 0; c < nct; ++c) {
         const bool full = !GEN || 16 * c + 16 <= nout;  // wave-uniform: only the last tile can be partial
         const int j0 = 16 * c + 4 * q;          // this lane's first task of the tile
-        uint32_t av[2] = {0u, 0u};  // 4 availability bits of this lane's tasks, per row
+        uint32_t av[kNT];  // 4 availability bits of this lane's tasks, per row
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) av[nt] = 0u;
         if (SEL) {
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
+            for (int nt = 0; nt < kNT; ++nt) {
                 const uint8_t *ap = arow[nt] + j0;
                 uint32_t w = 0;
                 if (ok[nt]) {
@@ -318,7 +340,9 @@ __device__ __forceinline__ void agent_rows(
             bq.z = j0 + 2 < nout ? b2[j0 + 2] : 0.f;
             bq.w = j0 + 3 < nout ? b2[j0 + 3] : 0.f;
         }
-        f32x4 a2[2] = {f32x4{bq.x, bq.y, bq.z, bq.w}, f32x4{bq.x, bq.y, bq.z, bq.w}};
+        f32x4 a2[kNT];
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) a2[nt] = f32x4{bq.x, bq.y, bq.z, bq.w};
         float4 w2[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) w2[t] = W2p[pk(t, c, nct, lane)];
@@ -327,9 +351,9 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) a2[nt] = mfma4(comp(w2[t], e), hp[t][nt][e], a2[nt]);
+                for (int nt = 0; nt < kNT; ++nt) a2[nt] = mfma4(comp(w2[t], e), hp[t][nt][e], a2[nt]);
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+        for (int nt = 0; nt < kNT; ++nt) {
             if (Q && ok[nt]) {
                 float *qp = Q + rows[nt] * nout + j0;
                 if (full && qvec) {
@@ -359,7 +383,7 @@ __device__ __forceinline__ void agent_rows(
 
     // ---- reduce each row over its 4 lanes (q = 0..3: lane ^ 16, lane ^ 32) -------------
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < kNT; ++nt) {
         auto red = [&](auto swp) {
             const SwapPair pb = swp(__builtin_bit_cast(uint32_t, best[nt]));
             const SwapPair pj = swp((uint32_t)bj[nt]);
@@ -377,7 +401,7 @@ __device__ __forceinline__ void agent_rows(
     }
     // lane q == nt finishes row nt: greedy action, or with probability epsilon the
     // target-th available task in index order (Categorical over avail, as asg_select.hip)
-    const int nt = q & 1;
+    const int nt = kNT == 1 ? 0 : (q & 1);
     const int64_t row = rows[nt];
     int action = bj[nt] == 0x7fffffff ? 0 : bj[nt];
     bool explore = false;
@@ -385,7 +409,7 @@ __device__ __forceinline__ void agent_rows(
     if (sel.epsilon > 0.0f) {
         rr = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect, sel.counter}, sel.k0, sel.k1);
         constexpr float k2m24 = 5.9604644775390625e-08f;
-        explore = ok[nt] && q < 2 && (float)(rr.x >> 8) * k2m24 < sel.epsilon;
+        explore = ok[nt] && q < kNT && (float)(rr.x >> 8) * k2m24 < sel.epsilon;
     }
     if (__ballot(explore)) {  // some row of the wave explores (about epsilon of the rows)
         // Per 64-task window: the row's availability in task order, assembled from its 4
@@ -393,7 +417,7 @@ __device__ __forceinline__ void agent_rows(
         // the exploring lane then takes the target-th set bit by a popcount bisection.
         const int nwin = (nct + 3) / 4;
         int target = -1, found = -1;
-        for (int ntt = 0; ntt < 2; ++ntt) {
+        for (int ntt = 0; ntt < kNT; ++ntt) {
             const bool mine_row = explore && nt == ntt;
             int cnt = __popcll(amask[ntt][0]) + (GEN ? __popcll(amask[ntt][1]) : 0);
             {
@@ -438,7 +462,7 @@ __device__ __forceinline__ void agent_rows(
         }
         if (found >= 0) action = found;
     }
-    if (q < 2 && ok[nt]) sel.out[oidx[nt]] = action;
+    if (q < kNT && ok[nt]) sel.out[oidx[nt]] = action;
 }
 
 // One wave per 32 rows, weights read through L1/L2 (any n_out).
@@ -456,7 +480,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AG
 // Persistent variant: one 512-thread workgroup per CU copies the recurrent and output
 // weights (packed fragments) into LDS once, then its 8 waves walk 256-row tiles; the
 // gate and fc2 A operands become conflict-free ds_read_b128 instead of L2 round trips.
-constexpr int kLdsWaves = 8;
+#ifndef ASG_AGENT_LDS_WAVES_PER_SIMD
+#define ASG_AGENT_LDS_WAVES_PER_SIMD 2
+#endif
+constexpr int kLdsWaves = 4 * ASG_AGENT_LDS_WAVES_PER_SIMD;
 // ASG_AGENT_NUM_VGPR: cap of the persistent kernel's unified (arch + acc) VGPRs, e.g. 224
 // (amdgpu_num_vgpr counts half the unified file on gfx950) to leave room for a co-resident
 // env-step wave on the same SIMD; default: the compiler's choice under 2 waves/SIMD.
@@ -466,7 +493,8 @@ constexpr int kLdsWaves = 8;
 #define ASG_AGENT_VGPR_ATTR
 #endif
 template <bool RNN, bool SEL, bool GEN>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) ASG_AGENT_VGPR_ATTR
+__global__ void __launch_bounds__(64 * kLdsWaves) __attribute__((amdgpu_waves_per_eu(ASG_AGENT_LDS_WAVES_PER_SIMD)))
+ASG_AGENT_VGPR_ATTR
 rnn_agent_lds_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,

@@ -13,4 +13,7 @@ timeout -k 10 300 python bench.py > "$OUT/bench.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 bench.py --cpu-baseline 0 > "$OUT/kt.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5 > "$OUT/fetch.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5 > "$OUT/write.log" 2>&1 &&
+timeout -k 10 300 python bench.py --selector sap --cpu-baseline 0 > "$OUT/bench_sap.log" 2>&1 &&
+timeout -k 10 300 python tools/bench_lsa.py > "$OUT/bench_lsa.json" 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_sap" -o run -- python3 bench.py --selector sap --cpu-baseline 0 --steps 20 --warmup 5 > "$OUT/kt_sap.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq" -o run -- python3 bench.py --cpu-baseline 0 --steps 20 --warmup 5 > "$OUT/sq.log" 2>&1
