@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(64) bids_assign_kernel(asg_batch_view bv, EnvS
     if constexpr (CPL == 1) {  // m <= 64: the working matrix stays in registers
         RegCostF32 rc;
         status = lsa_stage_regs<float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, rc);
-        if (status == ASG_OK) status = lsa_solve_wave<1>(rc, n, m, c4r);
+        if (status == ASG_OK) status = lsa_solve_reg64(rc, n, m, c4r);
     } else {
         status = lsa_stage_wave<float, float>(bids, bv.actions.stride[2], bv.actions.stride[3], n, m, true, cost);
         if (status == ASG_OK) status = lsa_solve_wave<CPL>(DenseCost<float>{cost, m}, n, m, c4r);

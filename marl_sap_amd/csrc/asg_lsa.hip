@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(64) lsa_reg_kernel(const float *C, int64_t s0,
     int status = lsa_stage_regs<float>(C + b * s0, s1, s2, nr0, nc0, maximize != 0, rc);
     if (status == ASG_OK) {
         int c4r[1];
-        status = lsa_solve_wave<1>(rc, nr, nc, c4r);
+        status = lsa_solve_reg64(rc, nr, nc, c4r);
         if (status == ASG_OK) lsa_emit_wave(c4r, nr0, nc0, mark, ro, co, nullptr);
     }
     const int lane = threadIdx.x;
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(64) sap_select_kernel(const float *q, int64_t 
     float *co = col_out + b * n;
     if (status == ASG_OK) {
         int c4r[1];
-        status = lsa_solve_wave<1>(rc, n, m, c4r);
+        status = lsa_solve_reg64(rc, n, m, c4r);
         if (status == ASG_OK) lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co);
     }
     if (status != ASG_OK)
@@ -351,6 +351,7 @@ struct HaaRegCost {
         const double tt = T_trans ? (j < m ? T_trans[(int64_t)p * m + j] : 0.0) : (j == p ? 0.0 : 1.0);
         return -(x - lambda_ * (tt * (x > 1e-12 ? 1.0 : 0.0)));
     }
+    __device__ double col(int i) const { return (*this)(i, (int)(threadIdx.x & 63)); }
 };
 
 __global__ void __launch_bounds__(64) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
@@ -375,7 +376,7 @@ __global__ void __launch_bounds__(64) haa_reg_kernel(const float *beta, int64_t 
     float *co = col_out + b * n;
     if (status == ASG_OK) {
         int c4r[1];
-        status = lsa_solve_wave<1>(acc, n, m, c4r);
+        status = lsa_solve_reg64(acc, n, m, c4r);
         if (status == ASG_OK) lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co);
     }
     if (status != ASG_OK)

@@ -44,6 +44,7 @@ struct RegCostF32 {
         return ii < 32 ? x0 : x1;
     }
     __device__ __forceinline__ double operator()(int i, int) const { return (double)get(i); }
+    __device__ __forceinline__ double col(int i) const { return (double)get(i); }
 };
 
 // Load the lane's working column (scipy orientation: transposed when nr0 > nc0, negated
@@ -305,6 +306,112 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
         }
     }
     return ASG_OK;
+}
+
+// The same algorithm specialised for nc <= 64 columns (one per lane) with a register
+// accessor (RegCostF32, HaaRegCost): `remaining` membership is a scalar 64-bit mask
+// (turned into a lane predicate by inverse-ballot, so no per-lane compare), the row read
+// is a uniform branch plus one indexed move, and column removal is scalar mask work.
+// Identical decisions to lsa_solve_wave<1> (same keys, same tie rule, same float64
+// operation order); ~30 vector instructions per augmenting-path step instead of ~42.
+template <class Acc>
+__device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]) {
+#ifdef ASG_LSA_GENERIC_REG
+    return lsa_solve_wave<1>(acc, nr, nc, col4row);
+#else
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t colmask = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);  // lanes that hold a column
+    const float kInfF = __builtin_inff();
+    double v = 0.0, u = 0.0;
+    int r4c = -1, path = -1, c4r = -1;
+    for (int cur = 0; cur < nr; ++cur) {
+        double spc = __builtin_inf();
+        int pos = (lane < nc) ? (nc - 1 - lane) : -1;  // remaining[it] = nc - it - 1
+        uint64_t rem = colmask;                         // columns still in `remaining`
+        int nrem = nc;
+        double minv = 0.0;
+        int i = cur, sink = -1;
+        bool infeasible = false;
+        do {
+            i = __builtin_amdgcn_readfirstlane(i);
+            const double ui = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                                              (int)(uint32_t)__builtin_bit_cast(uint64_t, u), i)) |
+                                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                                                  (int)(uint32_t)(__builtin_bit_cast(uint64_t, u) >> 32), i)
+                                                              << 32));
+            const bool remb = __builtin_amdgcn_inverse_ballot_w64(rem);
+            const double r = ((minv + acc.col(i)) - ui) - v;
+            const bool upd = remb && r < spc;
+            spc = upd ? r : spc;
+            path = upd ? i : path;
+            const float key = remb ? (float)spc : kInfF;
+            const float kmin = wave_min_f32_nonan(key);
+            const uint64_t cm = __ballot(key == kmin) & rem;
+            const int src0 = (int)__builtin_ctzll(cm);
+            const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
+            const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);
+            const uint32_t hi0 = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src0);
+            double lowest = __builtin_bit_cast(double, (uint64_t)lo0 | ((uint64_t)hi0 << 32));
+            int jsel = src0, psel = __builtin_amdgcn_readlane(pos, src0);
+            uint32_t lowest_hi = hi0, lowest_lo = lo0;
+            if (__popcll(cm) != 1) {
+                // equal keys: exact float64 ties (checked against the first candidate) or,
+                // rarely, distinct doubles rounding to one float (exact minimum first)
+                uint64_t cand = cm;
+                if ((__ballot(spc != lowest) & cm) != 0) {
+                    const double lo = remb ? spc : __builtin_inf();
+                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));
+                    lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
+                    lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
+                    lowest = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+                    cand = __ballot(spc == lowest) & rem;
+                }
+                // scipy's tie rule: unassigned 2^31 | pos (largest position), else 2^30 - pos
+                // (smallest position), max-reduced
+                const bool cb = __builtin_amdgcn_inverse_ballot_w64(cand);
+                const uint32_t k = (r4c == -1) ? (0x80000000u | (uint32_t)pos) : ((1u << 30) - (uint32_t)pos);
+                const uint32_t tk = __builtin_amdgcn_readfirstlane(wave_max_u32(cb ? k : 0u));
+                psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
+                jsel = (int)__builtin_ctzll(__ballot(pos == psel) & rem);  // positions are distinct
+            }
+            // remaining[index] = remaining[--num_remaining]
+            const int last = nrem - 1;
+            const uint64_t jbit = 1ull << jsel;
+            pos = __builtin_amdgcn_inverse_ballot_w64(jbit) ? -1 : (pos == last ? psel : pos);
+            rem &= ~jbit;
+            --nrem;
+            minv = lowest;
+            const int owner = __builtin_amdgcn_readlane(r4c, jsel);
+            infeasible = lowest_hi == 0x7ff00000u && lowest_lo == 0u;  // scipy: minVal == INFINITY
+            if (owner == -1) sink = jsel;
+            i = owner;
+        } while (sink == -1 && !infeasible);
+        if (infeasible) return ASG_E_LSA_INFEASIBLE;
+        // dual update: u[cur] += minv; u[r] += minv - spc[col4row[r]] for the other visited
+        // rows (row r != cur was visited iff its column was scanned); v[j] -= minv - spc[j]
+        // for the scanned columns (matrix columns no longer in `remaining`)
+        const int jm = c4r;
+        const double spc_j = __shfl(spc, jm & 63, kWave);
+        const bool sc_j = jm >= 0 && ((rem >> (jm & 63)) & 1ull) == 0;
+        if (lane < nr) {
+            if (lane == cur) u += minv;
+            else if (sc_j) u += minv - spc_j;
+        }
+        if (lane < nc && ((rem >> lane) & 1ull) == 0) v -= minv - spc;
+        // augment along path back to cur
+        int j = sink;
+        while (true) {
+            const int pi = __builtin_amdgcn_readlane(path, j);
+            r4c = (lane == j) ? pi : r4c;
+            const int t = __builtin_amdgcn_readlane(c4r, pi);
+            c4r = (lane == pi) ? j : c4r;
+            j = t;
+            if (pi == cur) break;
+        }
+    }
+    col4row[0] = c4r;
+    return ASG_OK;
+#endif
 }
 
 // Stage C (input [nr0][nc0], strides in elements) into dst as scipy's working matrix:
