@@ -104,7 +104,10 @@ static size_t lsa_scratch_bytes(int nr0) { return sizeof(int) * nr0 + 64; }
 
 // float32 problems up to 64 x 64 (working orientation): the working matrix lives in the
 // wave's registers (RegCostF32), so residency is set by registers alone (no LDS)
-__global__ void __launch_bounds__(64) lsa_reg_kernel(const float *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
+#ifndef ASG_LSA_REG_WAVES
+#define ASG_LSA_REG_WAVES 5
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) lsa_reg_kernel(const float *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
                                                      int nc0, int maximize, int64_t *row_out, int64_t *col_out,
                                                      int32_t *status_out) {
     __shared__ int mark[64];
@@ -172,7 +175,7 @@ hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3]
 // register-resident LSA (maximize).  The reference runs, per env on the host: abs, mean,
 // ones * avg * eps * 2, torch.normal, +=, scipy.
 // ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
                                                         int64_t env_base, float *col_out, int32_t *status_out) {
     const int64_t b = blockIdx.x;
@@ -354,7 +357,7 @@ struct HaaRegCost {
     __device__ double col(int i) const { return (*this)(i, (int)(threadIdx.x & 63)); }
 };
 
-__global__ void __launch_bounds__(64) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
                                                      const int64_t *prev, int64_t p0, int64_t p1, int n, int m,
                                                      const double *T_trans, double lambda_, float *col_out,
                                                      int32_t *status_out) {

@@ -122,6 +122,24 @@ __device__ __forceinline__ float wave_min_f32_nonan(float x) {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return wave_allreduce(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
 }
+// wave64 maximum of a uint32, returned wave-uniform: the row_bcast fold of
+// wave_min_f32_nonan with v_max_u32
+__device__ __forceinline__ uint32_t wave_max_u32_bcast(uint32_t x) {
+    asm("s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
+        "s_nop 1\n\t"
+        "v_max_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc"
+        : "+v"(x));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
 
 // Solve on the working matrix acc(i, j), i < nr <= nc <= 64*CPL (scipy's orientation).
 // All per-row and per-column state lives in registers, distributed over the lanes
@@ -370,7 +388,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
                 // (smallest position), max-reduced
                 const bool cb = __builtin_amdgcn_inverse_ballot_w64(cand);
                 const uint32_t k = (r4c == -1) ? (0x80000000u | (uint32_t)pos) : ((1u << 30) - (uint32_t)pos);
-                const uint32_t tk = __builtin_amdgcn_readfirstlane(wave_max_u32(cb ? k : 0u));
+                const uint32_t tk = wave_max_u32_bcast(cb ? k : 0u);
                 psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
                 jsel = (int)__builtin_ctzll(__ballot(pos == psel) & rem);  // positions are distinct
             }
