@@ -214,7 +214,8 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
  * nn.Linear / nn.GRUCell layouts (W1 [hidden][K], W_ih / W_hh [3*hidden][hidden] -- or
  * W_ih = W_rnn [hidden][hidden] and W_hh = NULL when use_rnn = 0 -- and W2 [n_out][hidden])
  * into a device buffer of asg_rnn_agent_packed_size() bytes.
- * X [R][K] f32, any K >= 1 and row stride x_stride (float4 row loads when K, x_stride and
+ * X [R][K] f32, any K >= 1 and row stride x_stride (>= K, or 0 = one row broadcast to all;
+ * float4 row loads when K, x_stride and
  * x are 16-B aligned, guarded scalar loads otherwise); h_in [R][hidden] with row stride
  * h_stride (% 4 == 0, 16-B aligned; 0 = one row broadcast to all, NULL = zeros); biases
  * contiguous.  Outputs h_out [R][hidden], q_out [R][n_out], contiguous.  hidden must be 64,

@@ -397,7 +397,7 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
                           int hidden, int n_out, int use_rnn, float *h_out, float *q_out, void *hip_stream) {
     if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !q_out || R < 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_forward: bad arguments");
-    if (!agent_shape_ok(K, hidden, n_out) || x_stride < K || h_stride % 4 != 0 ||
+    if (!agent_shape_ok(K, hidden, n_out) || (x_stride != 0 && x_stride < K) || h_stride % 4 != 0 ||
         (reinterpret_cast<uintptr_t>(x) % 4) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG,
                     "asg_rnn_agent_forward: needs hidden == 64, 1 <= n_out <= 512, x_stride >= K and 16-B aligned "
@@ -417,7 +417,7 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
     if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !avail || !avail_strides || !out || !out_strides ||
         !status || R < 0 || n <= 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: bad arguments");
-    if (!agent_shape_ok(K, hidden, n_out) || x_stride < K || h_stride % 4 != 0 ||
+    if (!agent_shape_ok(K, hidden, n_out) || (x_stride != 0 && x_stride < K) || h_stride % 4 != 0 ||
         (reinterpret_cast<uintptr_t>(x) % 4) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: unsupported shape / alignment");
     if (!(epsilon >= 0.0 && epsilon <= 1.0))

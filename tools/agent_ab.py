@@ -18,6 +18,9 @@ def main(E=16384, n=64, m=64, K=256, rounds=7, iters=30):
                            epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=0)
     fused = RNNFusedAgent(K, args).to(dev)
     x = torch.randn((E * n, K), device=dev)
+    if os.environ.get("ASG_AB_L2X"):  # diagnostic: every row reads row 0 (L2-resident obs)
+        x = torch.randn((1, K), device=dev).expand(E * n, K)
+        fused._prep = lambda inputs, hid: (inputs, hid.reshape(-1, 64), 64)
     h = torch.randn((E * n, 64), device=dev)
     avail = torch.ones((E, n, m), dtype=torch.bool, device=dev)
     out = torch.empty((E, n), dtype=torch.int64, device=dev)
@@ -35,7 +38,7 @@ def main(E=16384, n=64, m=64, K=256, rounds=7, iters=30):
             if r:
                 res.append(a.elapsed_time(b) / iters)
     res.sort()
-    print(f"{os.environ.get('ASG_LIB_PATH', 'default')} K={K} m={m} median {res[len(res) // 2]:.4f} ms "
+    print(f"{os.environ.get('ASG_LIB_PATH', 'default')} l2x={bool(os.environ.get('ASG_AB_L2X'))} K={K} m={m} median {res[len(res) // 2]:.4f} ms "
           f"min {res[0]:.4f}", flush=True)
 
 
