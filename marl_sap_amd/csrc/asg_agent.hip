@@ -96,7 +96,7 @@ __global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
 // t = mt, so activations go from layer to layer in registers: no LDS, no transposes, no
 // barriers.  One wave owns 32 rows (nt = 0, 1); lane (r, q) = (l & 15, l >> 4).
 // ---------------------------------------------------------------------------------
-// GEN = false: the bench shapes (K % 4 == 0 with 16-B aligned rows, n_out % 16 == 0, n_out
+// GEN = false: the bench shapes (K % 32 == 0 with 16-B aligned rows, n_out % 16 == 0, n_out
 // <= 256).  GEN = true: any K, any n_out <= 512 (checked by the ABI): guarded scalar row
 // loads, and the last output tile partial when n_out % 16 != 0 (zero weight rows, masked
 // bias / Q / availability).  A lane keeps 4 availability bits per output tile in two u64
@@ -120,6 +120,23 @@ __device__ __forceinline__ void agent_rows(
         ok[nt] = rows[nt] < R;
     }
 
+    // ---- h_in fragments (B operand of W_hh, and h of the GRU update): issued before fc1 so
+    // they arrive under its MFMAs (issued after it, every tile's GRU waited on them) -------
+    float4 hB[4][kNT];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt)
+            // rows past R read row 0 (their results are discarded): unconditional loads
+            // keep the memory counters countable (no exec-masked branches)
+            hB[t][nt] = GEN ? ldg4(Hin + (ok[nt] ? rows[nt] : 0) * hs + 16 * t + 4 * q, RNN && Hin && ok[nt])
+                            : ((RNN && Hin) ? *reinterpret_cast<const float4 *>(Hin + (ok[nt] ? rows[nt] : 0) * hs +
+                                                                               16 * t + 4 * q)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f));
+#ifdef ASG_AGENT_H_EARLY
+    __builtin_amdgcn_sched_barrier(0);  // issue them here, not next to the GRU
+#endif
+
     // ---- fc1: x^T = relu(W1 X^T + b1), X rows streamed from HBM, 2 chunks in flight ----
     f32x4 xB[4][kNT];
     {
@@ -136,10 +153,13 @@ __device__ __forceinline__ void agent_rows(
         const int nk = (K + 15) / 16;
         // float4 row loads when K, the row stride and X are 16-B aligned; else guarded scalars
         const bool xvec = !GEN || (((K | xs) & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0);
-        float4 a0[kNT], w0[4], a1[kNT], w1[4];
+        float4 aA[kNT], wA[4], aB[kNT], wB[4];
         auto load = [&](int t, float4 (&a4)[kNT], float4 (&w4)[4]) {
             const int k = 16 * t + 4 * q;
-            if (xvec) {
+            if (!GEN) {  // K % 32 == 0, aligned rows: every chunk is in bounds
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) a4[nt] = *reinterpret_cast<const float4 *>(xr[nt] + k);
+            } else if (xvec) {
 #pragma unroll
                 for (int nt = 0; nt < kNT; ++nt) a4[nt] = ldg4(xr[nt] + k, ok[nt] && k < K);
             } else {
@@ -155,18 +175,7 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) w4[mt] = W1p[pk(t, mt, 4, lane)];
         };
-        load(0, a0, w0);
-        if (nk > 1) load(1, a1, w1);
-        for (int t = 0; t < nk; ++t) {
-            float4 a4[kNT];
-#pragma unroll
-            for (int i = 0; i < kNT; ++i) a4[i] = a0[i];
-            float4 w4[4] = {w0[0], w0[1], w0[2], w0[3]};
-#pragma unroll
-            for (int i = 0; i < kNT; ++i) a0[i] = a1[i];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) w0[i] = w1[i];
-            if (t + 2 < nk) load(t + 2, a1, w1);
+        auto chunk = [&](const float4 (&a4)[kNT], const float4 (&w4)[4]) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -174,6 +183,48 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
                     for (int nt = 0; nt < kNT; ++nt)
                         acc[mt][nt] = mfma4(comp(w4[mt], e), comp(a4[nt], e), acc[mt][nt]);
+        };
+        // ping-pong over two register buffers, unrolled by two: a buffer is refilled right
+        // after its chunk's MFMAs, so two chunks stay in flight without register copies
+        // (a rotating a0 = a1 form compiles to copies that wait for the newest loads)
+#ifdef ASG_AGENT_FC1_PINGPONG
+        if (!GEN) {
+            // nk even (K % 32 == 0): ping-pong over two register buffers, each refilled right
+            // after its chunk's MFMAs, with scheduling barriers so the refills are not sunk
+            // next to their uses.  Measured slower (0.894 vs 0.868 ms): obs latency is not
+            // what bounds this kernel (tools/agent_ab.py, ASG_AB_L2X).
+            load(0, aA, wA);
+            __builtin_amdgcn_sched_barrier(0);
+            load(1, aB, wB);
+            __builtin_amdgcn_sched_barrier(0);
+            const int last = nk - 1;
+            for (int t = 0; t < nk; t += 2) {
+                chunk(aA, wA);
+                __builtin_amdgcn_sched_barrier(0);
+                load(t + 2 < last ? t + 2 : last, aA, wA);
+                __builtin_amdgcn_sched_barrier(0);
+                chunk(aB, wB);
+                __builtin_amdgcn_sched_barrier(0);
+                load(t + 3 < last ? t + 3 : last, aB, wB);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else
+#endif
+        {
+            load(0, aA, wA);
+            if (nk > 1) load(1, aB, wB);
+            for (int t = 0; t < nk; ++t) {
+                float4 a4[kNT];
+#pragma unroll
+                for (int i = 0; i < kNT; ++i) a4[i] = aA[i];
+                float4 w4[4] = {wA[0], wA[1], wA[2], wA[3]};
+#pragma unroll
+                for (int i = 0; i < kNT; ++i) aA[i] = aB[i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wA[i] = wB[i];
+                if (t + 2 < nk) load(t + 2, aB, wB);
+                chunk(a4, w4);
+            }
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -182,14 +233,6 @@ __device__ __forceinline__ void agent_rows(
 #pragma unroll
                 for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v], 0.f);
     }
-
-    // ---- h_in fragments (B operand of W_hh, and h of the GRU update), issued first -----
-    float4 hB[4][kNT];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < kNT; ++nt)
-            hB[t][nt] = ldg4(Hin + (ok[nt] ? rows[nt] : 0) * hs + 16 * t + 4 * q, RNN && Hin && ok[nt]);
 
     // ---- recurrent layer -> h'^T in registers (hp[hb] = B operand of fc2's chunk hb) ----
     f32x4 hp[4][kNT];
@@ -563,7 +606,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU)
     const int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)((nout + 15) / 16) * 64;
     const size_t lds = (size_t)nrf4 * sizeof(float4);
-    const bool gen = ((K | xs) & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 || nout > 256;
+    const bool gen = (K & 31) != 0 || (xs & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 ||
+                     nout > 256;
     if (use_lds_weights() && lds <= 160 * 1024) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
