@@ -31,6 +31,9 @@
 #include "asg_device.h"
 #include "asg_internal.h"
 
+#ifndef ASG_REAL_PROF_SKIP
+#define ASG_REAL_PROF_SKIP 0  // profiling only: skip phases (wrong results)
+#endif
 namespace asg {
 
 struct RealState {
@@ -122,51 +125,70 @@ __device__ __forceinline__ int wave_select(const double *vals, unsigned char *ta
 }
 
 // Top-K of vals[0..len) in the same order as K successive wave_select calls, for short
-// lists (len <= 64 * CAP): every lane sorts its own CAP candidates (j = lane + 64 c) once
-// in registers, then each pick is two wave reductions over the lanes' list heads and a
-// register shift in the winning lane -- no rescans, no LDS round trips.
+// lists (len <= 64 * CAP; vals in LDS): every lane sorts its own CAP candidates
+// (j = lane + 64 c) once, then keeps only their indices.  Each pick reads the lanes' list
+// heads back from LDS and reduces float32-rounded keys (one DPP-fused max): rounding is
+// monotone, so a unique maximal key is the unique float64 maximum; equal keys take the
+// exact path (float64 compare against the first candidate, then the index rule).  The
+// winning lane shifts its index list -- no rescans.
 template <int CAP, bool HIGHER_TIES>
 __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int K, int *out) {
     const int lane = threadIdx.x & 63;
-    double v[CAP];
     int id[CAP];
+    {
+        double v[CAP];
 #pragma unroll
-    for (int c = 0; c < CAP; ++c) {
-        const int j = lane + 64 * c;
-        v[c] = j < len ? vals[j] : -INFINITY;
-        id[c] = j < len ? j : -1;  // -1: no candidate (sorts last, never wins)
+        for (int c = 0; c < CAP; ++c) {
+            const int j = lane + 64 * c;
+            v[c] = j < len ? vals[j] : -INFINITY;
+            id[c] = j < len ? j : -1;  // -1: no candidate (sorts last, never wins)
+        }
+        auto before = [](double va, int ia, double vb, int ib) {
+            if (ia < 0) return false;
+            if (ib < 0) return true;
+            return va > vb || (va == vb && (HIGHER_TIES ? ia > ib : ia < ib));
+        };
+#pragma unroll
+        for (int pass = 0; pass < CAP; ++pass)  // odd-even transposition sort, fully unrolled
+#pragma unroll
+            for (int c = pass & 1; c + 1 < CAP; c += 2)
+                if (before(v[c + 1], id[c + 1], v[c], id[c])) {
+                    const double tv = v[c];
+                    v[c] = v[c + 1];
+                    v[c + 1] = tv;
+                    const int ti = id[c];
+                    id[c] = id[c + 1];
+                    id[c + 1] = ti;
+                }
     }
-    auto before = [](double va, int ia, double vb, int ib) {
-        if (ia < 0) return false;
-        if (ib < 0) return true;
-        return va > vb || (va == vb && (HIGHER_TIES ? ia > ib : ia < ib));
-    };
-#pragma unroll
-    for (int pass = 0; pass < CAP; ++pass)  // odd-even transposition sort, fully unrolled
-#pragma unroll
-        for (int c = pass & 1; c + 1 < CAP; c += 2)
-            if (before(v[c + 1], id[c + 1], v[c], id[c])) {
-                const double tv = v[c];
-                v[c] = v[c + 1];
-                v[c + 1] = tv;
-                const int ti = id[c];
-                id[c] = id[c + 1];
-                id[c + 1] = ti;
-            }
     for (int k = 0; k < K; ++k) {
         const bool has = id[0] >= 0;
-        const double vmax =
-            wave_allreduce(has ? v[0] : -INFINITY, [](double a, double b) { return a > b ? a : b; });
-        const bool cand = has && v[0] == vmax;
-        const int win = HIGHER_TIES ? wave_max_i32(cand ? id[0] : -1) : -wave_max_i32(cand ? -id[0] : -0x7fffffff);
-        if (lane == 0) out[k] = win;
-        if (id[0] == win) {
-#pragma unroll
-            for (int c = 0; c + 1 < CAP; ++c) {
-                v[c] = v[c + 1];
-                id[c] = id[c + 1];
+        const double x = has ? vals[id[0]] : -INFINITY;
+        const float key = has ? (float)x : -INFINITY;
+        const float kmax = wave_max_f32_nonan(key);
+        const uint64_t cm = __ballot(has && key == kmax);
+        int wl = (int)__builtin_ctzll(cm);  // winning lane
+        if (__popcll(cm) != 1) {
+            // equal keys: exact float64 maximum among them, then the index rule
+            const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+            const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)xb, wl);
+            const uint32_t hi0 = __builtin_amdgcn_readlane((int)(uint32_t)(xb >> 32), wl);
+            double vmax = __builtin_bit_cast(double, (uint64_t)lo0 | ((uint64_t)hi0 << 32));
+            uint64_t cand = cm;
+            if ((__ballot(x != vmax) & cm) != 0) {
+                const bool in = __builtin_amdgcn_inverse_ballot_w64(cm);
+                vmax = wave_allreduce(in ? x : -INFINITY, [](double a, double b) { return a > b ? a : b; });
+                cand = __ballot(x == vmax) & cm;
             }
-            v[CAP - 1] = -INFINITY;
+            const bool cb = __builtin_amdgcn_inverse_ballot_w64(cand);
+            const int win = HIGHER_TIES ? wave_max_i32(cb ? id[0] : -1) : -wave_max_i32(cb ? -id[0] : -0x7fffffff);
+            wl = (int)__builtin_ctzll(__ballot(has && id[0] == win));
+        }
+        const int win = __builtin_amdgcn_readlane(id[0], wl);
+        if (lane == 0) out[k] = win;
+        if (lane == wl) {
+#pragma unroll
+            for (int c = 0; c + 1 < CAP; ++c) id[c] = id[c + 1];
             id[CAP - 1] = -1;
         }
     }
@@ -377,11 +399,13 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
                 for (int l = 0; l < L; ++l) {
                     const double b = (l < eff ? t0[l * slice + j] : 0.0) * pr;
                     sum = l == 0 ? b : sum + b;
-                    bb[j * bs3 + l] = __float2half((float)b);
+                    if (!(ASG_REAL_PROF_SKIP & 2)) bb[j * bs3 + l] = __float2half((float)b);
                 }
                 trow[j] = sum;
-                ab[j * as3] = 1;
-                if (step) ob[j * os3] = (int16_t)(pa == j);
+                if (!(ASG_REAL_PROF_SKIP & 2)) {
+                    ab[j * as3] = 1;
+                    if (step) ob[j * os3] = (int16_t)(pa == j);
+                }
             }
         } else {
             for (int j = lane; j < m; j += 64) {
@@ -417,6 +441,13 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
     for (int r = wave; r < rows; r += waves) {
         const double *vals = tl + (int64_t)r * m;
         const int a = i0 + r;
+        if (ASG_REAL_PROF_SKIP & 1) {  // profiling: valid placeholder lists (tasks 0..)
+            for (int c = lane; c < MD; c += 64) {
+                if (c < M) st.topA[(e * n + a) * (int64_t)M + c] = c;
+                st.topD[(e * n + a) * (int64_t)MD + c] = c;
+            }
+            continue;
+        }
         wave_topk<CAP, false>(vals, m, M, st.topA + (e * n + a) * (int64_t)M, taken);
         wave_topk<CAP, true>(vals, m, MD, st.topD + (e * n + a) * (int64_t)MD, taken);
     }
@@ -462,7 +493,7 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     const double *totT = st.totT + e * (int64_t)n * m;
     for (int a = lane; a < n; a += 64) {
         double b = totT[(int64_t)top[0] * n + a];
-        for (int c = 1; c < M; ++c) {
+        for (int c = 1; c < ((ASG_REAL_PROF_SKIP & 4) ? 1 : M); ++c) {
             const double v = totT[(int64_t)top[c] * n + a];
             b = v > b ? v : b;
         }
@@ -471,7 +502,12 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     }
     wave_sync();
     // (c) the N strongest competitors (np.argsort(-best)[:N])
-    wave_topk<CAP, false>(best, n, N, topn, taken);
+    if (!(ASG_REAL_PROF_SKIP & 8)) {
+        wave_topk<CAP, false>(best, n, N, topn, taken);
+    } else {  // profiling: valid placeholder competitors (agents 0..)
+        for (int c = lane; c < N; c += 64) topn[c] = c;
+        wave_sync();
+    }
     // (d) competitor q's M/2 best tasks outside agent i's top M: the first M/2 entries of
     //     its topD list not in top[], stored ascending (largest picked first)
     for (int q = lane; q < N; q += 64) {
@@ -514,7 +550,7 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
         }
         store_real(bv.obs, o0 + p, real_beta(st, tab, knew, a, j, l));
     };
-    for (int p = lane; p < osz; p += 64) {
+    for (int p = lane; p < ((ASG_REAL_PROF_SKIP & 16) ? 0 : osz); p += 64) {
         if (p < r1) {
             bval(i, top[p / L], p % L, p);
         } else if (p < r2) {

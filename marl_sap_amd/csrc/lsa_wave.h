@@ -75,72 +75,6 @@ __device__ int lsa_stage_regs(const IT *C, int64_t rs, int64_t cs, int nr0, int 
     return wave_or_i32(bad) ? ASG_E_LSA_INVALID : ASG_OK;
 }
 
-// wave64 minimum of a float32 that is never NaN, returned wave-uniform (SGPR): one block
-// of DPP-fused v_min_f32 (fminf on DPP operands would add a canonicalising v_max per
-// step) -- 4 steps inside each 16-lane row, then row_bcast:15 / row_bcast:31 fold the rows
-// into lane 63.  s_nop 1 covers the VALU-write -> DPP-read hazard.  Call in wave-uniform
-// control flow.
-__device__ __forceinline__ float wave_min_f32_nonan(float x) {
-#ifndef ASG_LSA_PERMLANE_MIN
-    asm("s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc"
-        : "+v"(x));
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
-#else
-    float y, t;
-    asm("s_nop 1\n\t"
-        "v_min_f32_dpp %0, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "v_mov_b32 %1, %0\n\t"
-        "s_nop 1\n\t"
-        "v_permlane16_swap_b32 %0, %1\n\t"
-        "v_min_f32 %0, %0, %1\n\t"
-        "v_mov_b32 %1, %0\n\t"
-        "s_nop 1\n\t"
-        "v_permlane32_swap_b32 %0, %1\n\t"
-        "v_min_f32 %0, %0, %1"
-        : "=&v"(y), "=&v"(t)
-        : "v"(x));
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, y)));
-#endif
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    return wave_allreduce(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
-}
-// wave64 maximum of a uint32, returned wave-uniform: the row_bcast fold of
-// wave_min_f32_nonan with v_max_u32
-__device__ __forceinline__ uint32_t wave_max_u32_bcast(uint32_t x) {
-    asm("s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
-        "s_nop 1\n\t"
-        "v_max_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc"
-        : "+v"(x));
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
 // Solve on the working matrix acc(i, j), i < nr <= nc <= 64*CPL (scipy's orientation).
 // All per-row and per-column state lives in registers, distributed over the lanes
 // (column j / row r in lane j%64, slot j/64); only the cost matrix may be in memory.
