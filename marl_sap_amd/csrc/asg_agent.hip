@@ -37,6 +37,25 @@ constexpr int kRowsPerWave = 16 * kNT;
 #endif
 constexpr int kHid = 64;          // hidden_dim
 
+// ASG_AGENT_STAMPS (profiling builds only): s_memtime at the phase boundaries of the
+// first tiles of workgroup 0's waves, read back with asg_debug_agent_stamps()
+#ifdef ASG_AGENT_STAMPS
+__device__ unsigned long long g_agent_stamps[16][4][8];  // [wave][tile][stamp]
+__device__ int g_agent_tile[16];
+#define ASG_STAMP(k)                                                                                     \
+    do {                                                                                                 \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                                \
+            const int w_ = threadIdx.x >> 6, t_ = g_agent_tile[w_];                                      \
+            if (t_ < 4) g_agent_stamps[w_][t_][k] = __builtin_amdgcn_s_memtime();                       \
+            if (k == 7) g_agent_tile[w_] = t_ + 1;                                                        \
+        }                                                                                                \
+    } while (0)
+#else
+#define ASG_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -120,6 +139,7 @@ __device__ __forceinline__ void agent_rows(
         ok[nt] = rows[nt] < R;
     }
 
+    ASG_STAMP(0);
     // ---- h_in fragments (B operand of W_hh, and h of the GRU update): issued before fc1 so
     // they arrive under its MFMAs (issued after it, every tile's GRU waited on them) -------
     float4 hB[4][kNT];
@@ -234,10 +254,12 @@ __device__ __forceinline__ void agent_rows(
                 for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v], 0.f);
     }
 
+    ASG_STAMP(1);
     // ---- recurrent layer -> h'^T in registers (hp[hb] = B operand of fc2's chunk hb) ----
     f32x4 hp[4][kNT];
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb) {
+        if (hb > 0) ASG_STAMP(3 + hb);
         if (RNN) {
             // gate pre-activations: r and z sum the input and hidden products in one
             // accumulator; n keeps them apart (n = tanh(i_n + r * h_n))
@@ -314,6 +336,7 @@ __device__ __forceinline__ void agent_rows(
                     make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
     }
 
+    ASG_STAMP(2);
     // ---- selection state: (env, agent) of each row, running argmax, availability bits ----
     const uint8_t *arow[kNT];
     bool av4 = false;
@@ -422,7 +445,11 @@ __device__ __forceinline__ void agent_rows(
             }
         }
     }
-    if (!SEL) return;
+    ASG_STAMP(3);
+    if (!SEL) {
+        ASG_STAMP(7);
+        return;
+    }
 
     // ---- reduce each row over its 4 lanes (q = 0..3: lane ^ 16, lane ^ 32) -------------
 #pragma unroll
@@ -506,6 +533,7 @@ __device__ __forceinline__ void agent_rows(
         if (found >= 0) action = found;
     }
     if (q < kNT && ok[nt]) sel.out[oidx[nt]] = action;
+    ASG_STAMP(7);
 }
 
 // One wave per 32 rows, weights read through L1/L2 (any n_out).
@@ -653,3 +681,13 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 }
 
 }  // namespace asg
+
+#ifdef ASG_AGENT_STAMPS
+// profiling builds: copy the stamps out (uint64 [16][4][8]) and re-arm
+extern "C" int asg_debug_agent_stamps(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(asg::g_agent_stamps), sizeof(asg::g_agent_stamps)) != hipSuccess) return -2;
+    static const int zero[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(asg::g_agent_tile), zero, sizeof(zero)) != hipSuccess) return -2;
+    return 0;
+}
+#endif

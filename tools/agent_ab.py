@@ -37,6 +37,26 @@ def main(E=16384, n=64, m=64, K=256, rounds=7, iters=30):
             torch.cuda.synchronize()
             if r:
                 res.append(a.elapsed_time(b) / iters)
+    if os.environ.get("ASG_AB_STAMPS"):  # profiling build: phase stamps of workgroup 0's waves
+        import ctypes
+        import numpy as np
+        from marl_sap_amd import _lib
+        L = _lib.lib()
+        buf = np.zeros((16, 4, 8), dtype=np.uint64)
+        L.asg_debug_agent_stamps(buf.ctypes.data_as(ctypes.c_void_p))  # re-arm
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            e, s_, c, st = sel.fused_params(0, False, dev)
+            fused.forward_select(x, h, avail, n, e, s_, c, out, st)
+        torch.cuda.synchronize()
+        L.asg_debug_agent_stamps(buf.ctypes.data_as(ctypes.c_void_p))
+        order = [0, 1, 4, 5, 6, 2, 3, 7]
+        names = ["fc1", "gru0", "gru1", "gru2", "gru3", "fc2", "select"]
+        d = buf[:8, 1:4, :].astype(np.int64)  # waves 0-7, tiles 1-3 (steady state)
+        phases = np.stack([d[..., order[k + 1]] - d[..., order[k]] for k in range(7)], axis=-1)
+        med = np.median(phases.reshape(-1, 7), axis=0)
+        print("stamps (s_memtime ticks, median over waves 0-7 x tiles 1-3):",
+              {nm: int(v) for nm, v in zip(names, med)}, "tile total", int(med.sum()), flush=True)
     res.sort()
     print(f"{os.environ.get('ASG_LIB_PATH', 'default')} l2x={bool(os.environ.get('ASG_AB_L2X'))} K={K} m={m} median {res[len(res) // 2]:.4f} ms "
           f"min {res[0]:.4f}", flush=True)
