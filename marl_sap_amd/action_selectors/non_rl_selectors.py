@@ -51,7 +51,14 @@ def haa_select_batched(beta, prev, lambda_, T_trans=None, return_status=False):
         beta = beta.float()
     if prev.dtype != torch.int64:
         prev = prev.long()
-    tt_dev = None if T_trans is None else torch.as_tensor(T_trans, dtype=torch.float64).to(beta.device).contiguous()
+    tt_dev = None
+    if T_trans is not None:
+        tt_dev = torch.as_tensor(T_trans, dtype=torch.float64).to(beta.device).contiguous()
+        if tt_dev.shape != (m, m):
+            raise ValueError(f"T_trans must be [{m}, {m}], got {list(tt_dev.shape)}")
+        if not bool(torch.isfinite(tt_dev).all()):
+            # beta_hat would hold NaN / inf entries: scipy's error for the LSA on it
+            raise ValueError("matrix contains invalid numeric entries")
     out = torch.empty((B, n), dtype=torch.float32, device=beta.device)
     status = torch.empty((B,), dtype=torch.int32, device=beta.device)
     with torch.cuda.device(beta.device):

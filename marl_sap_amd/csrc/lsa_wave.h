@@ -140,6 +140,7 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
                 cmsk[c] = __ballot(key[c] == kmin);
                 total += __popcll(cmsk[c]);
             }
+            if (total == 0) return ASG_E_LSA_INVALID;  // NaN keys (see lsa_solve_reg64)
             // first candidate (the selection when it is the only one)
             int src0 = 0, c0 = 0;
 #pragma unroll
@@ -299,6 +300,9 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             const float key = remb ? (float)spc : kInfF;
             const float kmin = wave_min_f32_nonan(key);
             const uint64_t cm = __ballot(key == kmin) & rem;
+            // no candidate only if a cost turned NaN during the solve (e.g. a NaN T_trans
+            // entry under HAA): scipy's "invalid numeric entries", never an endless loop
+            if (cm == 0) return ASG_E_LSA_INVALID;
             const int src0 = (int)__builtin_ctzll(cm);
             const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
             const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);

@@ -149,6 +149,33 @@ def test_haa_select_vs_oracle(n, m, custom_T):
         assert np.array_equal(out[b], ora.lsa(bh, maximize=True)[1].astype(np.float32)), b
 
 
+def test_haa_non_finite_transition_matrix():
+    """A NaN T_trans entry makes beta_hat invalid (scipy raises); the host check raises the
+    same ValueError, and the kernel itself, fed the NaN directly through the ABI, still
+    terminates with a per-env status (the solver's guard against NaN-only candidates)."""
+    import ctypes
+
+    from marl_sap_amd import _lib
+    from marl_sap_amd.action_selectors.non_rl_selectors import haa_select_batched
+    B, n, m = 8, 6, 8
+    rng = np.random.RandomState(7)
+    beta = torch.as_tensor(rng.uniform(0.0, 1.0, size=(B, n, m)).astype(np.float32), device=DEV)
+    prev = torch.as_tensor(rng.randint(0, m, size=(B, n)), device=DEV)
+    tt = np.ones((m, m)) - np.eye(m)
+    tt[:, 3] = np.nan
+    with pytest.raises(ValueError, match="invalid numeric entries"):
+        haa_select_batched(beta, prev, 0.5, tt)
+    tt_dev = torch.as_tensor(tt, device=DEV)
+    out = torch.empty((B, n), dtype=torch.float32, device=DEV)
+    status = torch.empty((B,), dtype=torch.int32, device=DEV)
+    _lib.check(_lib.lib().asg_haa_select(
+        ctypes.c_void_p(beta.data_ptr()), _lib.i64arr(beta.stride()), ctypes.c_void_p(prev.data_ptr()),
+        _lib.i64arr(prev.stride()), B, n, m, ctypes.c_void_p(tt_dev.data_ptr()), 0.5,
+        ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(DEV)))
+    torch.cuda.synchronize()
+    assert set(status.cpu().tolist()) <= {0, -4}
+
+
 class _DictBatch:
     def __init__(self, d):
         self.d = d
