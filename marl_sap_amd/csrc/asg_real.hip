@@ -166,7 +166,10 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
         const double x = has ? vals[id[0]] : -INFINITY;
         const float key = has ? (float)x : -INFINITY;
         const float kmax = wave_max_f32_nonan(key);
-        const uint64_t cm = __ballot(has && key == kmax);
+        uint64_t cm = __ballot(has && key == kmax);
+        // NaN totals (an injected NaN benefit) match no key: rank them last, by index, so
+        // every pick stays a valid task index
+        if (cm == 0) cm = __ballot(has);
         int wl = (int)__builtin_ctzll(cm);  // winning lane
         if (__popcll(cm) != 1) {
             // equal keys: exact float64 maximum among them, then the index rule
@@ -180,6 +183,7 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
                 vmax = wave_allreduce(in ? x : -INFINITY, [](double a, double b) { return a > b ? a : b; });
                 cand = __ballot(x == vmax) & cm;
             }
+            if (cand == 0) cand = cm;  // NaN maximum: the index rule over all candidates
             const bool cb = __builtin_amdgcn_inverse_ballot_w64(cand);
             const int win = HIGHER_TIES ? wave_max_i32(cb ? id[0] : -1) : -wave_max_i32(cb ? -id[0] : -0x7fffffff);
             wl = (int)__builtin_ctzll(__ballot(has && id[0] == win));

@@ -94,6 +94,25 @@ def test_real_env_matches_oracle_per_env_tables(oracle, n, m, T, L, N, M, sparse
     env.sync()
 
 
+def test_real_env_nan_benefits_stay_in_bounds():
+    """NaN entries in an injected benefit table (the reference's argsort would rank them
+    last): every ranking pick must still be a valid task / agent index, so the observation
+    pass reads in bounds and the rollout completes."""
+    E, n, m, T, L, N, M = 3, 12, 20, 4, 2, 4, 4
+    rng = np.random.RandomState(11)
+    tables = rng.uniform(0.0, 1.0, size=(E, n, m, T))
+    tables[:, :, ::3] = np.nan          # a third of the tasks NaN for every agent
+    tables[1] = np.nan                  # one env entirely NaN
+    env = RealAssignEnvBatch(1, n, m, T, N, M, L, 0.5, sat_prox_mat=tables, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    for t in range(T):
+        b["actions"][:, t, :, 0] = torch.from_numpy(rng.randint(0, m, size=(E, n))).to(torch.int16).to(DEV)
+        env.step(b, t)
+    env.sync()
+    assert b["obs"].shape[0] == E
+
+
 def test_real_env_errors():
     tab = np.ones((4, 6, 3))
     with pytest.raises(ValueError):
