@@ -611,6 +611,24 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     return hipGetLastError();
 }
 
+// CUs a stream may run on (hipExtStreamCreateWithCUMask): the persistent grid is sized to
+// them, so a CU-masked agent stream leaves the other CUs to a concurrent env-step stream.
+static int stream_cus(hipStream_t s, int ncu) {
+    static thread_local hipStream_t last = nullptr;
+    static thread_local int last_n = 0;
+    if (!s) return ncu;
+    if (s == last && last_n > 0) return last_n < ncu ? last_n : ncu;
+    uint32_t mask[32] = {0};
+    int n = 0;
+    if (hipExtStreamGetCUMask(s, 32, mask) == hipSuccess)
+        for (int i = 0; i < 32; ++i) n += __builtin_popcount(mask[i]);
+    else
+        (void)hipGetLastError();
+    last = s;
+    last_n = n > 0 ? n : ncu;
+    return last_n < ncu ? last_n : ncu;
+}
+
 // ASG_AGENT_LDS_WEIGHTS=0 selects the L2-weight kernel (A/B experiments)
 static bool use_lds_weights() {
     static const int v = [] {
@@ -639,6 +657,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     if (use_lds_weights() && lds <= 160 * 1024) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        ncu = stream_cus(s, ncu);
         const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
 #define LL_(RNN, SEL, GEN)                                                                                   \
