@@ -46,10 +46,12 @@ def step_bytes(n, m, L):
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (= f32 vector peak; MI355X_MICROARCH.md)
 
 
-def agent_flops(n, m, L, hidden=64, use_rnn=True):
+def agent_flops(n, m, L, hidden=64, use_rnn=True, onehot=True):
     """Algorithmic flops of one agent row: fc1 (m(L+1) -> hidden), GRUCell (two hidden x
-    3*hidden products), fc2 (hidden -> m); 2 flops per multiply-add."""
-    K = m * (L + 1)
+    3*hidden products), fc2 (hidden -> m); 2 flops per multiply-add.  onehot: the obs
+    one-hot block (the first m inputs) is a column gather of W1, not m*hidden products
+    (the fused kernel's one-hot prefix, ASG_AGENT_ONEHOT), so fc1 counts K - m inputs."""
+    K = m * (L + 1) - (m if onehot else 0)
     rec = 2 * 3 * hidden * hidden if use_rnn else hidden * hidden
     return 2 * (K * hidden + rec + hidden * m)
 
@@ -60,7 +62,8 @@ def agent_roofline(a, E, sel_ms):
     peak: the kernel that takes most of each step's time next to the env step."""
     if a.selector == "random" or sel_ms <= 0:
         return None
-    flops = agent_flops(a.n, a.m, a.L) * E * a.n
+    onehot = a.agent == "rnn_fused" and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
+    flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
     tfs = flops / (sel_ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
             "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "traffic": None,

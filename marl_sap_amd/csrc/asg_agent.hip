@@ -128,7 +128,7 @@ __device__ __forceinline__ void agent_rows(
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
-    float *__restrict__ Q, const SelectArgs &sel) {
+    float *__restrict__ Q, const SelectArgs &sel, const float *__restrict__ W1T, int P) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= R) return;  // whole wave idle
     int64_t rows[kNT];
@@ -231,9 +231,66 @@ __device__ __forceinline__ void agent_rows(
         } else
 #endif
         {
-            load(0, aA, wA);
-            if (nk > 1) load(1, aB, wB);
-            for (int t = 0; t < nk; ++t) {
+            // one-hot prefix (onehot_prefix): when every row of the tile holds at most one
+            // nonzero in its first P inputs and that entry is exactly 1 (the mock env's
+            // onehot(previous task), or zeros at t = 0), those P / 16 chunks contribute
+            // W1[:, a] -- added from W1^T -- and their MFMAs are skipped; any other input
+            // (checked per tile) runs the full MFMA loop.
+            int t0 = 0;
+            if (!GEN && P > 0) {
+                int pos[kNT];
+                bool bad = false;
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) pos[nt] = -1;
+                for (int t4 = 0; t4 < P / 16; t4 += 4) {  // P % 64 == 0 or P / 16 < 4: guarded
+                    float4 pa[4][kNT];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt)
+                            pa[c][nt] = (t4 + c < P / 16)
+                                            ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const float v = comp(pa[c][nt], e);
+                                const bool one = v == 1.0f;
+                                bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
+                                pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
+                            }
+                }
+                bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) {
+                    const uint64_t mk = __ballot(pos[nt] >= 0);
+                    const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull,
+                                   g3 = mk >> 48;
+                    rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
+                }
+                if (rows_ok && __ballot(bad) == 0) {
+                    t0 = P / 16;
+#pragma unroll
+                    for (int nt = 0; nt < kNT; ++nt) {
+                        int a = pos[nt];
+                        a = max(a, __shfl_xor(a, 16));
+                        a = max(a, __shfl_xor(a, 32));
+                        if (a >= 0) {
+#pragma unroll
+                            for (int mt = 0; mt < 4; ++mt) {
+                                const float4 w = *reinterpret_cast<const float4 *>(W1T + a * kHid + 16 * mt + 4 * q);
+                                acc[mt][nt] += f32x4{w.x, w.y, w.z, w.w};
+                            }
+                        }
+                    }
+                }
+            }
+            load(t0, aA, wA);
+            if (nk > t0 + 1) load(t0 + 1, aB, wB);
+            for (int t = t0; t < nk; ++t) {
                 float4 a4[kNT];
 #pragma unroll
                 for (int i = 0; i < kNT; ++i) a4[i] = aA[i];
@@ -543,9 +600,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AG
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
-    float *__restrict__ Q, SelectArgs sel) {
+    float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1T, int P) {
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
-    agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel);
+    agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel,
+                              W1T, P);
 }
 
 // Persistent variant: one 512-thread workgroup per CU copies the recurrent and output
@@ -570,26 +628,43 @@ rnn_agent_lds_kernel(
     const float *__restrict__ X, int64_t xs, int64_t R, int K, const float *__restrict__ Hin, int64_t hs,
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
     const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,
-    float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel) {
+    float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1Tg, int P,
+    int64_t w1t_lds) {
     extern __shared__ float4 s_w[];
     for (int64_t i = threadIdx.x; i < nrf4; i += blockDim.x) s_w[i] = Wrp[i];
     __syncthreads();
     const float4 *Wih = s_w;
     const float4 *Whh = s_w + (RNN ? 4 * 12 * 64 : 4 * 4 * 64);
     const float4 *W2 = RNN ? Whh + 4 * 12 * 64 : Whh;
+    // W1^T of the one-hot prefix: staged with the other weights when it fit (w1t_lds >= 0)
+    const float *W1T = w1t_lds >= 0 ? reinterpret_cast<const float *>(s_w + w1t_lds) : W1Tg;
     const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
-        agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel);
+        agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel,
+                                  W1T, P);
     }
 }
+
+// One-hot input prefix: the first P = n_out inputs may be a one-hot block (the mock env's
+// obs starts with onehot(previous task), mock_constellation_env.py:141-152).  The pack adds
+// W1^T of those P columns ([P][64], one float4 per 4 hidden units), and a wave tile whose
+// prefix rows are verified one-hot (or zero) adds W1[:, a] instead of running the prefix
+// chunks' MFMAs.  P = 0 (no section) unless n_out % 16 == 0 and n_out < K.
+static int onehot_prefix(int K, int nout) { return (nout % 16 == 0 && nout < K && K % 32 == 0) ? nout : 0; }
 
 // float4 count of the packed weight buffer
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
     const int64_t w1 = (int64_t)((K + 15) / 16) * 4 * 64;
     const int64_t wr = use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64;
     const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
-    return w1 + wr + w2;
+    const int64_t w1t = (int64_t)onehot_prefix(K, nout) * 16;
+    return w1 + wr + w2 + w1t;
+}
+
+__global__ void pack_w1t_kernel(const float *W1, int K, int P, float *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // out[a][u] = W1[u][a]
+    if (i < P * kHid) out[i] = W1[(int64_t)(i % kHid) * K + i / kHid];
 }
 
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
@@ -608,6 +683,9 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
         one(Wih, kHid, kHid);
     }
     one(W2, nout, kHid);
+    if (const int P = onehot_prefix(K, nout))
+        hipLaunchKernelGGL(pack_w1t_kernel, dim3((P * kHid + 255) / 256), dim3(256), 0, s, W1, K, P,
+                           reinterpret_cast<float *>(p));
     return hipGetLastError();
 }
 
@@ -627,6 +705,15 @@ static int stream_cus(hipStream_t s, int ncu) {
     last = s;
     last_n = n > 0 ? n : ncu;
     return last_n < ncu ? last_n : ncu;
+}
+
+// ASG_AGENT_ONEHOT=0 disables the one-hot prefix shortcut (A/B experiments)
+static bool onehot_prefix_enabled() {
+    static const int v = [] {
+        const char *e = getenv("ASG_AGENT_ONEHOT");
+        return e ? atoi(e) : 1;
+    }();
+    return v != 0;
 }
 
 // ASG_AGENT_LDS_WEIGHTS=0 selects the L2-weight kernel (A/B experiments)
@@ -649,8 +736,16 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     const float4 *Whhp = Wihp + (use_rnn ? 4 * 12 * 64 : 4 * 4 * 64);
     const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
     const SelectArgs sa = sel ? *sel : SelectArgs{};
-    // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU)
-    const int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)((nout + 15) / 16) * 64;
+    const int P = onehot_prefix_enabled() ? onehot_prefix(K, nout) : 0;
+    // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU), then the
+    // one-hot prefix's W1^T when it fits too (else it is read through L2)
+    int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)((nout + 15) / 16) * 64;
+    const float *W1Tg = reinterpret_cast<const float *>(W2p + 4 * (int64_t)((nout + 15) / 16) * 64);
+    int64_t w1t_lds = -1;
+    if (P > 0 && (size_t)(nrf4 + (int64_t)P * 16) * sizeof(float4) <= 160 * 1024) {
+        w1t_lds = nrf4;
+        nrf4 += (int64_t)P * 16;
+    }
     const size_t lds = (size_t)nrf4 * sizeof(float4);
     const bool gen = (K & 31) != 0 || (xs & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 ||
                      nout > 256;
@@ -662,7 +757,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
 #define LL_(RNN, SEL, GEN)                                                                                   \
     hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL, GEN>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, \
-                       Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa)
+                       Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa, W1Tg, P, w1t_lds)
 #define LG_(RNN, SEL) \
     if (gen) LL_(RNN, SEL, true); else LL_(RNN, SEL, false)
         if (use_rnn) {
@@ -676,7 +771,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     }
 #define L_(RNN, SEL, GEN)                                                                                    \
     hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, SEL, GEN>), dim3(blocks), dim3(256), 0, s, X, xs, R, K, Hin, hs, \
-                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa)
+                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa, W1Tg, P)
 #define LG_(RNN, SEL) \
     if (gen) L_(RNN, SEL, true); else L_(RNN, SEL, false)
     if (use_rnn) {

@@ -44,6 +44,42 @@ def test_fused_agent_matches_pytorch(R, K, m, use_rnn, hidden):
     assert q2.requires_grad and torch.equal(q2.detach(), q0)
 
 
+@pytest.mark.parametrize("R,m,L,use_rnn,mode", [
+    (64 * 300, 64, 3, True, "onehot"), (64 * 300 + 40, 64, 3, True, "mixed"), (4096, 64, 3, False, "zeros"),
+    (2048 + 17, 256, 3, True, "onehot"), (1500, 128, 2, True, "mixed"), (999, 32, 4, True, "onehot"),
+    (800, 64, 3, True, "twos")])
+def test_fused_agent_onehot_prefix(R, m, L, use_rnn, mode):
+    """Inputs whose first m entries are onehot(previous task) (the mock env's obs): tiles
+    verified one-hot add W1[:, a] instead of running the prefix MFMAs; tiles with any other
+    prefix (a second 1, a 2, ...) take the full MFMA loop.  Both agree with the PyTorch
+    RNNAgent (ragged row counts, zero rows, the L2-read W1^T at m = 256)."""
+    torch.manual_seed(R + m)
+    K = m * (L + 1)
+    args = SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m)
+    ref = RNNAgent(K, args).to(DEV)
+    fused = RNNFusedAgent(K, args).to(DEV)
+    fused.load_state_dict(ref.state_dict())
+    x = torch.rand((R, K), device=DEV)
+    x[torch.rand((R, K), device=DEV) < 0.7] = 0.0
+    a = torch.randint(0, m, (R,), device=DEV)
+    x[:, :m] = torch.nn.functional.one_hot(a, m).float()
+    if mode == "zeros":
+        x[:, :m] = 0.0
+    elif mode == "mixed":  # every 7th row is zero, rows 5 and 300 carry a second one, row 77 a 0.5
+        x[::7, :m] = 0.0
+        x[5, (a[5] + 1) % m] = 1.0
+        x[min(300, R - 1), (a[min(300, R - 1)] + 3) % m] = 1.0
+        x[77, (a[77] + 2) % m] = 0.5
+    elif mode == "twos":
+        x[::3, :m] *= 2.0
+    h = torch.randn((R, 64), device=DEV) * 0.5
+    with torch.no_grad():
+        q0, h0 = ref(x, h)
+        q1, h1 = fused(x, h)
+    torch.testing.assert_close(h1, h0, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(q1, q0, rtol=1e-5, atol=2e-5)
+
+
 def test_fused_agent_reads_time_major_obs_slab():
     from marl_sap_amd.components import EpisodeBatch
     from marl_sap_amd.envs import AssignEnvBatch
