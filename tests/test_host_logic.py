@@ -133,4 +133,5 @@ def test_bench_accounting():
     import bench
     assert bench.step_bytes(64, 64, 3) == 120073
     assert bench.step_bytes(16, 16, 3) == 16 * 16 * 29 + 16 * 20 + 9
-    assert bench.agent_flops(64, 64, 3) == 90112  # 2 * (256*64 + 2*3*64*64 + 64*64)
+    assert bench.agent_flops(64, 64, 3, onehot=False) == 90112  # 2 * (256*64 + 2*3*64*64 + 64*64)
+    assert bench.agent_flops(64, 64, 3) == 81920  # the one-hot block is a W1 column gather
