@@ -18,6 +18,8 @@
 // hipBLASLt's (and the r/z gates add the input and hidden products in one accumulator).
 // One wave owns 32 agent rows; all activations stay in registers (see the transposed
 // formulation below), weights come from L1/L2 in a pre-packed fragment order.
+#include <type_traits>
+
 #include "asg_device.h"
 #include "asg_internal.h"
 
@@ -313,6 +315,16 @@ __device__ __forceinline__ void agent_rows(
 
     ASG_STAMP(1);
     // ---- recurrent layer -> h'^T in registers (hp[hb] = B operand of fc2's chunk hb) ----
+    bool h_zero = false;
+    if (RNN) {
+        bool nz = false;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt)
+                nz |= (hB[t][nt].x != 0.f) | (hB[t][nt].y != 0.f) | (hB[t][nt].z != 0.f) | (hB[t][nt].w != 0.f);
+        h_zero = __ballot(nz) == 0;
+    }
     f32x4 hp[4][kNT];
 #pragma unroll
     for (int hb = 0; hb < 4; ++hb) {
@@ -338,26 +350,36 @@ __device__ __forceinline__ void agent_rows(
                 gni[nt] = f32x4{bin.x, bin.y, bin.z, bin.w};
                 gnh[nt] = f32x4{bhn.x, bhn.y, bhn.z, bhn.w};
             }
+            // a tile whose h is all zero (BasicMAC.init_hidden at t = 0) skips the W_hh
+            // products (exact zeros): a third of the GRU's MFMAs on those steps
+            auto gates = [&](auto with_h) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                float4 wc[6];
+                for (int t = 0; t < 4; ++t) {
+                    float4 wc[6];
 #pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    wc[g] = Wihp[pk(t, 4 * g + hb, 12, lane)];
-                    wc[3 + g] = Whhp[pk(t, 4 * g + hb, 12, lane)];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int nt = 0; nt < kNT; ++nt) {
-                        gr[nt] = mfma4(comp(wc[0], e), xB[t][nt][e], gr[nt]);
-                        gz[nt] = mfma4(comp(wc[1], e), xB[t][nt][e], gz[nt]);
-                        gni[nt] = mfma4(comp(wc[2], e), xB[t][nt][e], gni[nt]);
-                        gr[nt] = mfma4(comp(wc[3], e), comp(hB[t][nt], e), gr[nt]);
-                        gz[nt] = mfma4(comp(wc[4], e), comp(hB[t][nt], e), gz[nt]);
-                        gnh[nt] = mfma4(comp(wc[5], e), comp(hB[t][nt], e), gnh[nt]);
+                    for (int g = 0; g < 3; ++g) {
+                        wc[g] = Wihp[pk(t, 4 * g + hb, 12, lane)];
+                        if (with_h) wc[3 + g] = Whhp[pk(t, 4 * g + hb, 12, lane)];
                     }
-            }
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt) {
+                            gr[nt] = mfma4(comp(wc[0], e), xB[t][nt][e], gr[nt]);
+                            gz[nt] = mfma4(comp(wc[1], e), xB[t][nt][e], gz[nt]);
+                            gni[nt] = mfma4(comp(wc[2], e), xB[t][nt][e], gni[nt]);
+                            if (with_h) {
+                                gr[nt] = mfma4(comp(wc[3], e), comp(hB[t][nt], e), gr[nt]);
+                                gz[nt] = mfma4(comp(wc[4], e), comp(hB[t][nt], e), gz[nt]);
+                                gnh[nt] = mfma4(comp(wc[5], e), comp(hB[t][nt], e), gnh[nt]);
+                            }
+                        }
+                }
+            };
+            if (h_zero)
+                gates(std::false_type{});
+            else
+                gates(std::true_type{});
 #pragma unroll
             for (int nt = 0; nt < kNT; ++nt)
 #pragma unroll
