@@ -62,6 +62,65 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// GRU products on bf16 MFMAs with a three-way operand split (ASG_AGENT_GRU_X3, default on):
+// an f32 x is truncated into hi + mid + lo bf16 parts with x == hi + mid + lo exactly (each
+// residual is exact and fits 8 significant bits), and x . w is summed from the six cross
+// products down to 2^-16 relative (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid): the
+// dropped terms are below 2^-22 relative, so the gates match the fp32 module to ~1e-7.
+// Each bf16 MFMA covers 32 k at 16 cycles, the f32 MFMA 4 k at 32 cycles: 6 bf16 vs 8 f32
+// MFMAs per 32-deep k-slice = 2.7x less matrix-pipe time.  Non-finite inputs come out NaN.
+#ifndef ASG_AGENT_GRU_X3
+#define ASG_AGENT_GRU_X3 1
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// packed W_ih / W_hh: [gate 3][slab hb 4][k-slice 2][plane 3][lane 64] x 8 bf16
+constexpr int kGruX3F4 = 3 * 4 * 2 * 3 * 64;
+// float4 count of one packed GRU matrix (W_ih or W_hh)
+constexpr int kGruF4 = ASG_AGENT_GRU_X3 ? kGruX3F4 : 4 * 12 * 64;
+__device__ __forceinline__ int gru_x3_idx(int g, int hb, int s, int plane, int lane) {
+    return (((g * 4 + hb) * 2 + s) * 3 + plane) * 64 + lane;
+}
+// the k of element j in lane quad q of k-slice s: the f32 accumulator layout of the layer
+// before (units 4q + v of tiles 2s and 2s + 1), so activations feed the MFMA in place
+__device__ __forceinline__ int gru_x3_k(int s, int q, int j) { return 32 * s + (j < 4 ? 4 * q + j : 16 + 4 * q + j - 4); }
+
+__device__ __forceinline__ f32x4 mfma_bf16(const u32x4v &a, const u32x4v &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+// 8 f32 -> three bf16x8 planes (element j in half j & 1 of dword j >> 1)
+__device__ __forceinline__ void split3(const float (&x)[8], u32x4v &h, u32x4v &m, u32x4v &l) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t xa = __builtin_bit_cast(uint32_t, x[2 * p]), xb = __builtin_bit_cast(uint32_t, x[2 * p + 1]);
+        const float ra = x[2 * p] - __builtin_bit_cast(float, xa & 0xffff0000u);
+        const float rb = x[2 * p + 1] - __builtin_bit_cast(float, xb & 0xffff0000u);
+        const uint32_t ua = __builtin_bit_cast(uint32_t, ra), ub = __builtin_bit_cast(uint32_t, rb);
+        const float sa = ra - __builtin_bit_cast(float, ua & 0xffff0000u);
+        const float sb = rb - __builtin_bit_cast(float, ub & 0xffff0000u);
+        h[p] = (xa >> 16) | (xb & 0xffff0000u);
+        m[p] = (ua >> 16) | (ub & 0xffff0000u);
+        l[p] = (__builtin_bit_cast(uint32_t, sa) >> 16) | (__builtin_bit_cast(uint32_t, sb) & 0xffff0000u);
+    }
+}
+// element j of the split back to f32 (exact)
+__device__ __forceinline__ float join3(const u32x4v &h, const u32x4v &m, const u32x4v &l, int j) {
+    const int sh = (j & 1) ? 0 : 16;
+    auto part = [&](const u32x4v &v) { return __builtin_bit_cast(float, (v[j >> 1] << sh) & 0xffff0000u); };
+    return (part(h) + part(m)) + part(l);
+}
+// sum of the six significant cross products of (wh, wm, wl) . (xh, xm, xl)
+__device__ __forceinline__ f32x4 mfma_x3(const u32x4v (&w)[3], const u32x4v (&x)[3], f32x4 c) {
+    c = mfma_bf16(w[0], x[0], c);
+    c = mfma_bf16(w[0], x[1], c);
+    c = mfma_bf16(w[1], x[0], c);
+    c = mfma_bf16(w[0], x[2], c);
+    c = mfma_bf16(w[2], x[0], c);
+    c = mfma_bf16(w[1], x[1], c);
+    return c;
+}
+
 __device__ __forceinline__ float4 ldg4(const float *p, bool ok) {
     return ok ? *reinterpret_cast<const float4 *>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
@@ -352,6 +411,46 @@ __device__ __forceinline__ void agent_rows(
             }
             // a tile whose h is all zero (BasicMAC.init_hidden at t = 0) skips the W_hh
             // products (exact zeros): a third of the GRU's MFMAs on those steps
+#if ASG_AGENT_GRU_X3
+            const u32x4v *Wih3 = reinterpret_cast<const u32x4v *>(Wihp);
+            const u32x4v *Whh3 = reinterpret_cast<const u32x4v *>(Whhp);
+            auto gates = [&](auto with_h) {
+#pragma unroll
+                for (int sl = 0; sl < 2; ++sl) {
+                    // k-slice sl = f32 chunks 2 sl and 2 sl + 1 of x (then h), split per use
+                    // and the input and hidden products one after the other: registers, not
+                    // VALU, are the scarce resource at two waves per SIMD
+#pragma unroll
+                    for (int src = 0; src < (with_h ? 2 : 1); ++src) {
+                        u32x4v a3[kNT][3];
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt) {
+                            float v8[8];
+#pragma unroll
+                            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                                for (int v = 0; v < 4; ++v)
+                                    v8[4 * c + v] = src == 0 ? xB[2 * sl + c][nt][v] : comp(hB[2 * sl + c][nt], v);
+                            split3(v8, a3[nt][0], a3[nt][1], a3[nt][2]);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);  // keep the weight reads of
+                        // later slices from being hoisted here (register pressure)
+                        const u32x4v *W3 = src == 0 ? Wih3 : Whh3;
+#pragma unroll
+                        for (int g = 0; g < 3; ++g) {
+                            u32x4v w3[3];
+#pragma unroll
+                            for (int pl = 0; pl < 3; ++pl) w3[pl] = W3[gru_x3_idx(g, hb, sl, pl, lane)];
+#pragma unroll
+                            for (int nt = 0; nt < kNT; ++nt) {
+                                f32x4 &acc = g == 0 ? gr[nt] : (g == 1 ? gz[nt] : (src == 0 ? gni[nt] : gnh[nt]));
+                                acc = mfma_x3(w3, a3[nt], acc);
+                            }
+                        }
+                    }
+                }
+            };
+#else
             auto gates = [&](auto with_h) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -376,6 +475,7 @@ __device__ __forceinline__ void agent_rows(
                         }
                 }
             };
+#endif
             if (h_zero)
                 gates(std::false_type{});
             else
@@ -387,7 +487,8 @@ __device__ __forceinline__ void agent_rows(
                     const float rg = sigmoidf_(gr[nt][v]);
                     const float zg = sigmoidf_(gz[nt][v]);
                     const float ng = tanhf_(gni[nt][v] + rg * gnh[nt][v]);
-                    hp[hb][nt][v] = ng + zg * (comp(hB[hb][nt], v) - ng);
+                    const float hv = comp(hB[hb][nt], v);
+                    hp[hb][nt][v] = ng + zg * (hv - ng);
                 }
         } else {
             const float4 bb = *reinterpret_cast<const float4 *>(bih + 16 * hb + 4 * q);
@@ -651,13 +752,14 @@ rnn_agent_lds_kernel(
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
     const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,
     float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1Tg, int P,
-    int64_t w1t_lds) {
+    int64_t wr_f4, int64_t w2_lds, int64_t w1t_lds) {
     extern __shared__ float4 s_w[];
     for (int64_t i = threadIdx.x; i < nrf4; i += blockDim.x) s_w[i] = Wrp[i];
     __syncthreads();
     const float4 *Wih = s_w;
-    const float4 *Whh = s_w + (RNN ? 4 * 12 * 64 : 4 * 4 * 64);
-    const float4 *W2 = RNN ? Whh + 4 * 12 * 64 : Whh;
+    const float4 *Whh = s_w + (RNN ? kGruF4 : 0);
+    // W2 staged after the recurrent weights when it fit (w2_lds >= 0), else read through L2
+    const float4 *W2 = w2_lds >= 0 ? s_w + w2_lds : Wrp + wr_f4;
     // W1^T of the one-hot prefix: staged with the other weights when it fit (w1t_lds >= 0)
     const float *W1T = w1t_lds >= 0 ? reinterpret_cast<const float *>(s_w + w1t_lds) : W1Tg;
     const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
@@ -678,10 +780,25 @@ static int onehot_prefix(int K, int nout) { return (nout % 16 == 0 && nout < K &
 // float4 count of the packed weight buffer
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
     const int64_t w1 = (int64_t)((K + 15) / 16) * 4 * 64;
-    const int64_t wr = use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64;
+    const int64_t wr = use_rnn ? 2 * kGruF4 : 4 * 4 * 64;
     const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
     const int64_t w1t = (int64_t)onehot_prefix(K, nout) * 16;
     return w1 + wr + w2 + w1t;
+}
+
+// W_ih / W_hh [3 * 64][64] -> kGruX3F4 x 8 bf16 (gru_x3_idx order, k order gru_x3_k)
+__global__ void pack_gru_x3_kernel(const float *W, u32x4v *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kGruX3F4) return;
+    const int lane = i & 63, pl = (i >> 6) % 3, sl = (i / (64 * 3)) & 1, hb = (i / (64 * 3 * 2)) & 3,
+              g = i / (64 * 3 * 2 * 4);
+    const int row = g * kHid + 16 * hb + (lane & 15), q = lane >> 4;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = W[(int64_t)row * kHid + gru_x3_k(sl, q, j)];
+    u32x4v h, m, l;
+    split3(x, h, m, l);
+    out[i] = pl == 0 ? h : (pl == 1 ? m : l);
 }
 
 __global__ void pack_w1t_kernel(const float *W1, int K, int P, float *out) {
@@ -699,8 +816,16 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     };
     one(W1, kHid, K);
     if (use_rnn) {
+#if ASG_AGENT_GRU_X3
+        for (const float *W : {Wih, Whh}) {
+            hipLaunchKernelGGL(pack_gru_x3_kernel, dim3((kGruX3F4 + 255) / 256), dim3(256), 0, s, W,
+                               reinterpret_cast<u32x4v *>(p));
+            p += kGruX3F4;
+        }
+#else
         one(Wih, 3 * kHid, kHid);
         one(Whh, 3 * kHid, kHid);
+#endif
     } else {
         one(Wih, kHid, kHid);
     }
@@ -755,18 +880,24 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
     const float4 *W1p = packed;
     const float4 *Wihp = W1p + (int64_t)((K + 15) / 16) * 4 * 64;
-    const float4 *Whhp = Wihp + (use_rnn ? 4 * 12 * 64 : 4 * 4 * 64);
-    const float4 *W2p = use_rnn ? Whhp + 4 * 12 * 64 : Whhp;
+    const int64_t wr_f4 = use_rnn ? 2 * kGruF4 : 4 * 4 * 64;
+    const int64_t w2_f4 = 4 * (int64_t)((nout + 15) / 16) * 64;
+    const float4 *Whhp = Wihp + (use_rnn ? kGruF4 : 4 * 4 * 64);
+    const float4 *W2p = Wihp + wr_f4;
     const SelectArgs sa = sel ? *sel : SelectArgs{};
     const int P = onehot_prefix_enabled() ? onehot_prefix(K, nout) : 0;
-    // recurrent + output weights in LDS when they fit (n_out <= 64 with the GRU), then the
-    // one-hot prefix's W1^T when it fits too (else it is read through L2)
-    int64_t nrf4 = (int64_t)(use_rnn ? 2 * 4 * 12 * 64 : 4 * 4 * 64) + 4 * (int64_t)((nout + 15) / 16) * 64;
-    const float *W1Tg = reinterpret_cast<const float *>(W2p + 4 * (int64_t)((nout + 15) / 16) * 64);
-    int64_t w1t_lds = -1;
-    if (P > 0 && (size_t)(nrf4 + (int64_t)P * 16) * sizeof(float4) <= 160 * 1024) {
-        w1t_lds = nrf4;
-        nrf4 += (int64_t)P * 16;
+    // recurrent weights in LDS, then the output weights when they fit (n_out <= 64 with the
+    // GRU), then the one-hot prefix's W1^T when it fits too (else each is read through L2)
+    constexpr size_t kLdsMax = 160 * 1024;
+    int64_t nrf4 = wr_f4, w2_lds = -1, w1t_lds = -1;
+    const float *W1Tg = reinterpret_cast<const float *>(W2p + w2_f4);
+    if ((size_t)(nrf4 + w2_f4) * sizeof(float4) <= kLdsMax) {
+        w2_lds = nrf4;
+        nrf4 += w2_f4;
+        if (P > 0 && (size_t)(nrf4 + (int64_t)P * 16) * sizeof(float4) <= kLdsMax) {
+            w1t_lds = nrf4;
+            nrf4 += (int64_t)P * 16;
+        }
     }
     const size_t lds = (size_t)nrf4 * sizeof(float4);
     const bool gen = (K & 31) != 0 || (xs & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 ||
@@ -779,7 +910,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
 #define LL_(RNN, SEL, GEN)                                                                                   \
     hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL, GEN>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, \
-                       Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa, W1Tg, P, w1t_lds)
+                       Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa, W1Tg, P, wr_f4, w2_lds, \
+                       w1t_lds)
 #define LG_(RNN, SEL) \
     if (gen) LL_(RNN, SEL, true); else LL_(RNN, SEL, false)
         if (use_rnn) {
