@@ -72,6 +72,12 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 #ifndef ASG_AGENT_GRU_X3
 #define ASG_AGENT_GRU_X3 1
 #endif
+// fc1 the same way (-DASG_AGENT_FC1_X3=1; needs K % 32 == 0): measured 0.714 vs 0.702 ms with
+// the f32 fc1 -- its W1 planes (96 KiB) do not fit next to the GRU planes in LDS, and one
+// output tile of L2 prefetch does not cover their latency -- so off by default
+#ifndef ASG_AGENT_FC1_X3
+#define ASG_AGENT_FC1_X3 0
+#endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // packed W_ih / W_hh: [gate 3][slab hb 4][k-slice 2][plane 3][lane 64] x 8 bf16
@@ -189,7 +195,8 @@ __device__ __forceinline__ void agent_rows(
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
-    float *__restrict__ Q, const SelectArgs &sel, const float *__restrict__ W1T, int P) {
+    float *__restrict__ Q, const SelectArgs &sel, const float *__restrict__ W1T, int P,
+    const u32x4v *__restrict__ W1x3) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= R) return;  // whole wave idle
     int64_t rows[kNT];
@@ -349,6 +356,54 @@ __device__ __forceinline__ void agent_rows(
                     }
                 }
             }
+#if ASG_AGENT_FC1_X3
+            if (!GEN && W1x3 && (t0 & 1) == 0) {
+                // fc1 on bf16 MFMAs, three-way split (see split3): k-slice sl = f32 chunks
+                // 2 sl and 2 sl + 1 of the row, whose float4s are exactly the gru_x3_k order;
+                // W1 planes from L2 one output tile ahead, X one slice ahead
+                const int ns = nk >> 1;
+                auto load_x = [&](int sl, float4 (&xb)[2][kNT]) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt)
+                            xb[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + 32 * sl + 16 * c + 4 * q);
+                };
+                auto load_w = [&](int sl, int mt, u32x4v (&w)[3]) {
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) w[pl] = W1x3[((sl * 4 + mt) * 3 + pl) * 64 + lane];
+                };
+                float4 xa[2][kNT], xn[2][kNT];
+                u32x4v wc[3], wn[3];
+                load_x(t0 >> 1, xa);
+                if ((t0 >> 1) + 1 < ns) load_x((t0 >> 1) + 1, xn);
+                load_w(t0 >> 1, 0, wc);
+                for (int sl = t0 >> 1; sl < ns; ++sl) {
+                    u32x4v a3[kNT][3];
+#pragma unroll
+                    for (int nt = 0; nt < kNT; ++nt) {
+                        const float v8[8] = {xa[0][nt].x, xa[0][nt].y, xa[0][nt].z, xa[0][nt].w,
+                                             xa[1][nt].x, xa[1][nt].y, xa[1][nt].z, xa[1][nt].w};
+                        split3(v8, a3[nt][0], a3[nt][1], a3[nt][2]);
+                    }
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt) xa[c][nt] = xn[c][nt];
+                    if (sl + 2 < ns) load_x(sl + 2, xn);
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) {
+                        if (mt < 3) load_w(sl, mt + 1, wn);
+                        else if (sl + 1 < ns) load_w(sl + 1, 0, wn);
+#pragma unroll
+                        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma_x3(wc, a3[nt], acc[mt][nt]);
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) wc[pl] = wn[pl];
+                    }
+                }
+            } else
+#endif
+            {
             load(t0, aA, wA);
             if (nk > t0 + 1) load(t0 + 1, aB, wB);
             for (int t = t0; t < nk; ++t) {
@@ -362,6 +417,7 @@ __device__ __forceinline__ void agent_rows(
                 for (int i = 0; i < 4; ++i) wA[i] = wB[i];
                 if (t + 2 < nk) load(t + 2, aB, wB);
                 chunk(a4, w4);
+            }
             }
         }
 #pragma unroll
@@ -723,10 +779,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ASG_AG
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wihp,
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
-    float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1T, int P) {
+    float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1T, int P, const u32x4v *__restrict__ W1x3) {
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRowsPerWave;
     agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sel,
-                              W1T, P);
+                              W1T, P, W1x3);
 }
 
 // Persistent variant: one 512-thread workgroup per CU copies the recurrent and output
@@ -752,7 +808,7 @@ rnn_agent_lds_kernel(
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
     const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,
     float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1Tg, int P,
-    int64_t wr_f4, int64_t w2_lds, int64_t w1t_lds) {
+    int64_t wr_f4, int64_t w2_lds, int64_t w1t_lds, const u32x4v *__restrict__ W1x3) {
     extern __shared__ float4 s_w[];
     for (int64_t i = threadIdx.x; i < nrf4; i += blockDim.x) s_w[i] = Wrp[i];
     __syncthreads();
@@ -766,7 +822,7 @@ rnn_agent_lds_kernel(
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
         agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel,
-                                  W1T, P);
+                                  W1T, P, W1x3);
     }
 }
 
@@ -776,6 +832,8 @@ rnn_agent_lds_kernel(
 // prefix rows are verified one-hot (or zero) adds W1[:, a] instead of running the prefix
 // chunks' MFMAs.  P = 0 (no section) unless n_out % 16 == 0 and n_out < K.
 static int onehot_prefix(int K, int nout) { return (nout % 16 == 0 && nout < K && K % 32 == 0) ? nout : 0; }
+// W1 as three bf16 planes for the split fc1 ([K / 32][mt 4][plane 3][lane 64] x 8 bf16)
+static int64_t w1x3_f4(int K) { return ASG_AGENT_FC1_X3 && K % 32 == 0 ? (int64_t)(K / 32) * 4 * 3 * 64 : 0; }
 
 // float4 count of the packed weight buffer
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
@@ -783,7 +841,7 @@ int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
     const int64_t wr = use_rnn ? 2 * kGruF4 : 4 * 4 * 64;
     const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
     const int64_t w1t = (int64_t)onehot_prefix(K, nout) * 16;
-    return w1 + wr + w2 + w1t;
+    return w1 + wr + w2 + w1t + w1x3_f4(K);
 }
 
 // W_ih / W_hh [3 * 64][64] -> kGruX3F4 x 8 bf16 (gru_x3_idx order, k order gru_x3_k)
@@ -796,6 +854,19 @@ __global__ void pack_gru_x3_kernel(const float *W, u32x4v *out) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = W[(int64_t)row * kHid + gru_x3_k(sl, q, j)];
+    u32x4v h, m, l;
+    split3(x, h, m, l);
+    out[i] = pl == 0 ? h : (pl == 1 ? m : l);
+}
+
+__global__ void pack_w1_x3_kernel(const float *W1, int K, u32x4v *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (K / 32) * 4 * 3 * 64) return;
+    const int lane = i & 63, pl = (i >> 6) % 3, mt = (i / (64 * 3)) & 3, sl = i / (64 * 3 * 4);
+    const int row = 16 * mt + (lane & 15), q = lane >> 4;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = W1[(int64_t)row * K + gru_x3_k(sl, q, j)];
     u32x4v h, m, l;
     split3(x, h, m, l);
     out[i] = pl == 0 ? h : (pl == 1 ? m : l);
@@ -830,9 +901,14 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
         one(Wih, kHid, kHid);
     }
     one(W2, nout, kHid);
-    if (const int P = onehot_prefix(K, nout))
+    const int P = onehot_prefix(K, nout);
+    if (P)
         hipLaunchKernelGGL(pack_w1t_kernel, dim3((P * kHid + 255) / 256), dim3(256), 0, s, W1, K, P,
                            reinterpret_cast<float *>(p));
+    p += (int64_t)P * 16;
+    if (const int64_t n3 = w1x3_f4(K))
+        hipLaunchKernelGGL(pack_w1_x3_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, s, W1, K,
+                           reinterpret_cast<u32x4v *>(p));
     return hipGetLastError();
 }
 
@@ -891,6 +967,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     constexpr size_t kLdsMax = 160 * 1024;
     int64_t nrf4 = wr_f4, w2_lds = -1, w1t_lds = -1;
     const float *W1Tg = reinterpret_cast<const float *>(W2p + w2_f4);
+    const u32x4v *W1x3 = w1x3_f4(K) ? reinterpret_cast<const u32x4v *>(W2p + w2_f4 + (int64_t)onehot_prefix(K, nout) * 16)
+                                    : nullptr;
     if ((size_t)(nrf4 + w2_f4) * sizeof(float4) <= kLdsMax) {
         w2_lds = nrf4;
         nrf4 += w2_f4;
@@ -911,7 +989,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
 #define LL_(RNN, SEL, GEN)                                                                                   \
     hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL, GEN>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, \
                        Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa, W1Tg, P, wr_f4, w2_lds, \
-                       w1t_lds)
+                       w1t_lds, W1x3)
 #define LG_(RNN, SEL) \
     if (gen) LL_(RNN, SEL, true); else LL_(RNN, SEL, false)
         if (use_rnn) {
@@ -925,7 +1003,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     }
 #define L_(RNN, SEL, GEN)                                                                                    \
     hipLaunchKernelGGL((rnn_agent_fwd_kernel<RNN, SEL, GEN>), dim3(blocks), dim3(256), 0, s, X, xs, R, K, Hin, hs, \
-                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa, W1Tg, P)
+                       W1p, b1, Wihp, bih, Whhp, bhh, W2p, b2, nout, Hout, Q, sa, W1Tg, P, W1x3)
 #define LG_(RNN, SEL) \
     if (gen) L_(RNN, SEL, true); else L_(RNN, SEL, false)
     if (use_rnn) {
