@@ -44,6 +44,20 @@ def step_bytes(n, m, L):
 
 
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (= f32 vector peak; MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+# f32 products as three-way-split bf16 MFMAs cost six bf16 products each
+X3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6
+
+
+def agent_peak(n, m, L, mode, hidden=64, use_rnn=True, onehot=True):
+    """f32-equivalent MFMA roof of the agent forward: each layer's flops at the peak of the
+    MFMA it runs on (asg_rnn_agent_mfma_mode: bit 0 GRU, bit 1 fc1 on split bf16), combined
+    as the time-weighted harmonic mean (flops / sum of per-layer minimum times)."""
+    K = m * (L + 1) - (m if onehot else 0)
+    fc1, rec, fc2 = 2 * K * hidden, 2 * (2 * 3 * hidden * hidden if use_rnn else hidden * hidden), 2 * hidden * m
+    t = (fc1 / (X3_PEAK_TFS if mode & 2 else F32_MFMA_PEAK_TFS) + rec / (X3_PEAK_TFS if mode & 1 else F32_MFMA_PEAK_TFS)
+         + fc2 / F32_MFMA_PEAK_TFS)
+    return (fc1 + rec + fc2) / t
 
 
 def agent_flops(n, m, L, hidden=64, use_rnn=True, onehot=True):
@@ -62,11 +76,17 @@ def agent_roofline(a, E, sel_ms):
     peak: the kernel that takes most of each step's time next to the env step."""
     if a.selector == "random" or sel_ms <= 0:
         return None
-    onehot = a.agent == "rnn_fused" and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
+    fused = a.agent == "rnn_fused"
+    onehot = fused and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
     flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
     tfs = flops / (sel_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "traffic": None,
+    from marl_sap_amd import _lib
+    mode = int(_lib.lib().asg_rnn_agent_mfma_mode()) if fused else 0
+    peak = agent_peak(a.n, a.m, a.L, mode, onehot=onehot)
+    return {"bound": "mfma", "achieved": round(tfs, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(tfs / peak, 4), "traffic": None,
+            "peak_note": ("f32-equivalent: GRU products on three-way-split bf16 MFMAs (2.5 PF / 6), fc1/fc2 "
+                          "on f32 MFMAs (157.3 TF), time-weighted" if mode else "f32 MFMA peak"),
             "kernel": ("asg::rnn_agent_lds_kernel" if a.agent == "rnn_fused" else "torch agent + selector")
             if a.selector == "eps" else f"{a.agent} forward + asg::sap_select_kernel (whole selection)",
             "kernel_ms": round(sel_ms, 4), "flops_per_launch": flops}

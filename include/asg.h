@@ -221,6 +221,10 @@ int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t
  * contiguous.  Outputs h_out [R][hidden], q_out [R][n_out], contiguous.  hidden must be 64,
  * 1 <= n_out <= 512 (the real envs' m, e.g. 450; a partial last 16-task tile is masked). */
 int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn);
+/* Which layers of this build run their f32 products as three-way-split bf16 MFMAs (six cross
+ * products, fp32-level accuracy; asg_agent.hip): bit 0 = GRU (default), bit 1 = fc1.  The
+ * rest run f32 MFMAs.  For roofline accounting (bench.py); results match either way. */
+int asg_rnn_agent_mfma_mode(void);
 int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, const float *W2, int K,
                        int hidden, int n_out, int use_rnn, void *packed, void *hip_stream);
 int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,

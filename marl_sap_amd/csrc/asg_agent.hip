@@ -1028,6 +1028,8 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 
 }  // namespace asg
 
+extern "C" int asg_rnn_agent_mfma_mode(void) { return (ASG_AGENT_GRU_X3 ? 1 : 0) | (ASG_AGENT_FC1_X3 ? 2 : 0); }
+
 #ifdef ASG_AGENT_STAMPS
 // profiling builds: copy the stamps out (uint64 [16][4][8]) and re-arm
 extern "C" int asg_debug_agent_stamps(unsigned long long *out) {

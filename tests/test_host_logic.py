@@ -135,3 +135,6 @@ def test_bench_accounting():
     assert bench.step_bytes(16, 16, 3) == 16 * 16 * 29 + 16 * 20 + 9
     assert bench.agent_flops(64, 64, 3, onehot=False) == 90112  # 2 * (256*64 + 2*3*64*64 + 64*64)
     assert bench.agent_flops(64, 64, 3) == 81920  # the one-hot block is a W1 column gather
+    # roof: f32 MFMA everywhere, or the GRU's 49,152 flops at 2.5 PF / 6 (split bf16)
+    assert bench.agent_peak(64, 64, 3, 0) == pytest.approx(157.3)
+    assert bench.agent_peak(64, 64, 3, 1) == pytest.approx(81920 / (32768 / 157.3 + 49152 / (2500 / 6)))
