@@ -105,9 +105,10 @@ __device__ __forceinline__ void split3(const float (&x)[8], u32x4v &h, u32x4v &m
         const uint32_t ua = __builtin_bit_cast(uint32_t, ra), ub = __builtin_bit_cast(uint32_t, rb);
         const float sa = ra - __builtin_bit_cast(float, ua & 0xffff0000u);
         const float sb = rb - __builtin_bit_cast(float, ub & 0xffff0000u);
-        h[p] = (xa >> 16) | (xb & 0xffff0000u);
-        m[p] = (ua >> 16) | (ub & 0xffff0000u);
-        l[p] = (__builtin_bit_cast(uint32_t, sa) >> 16) | (__builtin_bit_cast(uint32_t, sb) & 0xffff0000u);
+        // upper halves of (a, b) -> one dword (v_perm_b32: bytes 2, 3 of a, then of b)
+        h[p] = __builtin_amdgcn_perm(xb, xa, 0x07060302u);
+        m[p] = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+        l[p] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, sb), __builtin_bit_cast(uint32_t, sa), 0x07060302u);
     }
 }
 // element j of the split back to f32 (exact)
