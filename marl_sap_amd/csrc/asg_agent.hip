@@ -276,18 +276,75 @@ __device__ __forceinline__ void agent_rows(
         // ping-pong over two register buffers, unrolled by two: a buffer is refilled right
         // after its chunk's MFMAs, so two chunks stay in flight without register copies
         // (a rotating a0 = a1 form compiles to copies that wait for the newest loads)
+        // one-hot prefix (onehot_prefix): when every row of the tile holds at most one
+        // nonzero in its first P inputs and that entry is exactly 1 (the mock env's
+        // onehot(previous task), or zeros at t = 0), those P / 16 chunks contribute
+        // W1[:, a] -- added from W1^T -- and their MFMAs are skipped; any other input
+        // (checked per tile) runs the full MFMA loop.
+        int t0 = 0;
+        if (!GEN && P > 0) {
+            int pos[kNT];
+            bool bad = false;
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt) pos[nt] = -1;
+            for (int t4 = 0; t4 < P / 16; t4 += 4) {  // P % 64 == 0 or P / 16 < 4: guarded
+                float4 pa[4][kNT];
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int nt = 0; nt < kNT; ++nt)
+                        pa[c][nt] = (t4 + c < P / 16)
+                                        ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float v = comp(pa[c][nt], e);
+                            const bool one = v == 1.0f;
+                            bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
+                            pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
+                        }
+            }
+            bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
+#pragma unroll
+            for (int nt = 0; nt < kNT; ++nt) {
+                const uint64_t mk = __ballot(pos[nt] >= 0);
+                const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull,
+                               g3 = mk >> 48;
+                rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
+            }
+            if (rows_ok && __ballot(bad) == 0) {
+                t0 = P / 16;
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) {
+                    int a = pos[nt];
+                    a = max(a, __shfl_xor(a, 16));
+                    a = max(a, __shfl_xor(a, 32));
+                    if (a >= 0) {
+#pragma unroll
+                        for (int mt = 0; mt < 4; ++mt) {
+                            const float4 w = *reinterpret_cast<const float4 *>(W1T + a * kHid + 16 * mt + 4 * q);
+                            acc[mt][nt] += f32x4{w.x, w.y, w.z, w.w};
+                        }
+                    }
+                }
+            }
+        }
 #ifdef ASG_AGENT_FC1_PINGPONG
-        if (!GEN) {
+        if (!GEN && ((nk - t0) & 1) == 0) {
             // nk even (K % 32 == 0): ping-pong over two register buffers, each refilled right
             // after its chunk's MFMAs, with scheduling barriers so the refills are not sunk
             // next to their uses.  Measured slower (0.894 vs 0.868 ms): obs latency is not
             // what bounds this kernel (tools/agent_ab.py, ASG_AB_L2X).
-            load(0, aA, wA);
+            load(t0, aA, wA);
             __builtin_amdgcn_sched_barrier(0);
-            load(1, aB, wB);
+            load(t0 + 1, aB, wB);
             __builtin_amdgcn_sched_barrier(0);
             const int last = nk - 1;
-            for (int t = 0; t < nk; t += 2) {
+            for (int t = t0; t < nk; t += 2) {
                 chunk(aA, wA);
                 __builtin_amdgcn_sched_barrier(0);
                 load(t + 2 < last ? t + 2 : last, aA, wA);
@@ -300,63 +357,6 @@ __device__ __forceinline__ void agent_rows(
         } else
 #endif
         {
-            // one-hot prefix (onehot_prefix): when every row of the tile holds at most one
-            // nonzero in its first P inputs and that entry is exactly 1 (the mock env's
-            // onehot(previous task), or zeros at t = 0), those P / 16 chunks contribute
-            // W1[:, a] -- added from W1^T -- and their MFMAs are skipped; any other input
-            // (checked per tile) runs the full MFMA loop.
-            int t0 = 0;
-            if (!GEN && P > 0) {
-                int pos[kNT];
-                bool bad = false;
-#pragma unroll
-                for (int nt = 0; nt < kNT; ++nt) pos[nt] = -1;
-                for (int t4 = 0; t4 < P / 16; t4 += 4) {  // P % 64 == 0 or P / 16 < 4: guarded
-                    float4 pa[4][kNT];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-#pragma unroll
-                        for (int nt = 0; nt < kNT; ++nt)
-                            pa[c][nt] = (t4 + c < P / 16)
-                                            ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-#pragma unroll
-                        for (int nt = 0; nt < kNT; ++nt)
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) {
-                                const float v = comp(pa[c][nt], e);
-                                const bool one = v == 1.0f;
-                                bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
-                                pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
-                            }
-                }
-                bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
-#pragma unroll
-                for (int nt = 0; nt < kNT; ++nt) {
-                    const uint64_t mk = __ballot(pos[nt] >= 0);
-                    const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull,
-                                   g3 = mk >> 48;
-                    rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
-                }
-                if (rows_ok && __ballot(bad) == 0) {
-                    t0 = P / 16;
-#pragma unroll
-                    for (int nt = 0; nt < kNT; ++nt) {
-                        int a = pos[nt];
-                        a = max(a, __shfl_xor(a, 16));
-                        a = max(a, __shfl_xor(a, 32));
-                        if (a >= 0) {
-#pragma unroll
-                            for (int mt = 0; mt < 4; ++mt) {
-                                const float4 w = *reinterpret_cast<const float4 *>(W1T + a * kHid + 16 * mt + 4 * q);
-                                acc[mt][nt] += f32x4{w.x, w.y, w.z, w.w};
-                            }
-                        }
-                    }
-                }
-            }
 #if ASG_AGENT_FC1_X3
             if (!GEN && W1x3 && (t0 & 1) == 0) {
                 // fc1 on bf16 MFMAs, three-way split (see split3): k-slice sl = f32 chunks
