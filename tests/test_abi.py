@@ -77,3 +77,20 @@ def test_kernel_entry_points_validate_without_gpu(L):
         _lib.ASG_E_INVALID_ARG
     assert L.asg_reset(None, None, 0) == _lib.ASG_E_INVALID_ARG
     assert L.asg_step(None, None, 0) == _lib.ASG_E_INVALID_ARG
+
+
+def test_agent_pack_layout_without_gpu(L):
+    """Host-only sizing of the packed agent buffer: f32 W1 fragments, the GRU as three bf16
+    planes (split-bf16 MFMAs, asg_rnn_agent_mfma_mode bit 0), f32 W2, and W1^T of the one-hot
+    prefix when n_out % 16 == 0, n_out < K and K % 32 == 0."""
+    mode = L.asg_rnn_agent_mfma_mode()
+    assert mode & 1 == 1
+    gru = 3 * 4 * 2 * 3 * 64 if mode & 1 else 4 * 12 * 64
+    w1x3 = lambda K: (K // 32) * 4 * 3 * 64 if (mode & 2 and K % 32 == 0) else 0  # noqa: E731
+    for K, m, rnn in [(256, 64, 1), (1024, 256, 1), (70, 16, 1), (256, 64, 0), (490, 450, 1)]:
+        wr = 2 * gru if rnn else 4 * 4 * 64
+        w1 = ((K + 15) // 16) * 4 * 64
+        w2 = 4 * ((m + 15) // 16) * 64
+        P = m if (m % 16 == 0 and m < K and K % 32 == 0) else 0
+        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K)), (K, m, rnn)
+    assert L.asg_rnn_agent_packed_size(256, 32, 64, 1) < 0  # hidden must be 64
