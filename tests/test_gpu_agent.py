@@ -131,3 +131,32 @@ def test_fused_select_equals_forward_then_selector(eps, B, n, m, K, use_rnn):
     assert torch.equal(h2, h1)
     assert torch.equal(out, a1)
     assert int(status.item()) == 0
+
+
+@pytest.mark.parametrize("use_rnn", [True])
+def test_split_bf16_gru_is_fp32_accurate(use_rnn):
+    """The GRU's products run on three-way-split bf16 MFMAs (asg_rnn_agent_mfma_mode bit 0):
+    against a float64 evaluation of the same module, the fused kernel's error is of the
+    same size as PyTorch's own fp32 error (not bf16's ~4e-3), for h' and Q."""
+    from marl_sap_amd import _lib
+    assert _lib.lib().asg_rnn_agent_mfma_mode() & 1
+    torch.manual_seed(11)
+    R, m, K = 64 * 128, 64, 256
+    args = SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m)
+    ref = RNNAgent(K, args).to(DEV)
+    fused = RNNFusedAgent(K, args).to(DEV)
+    fused.load_state_dict(ref.state_dict())
+    ref64 = RNNAgent(K, args).to(DEV).double()
+    ref64.load_state_dict({k: v.double() for k, v in ref.state_dict().items()})
+    x = torch.randn((R, K), device=DEV)
+    h = torch.randn((R, 64), device=DEV) * 0.5
+    with torch.no_grad():
+        q64, h64 = ref64(x.double(), h.double())
+        q32, h32 = ref(x, h)
+        qf, hf = fused(x, h)
+    for got, want, base in ((hf, h64, h32), (qf, q64, q32)):
+        err_fused = (got.double() - want).abs().max().item()
+        err_torch = (base.double() - want).abs().max().item()
+        print(f"max |err| vs float64: fused {err_fused:.3e}, torch fp32 {err_torch:.3e}")
+        assert err_fused <= 4 * err_torch + 1e-7, (err_fused, err_torch)
+        assert err_fused < 1e-5
