@@ -78,6 +78,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 #ifndef ASG_AGENT_FC1_X3
 #define ASG_AGENT_FC1_X3 0
 #endif
+// fc2 the same way (-DASG_AGENT_FC2_X3=1): W2's hi + mid planes take W2's 16 KiB of LDS
+// (n_out = 64), its lo plane is read through L2
+#ifndef ASG_AGENT_FC2_X3
+#define ASG_AGENT_FC2_X3 0
+#endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // packed W_ih / W_hh: [gate 3][slab hb 4][k-slice 2][plane 3][lane 64] x 8 bf16
@@ -197,7 +202,7 @@ __device__ __forceinline__ void agent_rows(
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
     float *__restrict__ Q, const SelectArgs &sel, const float *__restrict__ W1T, int P,
-    const u32x4v *__restrict__ W1x3) {
+    const u32x4v *__restrict__ W1x3, const u32x4v *W2hm = nullptr, const u32x4v *__restrict__ W2lo = nullptr) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= R) return;  // whole wave idle
     int64_t rows[kNT];
@@ -646,6 +651,26 @@ __device__ __forceinline__ void agent_rows(
         f32x4 a2[kNT];
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) a2[nt] = f32x4{bq.x, bq.y, bq.z, bq.w};
+#if ASG_AGENT_FC2_X3
+        if (!GEN && W2lo) {
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl) {
+                u32x4v a3[kNT][3];
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) {
+                    const float v8[8] = {hp[2 * sl][nt][0],     hp[2 * sl][nt][1],     hp[2 * sl][nt][2],
+                                         hp[2 * sl][nt][3],     hp[2 * sl + 1][nt][0], hp[2 * sl + 1][nt][1],
+                                         hp[2 * sl + 1][nt][2], hp[2 * sl + 1][nt][3]};
+                    split3(v8, a3[nt][0], a3[nt][1], a3[nt][2]);
+                }
+                const u32x4v w3[3] = {W2hm[((c * 2 + sl) * 2 + 0) * 64 + lane], W2hm[((c * 2 + sl) * 2 + 1) * 64 + lane],
+                                      W2lo[(c * 2 + sl) * 64 + lane]};
+#pragma unroll
+                for (int nt = 0; nt < kNT; ++nt) a2[nt] = mfma_x3(w3, a3[nt], a2[nt]);
+            }
+        } else
+#endif
+        {
         float4 w2[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) w2[t] = W2p[pk(t, c, nct, lane)];
@@ -655,6 +680,7 @@ __device__ __forceinline__ void agent_rows(
             for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int nt = 0; nt < kNT; ++nt) a2[nt] = mfma4(comp(w2[t], e), hp[t][nt][e], a2[nt]);
+        }
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) {
             if (Q && ok[nt]) {
@@ -809,21 +835,31 @@ rnn_agent_lds_kernel(
     const float4 *__restrict__ W1p, const float *__restrict__ b1, const float4 *__restrict__ Wrp, int64_t nrf4,
     const float *__restrict__ bih, const float *__restrict__ bhh, const float *__restrict__ b2, int nout,
     float *__restrict__ Hout, float *__restrict__ Q, SelectArgs sel, const float *__restrict__ W1Tg, int P,
-    int64_t wr_f4, int64_t w2_lds, int64_t w1t_lds, const u32x4v *__restrict__ W1x3) {
+    int64_t wr_f4, int64_t w2_lds, int64_t w1t_lds, const u32x4v *__restrict__ W1x3,
+    const u32x4v *__restrict__ W2hmg, const u32x4v *__restrict__ W2lo, int64_t w2hm_f4) {
     extern __shared__ float4 s_w[];
-    for (int64_t i = threadIdx.x; i < nrf4; i += blockDim.x) s_w[i] = Wrp[i];
+    // W2's split hi + mid planes (w2hm_f4 > 0) are staged where the f32 W2 would sit
+    const int64_t lead = w2hm_f4 > 0 ? wr_f4 : nrf4;
+    for (int64_t i = threadIdx.x; i < lead; i += blockDim.x) s_w[i] = Wrp[i];
+    for (int64_t i = threadIdx.x; i < w2hm_f4; i += blockDim.x)
+        s_w[wr_f4 + i] = reinterpret_cast<const float4 *>(W2hmg)[i];
     __syncthreads();
+    // always an LDS address (a select with NULL would make it a flat pointer); used only when
+    // w2hm_f4 > 0, signalled to agent_rows through W2lo != NULL
+    const u32x4v *W2hm = reinterpret_cast<const u32x4v *>(s_w + wr_f4);
     const float4 *Wih = s_w;
     const float4 *Whh = s_w + (RNN ? kGruF4 : 0);
     // W2 staged after the recurrent weights when it fit (w2_lds >= 0), else read through L2
     const float4 *W2 = w2_lds >= 0 ? s_w + w2_lds : Wrp + wr_f4;
-    // W1^T of the one-hot prefix: staged with the other weights when it fit (w1t_lds >= 0)
-    const float *W1T = w1t_lds >= 0 ? reinterpret_cast<const float *>(s_w + w1t_lds) : W1Tg;
+    // W1^T of the one-hot prefix: read through L2 (a select between an LDS and a global
+    // pointer would make every gather a flat load); w1t_lds is unused
+    (void)w1t_lds;
+    const float *W1T = W1Tg;
     const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
         agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel,
-                                  W1T, P, W1x3);
+                                  W1T, P, W1x3, W2hm, W2lo);
     }
 }
 
@@ -833,6 +869,9 @@ rnn_agent_lds_kernel(
 // prefix rows are verified one-hot (or zero) adds W1[:, a] instead of running the prefix
 // chunks' MFMAs.  P = 0 (no section) unless n_out % 16 == 0 and n_out < K.
 static int onehot_prefix(int K, int nout) { return (nout % 16 == 0 && nout < K && K % 32 == 0) ? nout : 0; }
+// W2 as three bf16 planes for the split fc2: hi + mid planes [c][sl 2][plane 2][lane 64],
+// then the lo planes [c][sl 2][lane 64] (x 8 bf16)
+static int64_t w2x3_f4(int nout) { return ASG_AGENT_FC2_X3 ? (int64_t)((nout + 15) / 16) * 2 * 3 * 64 : 0; }
 // W1 as three bf16 planes for the split fc1 ([K / 32][mt 4][plane 3][lane 64] x 8 bf16)
 static int64_t w1x3_f4(int K) { return ASG_AGENT_FC1_X3 && K % 32 == 0 ? (int64_t)(K / 32) * 4 * 3 * 64 : 0; }
 
@@ -842,7 +881,7 @@ int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
     const int64_t wr = use_rnn ? 2 * kGruF4 : 4 * 4 * 64;
     const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
     const int64_t w1t = (int64_t)onehot_prefix(K, nout) * 16;
-    return w1 + wr + w2 + w1t + w1x3_f4(K);
+    return w1 + wr + w2 + w1t + w1x3_f4(K) + w2x3_f4(nout);
 }
 
 // W_ih / W_hh [3 * 64][64] -> kGruX3F4 x 8 bf16 (gru_x3_idx order, k order gru_x3_k)
@@ -871,6 +910,22 @@ __global__ void pack_w1_x3_kernel(const float *W1, int K, u32x4v *out) {
     u32x4v h, m, l;
     split3(x, h, m, l);
     out[i] = pl == 0 ? h : (pl == 1 ? m : l);
+}
+
+__global__ void pack_w2_x3_kernel(const float *W2, int nout, u32x4v *out) {
+    const int nct = (nout + 15) / 16;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over [c][sl][lane]
+    if (i >= nct * 2 * 64) return;
+    const int lane = i & 63, sl = (i >> 6) & 1, c = i >> 7;
+    const int row = 16 * c + (lane & 15), q = lane >> 4;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = row < nout ? W2[(int64_t)row * kHid + gru_x3_k(sl, q, j)] : 0.f;
+    u32x4v h, m, l;
+    split3(x, h, m, l);
+    out[((c * 2 + sl) * 2 + 0) * 64 + lane] = h;
+    out[((c * 2 + sl) * 2 + 1) * 64 + lane] = m;
+    out[nct * 2 * 2 * 64 + (c * 2 + sl) * 64 + lane] = l;
 }
 
 __global__ void pack_w1t_kernel(const float *W1, int K, int P, float *out) {
@@ -910,6 +965,10 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     if (const int64_t n3 = w1x3_f4(K))
         hipLaunchKernelGGL(pack_w1_x3_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, s, W1, K,
                            reinterpret_cast<u32x4v *>(p));
+    p += w1x3_f4(K);
+    if (w2x3_f4(nout))
+        hipLaunchKernelGGL(pack_w2_x3_kernel, dim3((unsigned)(((nout + 15) / 16 * 128 + 255) / 256)), dim3(256), 0, s,
+                           W2, nout, reinterpret_cast<u32x4v *>(p));
     return hipGetLastError();
 }
 
@@ -973,14 +1032,17 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     if ((size_t)(nrf4 + w2_f4) * sizeof(float4) <= kLdsMax) {
         w2_lds = nrf4;
         nrf4 += w2_f4;
-        if (P > 0 && (size_t)(nrf4 + (int64_t)P * 16) * sizeof(float4) <= kLdsMax) {
-            w1t_lds = nrf4;
-            nrf4 += (int64_t)P * 16;
-        }
     }
+    // split fc2 (ASG_AGENT_FC2_X3): hi + mid planes in W2's LDS slot, lo through L2
+    const int64_t w2hm_f4 = w2x3_f4(nout) ? (int64_t)((nout + 15) / 16) * 2 * 2 * 64 : 0;
+    const u32x4v *W2x3g = w2x3_f4(nout) ? reinterpret_cast<const u32x4v *>(
+                                             W2p + w2_f4 + (int64_t)onehot_prefix(K, nout) * 16 + w1x3_f4(K))
+                                       : nullptr;
     const size_t lds = (size_t)nrf4 * sizeof(float4);
     const bool gen = (K & 31) != 0 || (xs & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0 ||
                      nout > 256;
+    // (the general-shape instantiation keeps the f32 W2 in that LDS slot)
+    const bool fc2x3 = use_rnn && !gen && W2x3g && w2_lds == wr_f4 && w2hm_f4 <= w2_f4;
     if (use_lds_weights() && lds <= 160 * 1024) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -990,7 +1052,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
 #define LL_(RNN, SEL, GEN)                                                                                   \
     hipLaunchKernelGGL((rnn_agent_lds_kernel<RNN, SEL, GEN>), dim3(grid), dim3(64 * kLdsWaves), lds, s, X, xs, R, K, \
                        Hin, hs, W1p, b1, Wihp, nrf4, bih, bhh, b2, nout, Hout, Q, sa, W1Tg, P, wr_f4, w2_lds, \
-                       w1t_lds, W1x3)
+                       w1t_lds, W1x3, fc2x3 ? W2x3g : nullptr, fc2x3 ? W2x3g + w2hm_f4 : nullptr, \
+                       fc2x3 ? w2hm_f4 : (int64_t)0)
 #define LG_(RNN, SEL) \
     if (gen) LL_(RNN, SEL, true); else LL_(RNN, SEL, false)
         if (use_rnn) {
