@@ -202,7 +202,8 @@ __device__ __forceinline__ void agent_rows(
     const float *__restrict__ bih, const float4 *__restrict__ Whhp, const float *__restrict__ bhh,
     const float4 *__restrict__ W2p, const float *__restrict__ b2, int nout, float *__restrict__ Hout,
     float *__restrict__ Q, const SelectArgs &sel, const float *__restrict__ W1T, int P,
-    const u32x4v *__restrict__ W1x3, const u32x4v *W2hm = nullptr, const u32x4v *__restrict__ W2lo = nullptr) {
+    const u32x4v *__restrict__ W1x3, const u32x4v *W2hm = nullptr, const u32x4v *__restrict__ W2lo = nullptr,
+    const float4 *W2l = nullptr, bool w2l_on = false) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= R) return;  // whole wave idle
     int64_t rows[kNT];
@@ -672,8 +673,18 @@ __device__ __forceinline__ void agent_rows(
 #endif
         {
         float4 w2[4];
+        if (w2l_on) {  // staged in LDS: ds_read, not a flat load through a merged pointer
+            typedef const f32x4 __attribute__((address_space(3))) * lds_f4p;
+            const lds_f4p W2s = (lds_f4p)W2l;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) w2[t] = W2p[pk(t, c, nct, lane)];
+            for (int t = 0; t < 4; ++t) {
+                const f32x4 v = W2s[pk(t, c, nct, lane)];
+                w2[t] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) w2[t] = W2p[pk(t, c, nct, lane)];
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -850,7 +861,8 @@ rnn_agent_lds_kernel(
     const float4 *Wih = s_w;
     const float4 *Whh = s_w + (RNN ? kGruF4 : 0);
     // W2 staged after the recurrent weights when it fit (w2_lds >= 0), else read through L2
-    const float4 *W2 = w2_lds >= 0 ? s_w + w2_lds : Wrp + wr_f4;
+    const float4 *W2 = Wrp + wr_f4;
+    const float4 *W2l = s_w + (w2_lds >= 0 ? w2_lds : 0);
     // W1^T of the one-hot prefix: read through L2 (a select between an LDS and a global
     // pointer would make every gather a flat load); w1t_lds is unused
     (void)w1t_lds;
@@ -859,7 +871,7 @@ rnn_agent_lds_kernel(
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kLdsWaves + (threadIdx.x >> 6)) * kRowsPerWave;
         agent_rows<RNN, SEL, GEN>(row0, X, xs, R, K, Hin, hs, W1p, b1, Wih, bih, Whh, bhh, W2, b2, nout, Hout, Q, sel,
-                                  W1T, P, W1x3, W2hm, W2lo);
+                                  W1T, P, W1x3, W2hm, W2lo, W2l, w2_lds >= 0 && !W2lo);
     }
 }
 
