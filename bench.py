@@ -1,27 +1,41 @@
 """Headline benchmark: env-steps/s of the batched assignment-env rollout on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--selector eps|sap|random]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 0..4] [--selector eps|sap|random]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
 
-Workload (BASELINE.json configs[2]; configs[3] when N = 8): n = m = 64 agents/tasks,
-T = 20, L = 3, lambda = 0.5, E = 16,384 envs per GPU, BasicMAC + RNNAgent (hidden 64,
-GRUCell, fp32, PyTorch-ROCm) with the epsilon-greedy selector (eps = 0.05), Philox bump
-benefits.  One "step" = one transition of every env on every rank: agent forward +
-action selection + actions row write + one HIP env step kernel; every T steps an episode
-ends (returns all-gathered over RCCL on the device) and the next one is reset inside the
-timed region; the host-side episode checks (device error words, selector status, logging)
-run once after it (GpuVecRunner.finish_episode(sync=False) / flush_pending).  value = world * E * K / (max over ranks of the K-step time).
+--config i selects BASELINE.json configs[i] (default 2; 3 is configs[2] per GPU on N GPUs):
+  0  4 x 4, 1 env, fused RNN agent + epsilon-greedy  (the reference's CPU plumbing case)
+  1  16 x 16, 4,096 envs per GPU, random policy
+  2  64 x 64, 16,384 envs per GPU, BasicMAC + RNNAgent (GRU 64, fp32) + epsilon-greedy 0.05
+  3  as 2 on every rank of an N-GPU job (131,072 envs at N = 8; weak scaling)
+  4  256 x 256 dense benefits, 2,048 envs per GPU, BasicMAC + RNNAgent + epsilon-greedy
+Explicit --n/--m/--envs/--selector/--agent/--benefits override the config's values.
+
+One "step" = one transition of every env on every rank: action selection (agent forward +
+selector, writing the actions row of the EpisodeBatch) + one HIP env step kernel; every T
+steps an episode ends (returns all-gathered on the device) and the next one is reset inside
+the timed region; the host-side episode checks (device error words, selector status,
+logging) run once after it (GpuVecRunner.finish_episode(sync=False) / flush_pending).
+value = (sum over ranks of envs) * K / (max over ranks of the K-step time).
 
 The JSON line also carries:
-  roofline: the env step kernel (the HIP hot path): algorithmic bytes per launch
-            (B_step * E) / its average duration, timed live with HIP events
-            on the stream it is launched on, against the 8 TB/s HBM3E peak; `traffic` is the
-            PMC-measured HBM bytes per launch from profiles/ when a matching summary exists.
-  cpu_baseline: rank 0 at N = 1 only: the reference's CPU design (subprocess-per-env
-            ParallelRunner + numpy env + CPU RNN agent, oracle/cpu_parallel_runner.py) on a
-            bounded sample of the same workload.
+  roofline        the env step kernel (the HIP hot path): algorithmic bytes per launch
+                  (B_step * E) / its mean duration, timed live with HIP events on
+                  the stream it is launched on, against the 8 TB/s HBM3E peak; `traffic` is the
+                  PMC-measured HBM bytes per launch from profiles/pmc_step_kernel*.json when one
+                  matches the workload.
+  roofline_agent  the agent forward (fused RNNAgent kernel) against its MFMA roof.
+  cpu_baseline    rank 0 at N = 1 only: the reference's CPU design (subprocess-per-env
+                  ParallelRunner + numpy env + CPU RNN agent, oracle/cpu_parallel_runner.py) on
+                  a bounded sample of the same workload: step-loop-only and reset-amortised
+                  rates, the worker count used and the host's core count.
+  secondary       (N = 1, --secondary 1, the default then) configs[2] read literally -- the
+                  PyTorch RNNAgent forward + asg_epsilon_greedy -- and the SAP selector (fused
+                  noise + LSA per env) with its LSA efficiency figure; each with its own
+                  value and ms_per_step.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -34,19 +48,33 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-
-
-def step_bytes(n, m, L):
-    """Algorithmic HBM bytes of one env step (DESIGN.md 'Roofline'): obs f32 n*m*(L+1),
-    beta f32 n*m, avail_actions bool n*m, actions_onehot i64 n*m, actions i64 n (read),
-    rewards f32 n, prev_assigns i64 n, terminated 1 B, filled 8 B."""
-    return n * m * (4 * (L + 1) + 4 + 1 + 8) + n * (8 + 4 + 8) + 1 + 8
-
-
 F32_MFMA_PEAK_TFS = 157.3  # MI355X dense f32 MFMA (= f32 vector peak; MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 # f32 products as three-way-split bf16 MFMAs cost six bf16 products each
 X3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6
+SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock (MI355X_MICROARCH.md)
+VALU_CYCLES_PER_WAVE_INSTR = 2  # wave64 VALU over a SIMD-32 (MI355X_MICROARCH.md "Wave scheduling")
+CPU_WORKER_CAP = 16  # CPU share of one GPU on the gpurun box (os.cpu_count() shows the whole host)
+
+CONFIGS = {
+    0: dict(n=4, m=4, envs=1, selector="eps", agent="rnn_fused", benefits="bump",
+            label="4-agent/4-task assignment env, batch_size_run=1 (configs[0]: the reference's plumbing case)"),
+    1: dict(n=16, m=16, envs=4096, selector="random", agent="rnn_fused", benefits="bump",
+            label="16-agent/16-task assignment env, 4096 envs per GPU, random policy (configs[1])"),
+    2: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn_fused", benefits="bump",
+            label="64-agent/64-task assignment env, 16384 envs per GPU, BasicMAC+RNN (configs[2])"),
+    3: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn_fused", benefits="bump",
+            label="64-agent/64-task assignment env, 16384 envs per GPU sharded over the node (configs[3])"),
+    4: dict(n=256, m=256, envs=2048, selector="eps", agent="rnn_fused", benefits="dense",
+            label="256-agent/256-task dense-benefit assignment env, 2048 envs per GPU (configs[4])"),
+}
+
+
+def step_bytes(n, m, L):
+    """Algorithmic HBM bytes of one env step: obs f32 n*m*(L+1),
+    beta f32 n*m, avail_actions bool n*m, actions_onehot i64 n*m, actions i64 n (read),
+    rewards f32 n, prev_assigns i64 n, terminated 1 B, filled 8 B."""
+    return n * m * (4 * (L + 1) + 4 + 1 + 8) + n * (8 + 4 + 8) + 1 + 8
 
 
 def agent_peak(n, m, L, mode, hidden=64, use_rnn=True, onehot=True):
@@ -70,16 +98,14 @@ def agent_flops(n, m, L, hidden=64, use_rnn=True, onehot=True):
     return 2 * (K * hidden + rec + hidden * m)
 
 
-def agent_roofline(a, E, sel_ms):
-    """The action-selection launch (fused agent forward + epsilon-greedy, or the PyTorch
-    agent + selector kernel), timed with HIP events on its stream, against the f32 MFMA
-    peak: the kernel that takes most of each step's time next to the env step."""
-    if a.selector == "random" or sel_ms <= 0:
+def agent_roofline(a, E, agent_ms, kernel):
+    """The agent forward (timed with HIP events on its stream) against its MFMA roof."""
+    if agent_ms is None or agent_ms <= 0:
         return None
     fused = a.agent == "rnn_fused"
     onehot = fused and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
     flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
-    tfs = flops / (sel_ms * 1e-3) / 1e12
+    tfs = flops / (agent_ms * 1e-3) / 1e12
     from marl_sap_amd import _lib
     mode = int(_lib.lib().asg_rnn_agent_mfma_mode()) if fused else 0
     peak = agent_peak(a.n, a.m, a.L, mode, onehot=onehot)
@@ -87,42 +113,64 @@ def agent_roofline(a, E, sel_ms):
             "frac": round(tfs / peak, 4), "traffic": None,
             "peak_note": ("f32-equivalent: GRU products on three-way-split bf16 MFMAs (2.5 PF / 6), fc1/fc2 "
                           "on f32 MFMAs (157.3 TF), time-weighted" if mode else "f32 MFMA peak"),
-            "kernel": ("asg::rnn_agent_lds_kernel" if a.agent == "rnn_fused" else "torch agent + selector")
-            if a.selector == "eps" else f"{a.agent} forward + asg::sap_select_kernel (whole selection)",
-            "kernel_ms": round(sel_ms, 4), "flops_per_launch": flops}
+            "kernel": kernel, "kernel_ms": round(agent_ms, 4), "flops_per_launch": flops}
 
 
-def parse():
+def pmc_lookup(pattern, **match):
+    """First profiles/ summary matching the workload keys (n, m, E, L), else None."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+        try:
+            pm = json.load(open(path))
+        except (ValueError, OSError):
+            continue
+        if all(pm.get(k) == v for k, v in match.items()):
+            return pm
+    return None
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=60)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--envs", type=int, default=16384, help="envs per GPU")
-    p.add_argument("--n", type=int, default=64)
-    p.add_argument("--m", type=int, default=64)
+    p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    p.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    p.add_argument("--n", type=int, default=None)
+    p.add_argument("--m", type=int, default=None)
     p.add_argument("--T", type=int, default=20)
     p.add_argument("--L", type=int, default=3)
-    p.add_argument("--selector", default="eps", choices=["eps", "sap", "random"])
-    p.add_argument("--benefits", default="bump", choices=["bump", "dense"])
+    p.add_argument("--selector", default=None, choices=["eps", "sap", "random"])
+    p.add_argument("--benefits", default=None, choices=["bump", "dense"])
+    p.add_argument("--agent", default=None, choices=["rnn_fused", "rnn"],
+                   help="rnn_fused: the same RNNAgent (weights, fp32) with its inference forward as one HIP kernel")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-episodes", type=int, default=2, help="minimum CPU-baseline episodes")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample length (s)")
-    p.add_argument("--agent", default="rnn_fused", choices=["rnn_fused", "rnn"],
-                   help="rnn_fused: the same RNNAgent (weights, fp32) with its inference forward as one HIP kernel")
+    p.add_argument("--cpu-workers", type=int, default=None,
+                   help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
+    p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    return p.parse_args()
+    a = p.parse_args(argv)
+    cfg = CONFIGS[a.config]
+    for k in ("n", "m", "envs", "selector", "agent", "benefits"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    return a
 
 
-def make_args(a, E):
-    sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy"}[a.selector]
+def make_args(a, E, selector=None, agent=None):
+    selector = selector or a.selector
+    sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy"}[selector]
     return SimpleNamespace(
         batch_size_run=E, env="mock_constellation_env",
         env_args=dict(n=a.n, m=a.m, T=a.T, L=a.L, lambda_=0.5, bids_as_actions=False, seed=a.seed,
                       benefits=a.benefits),
         env_rng="philox", env_quirks=(), runner_protocol="episode", test_nepisode=1,
         runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, hidden_dim=64, use_rnn=True,
-        obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel, agent=a.agent,
-        epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac")
+        obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
+        agent=agent or a.agent, seed=a.seed,
+        epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac",
+        reuse_batch=True)
 
 
 class NullLogger:
@@ -130,53 +178,71 @@ class NullLogger:
         pass
 
 
-def main():
-    a = parse()
+def cpu_baseline(a):
+    """The reference's CPU design on this host (oracle/cpu_parallel_runner.py), SURVEY §8(d):
+    one worker process per env, batch_size_run = os.cpu_count() capped at the GPU's CPU
+    share; rates with resets amortised and for the step loop alone."""
+    from oracle import oracle as ora
+    from oracle.cpu_parallel_runner import run_parallel_baseline
+    host = os.cpu_count() or 1
+    workers = a.cpu_workers or min(host, CPU_WORKER_CAP)
+    rate, steps_done, secs, reset_secs = run_parallel_baseline(
+        n=a.n, m=a.m, T=a.T, L=a.L, workers=workers, episodes=a.cpu_episodes, epsilon=0.05,
+        min_seconds=a.cpu_seconds)
+    # second, stronger CPU number: the C oracle env, multi-threaded, random policy (env only)
+    c_envs = 4096 if a.n * a.m <= 4096 else 256
+    c_secs, _ = ora.rollout_random(c_envs, a.n, a.m, a.T, a.L, 0.5, a.seed, workers, 1)
+    return {"value": round(rate, 2), "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "host_cores": host, "workers": workers,
+            "worker_cap_note": f"batch_size_run = min(os.cpu_count()={host}, {CPU_WORKER_CAP}): the gpurun box "
+                               f"allots {CPU_WORKER_CAP} CPUs per GPU while os.cpu_count() reports the whole host",
+            "value_step_loop_only": round(steps_done / max(1e-9, secs - reset_secs), 2),
+            "value_reset_amortised": round(rate, 2),
+            "sample": f"{steps_done // (workers * a.T)} episodes x {workers} subprocess envs x T={a.T} at "
+                      f"{a.n}x{a.m} ({steps_done} env-steps, {secs:.1f} s, {reset_secs:.1f} s of it in resets): "
+                      f"the reference's ParallelRunner design (Pipe protocol, numpy env, CPU RNN agent + "
+                      f"eps-greedy, 1 torch thread; oracle/cpu_parallel_runner.py)",
+            "c_env_only": {"value": round(c_envs * a.T / c_secs, 1), "unit": "env-steps/s", "cores": workers,
+                           "kind": "port", "sample": f"{c_envs} envs x 1 episode, random policy, C oracle "
+                                                     f"(oracle/asg_rollout.c), no agent network"}}
+
+
+def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_lsa=False):
+    """Build runner + MAC for one workload and time `steps` transitions after `warmup`.
+    Returns elapsed seconds (max over ranks) and mean HIP-event times of the env step, the
+    whole selection, and (SAP) the selector kernel alone."""
     from marl_sap_amd import dist as asg_dist
-    rank, world = asg_dist.init_from_env()
-    # CPU baseline first: its worker processes are forked before this process touches
-    # the GPU
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_baseline:
-        from oracle import oracle as ora
-        from oracle.cpu_parallel_runner import run_parallel_baseline
-        workers = 8
-        rate, steps_done, secs = run_parallel_baseline(n=a.n, m=a.m, T=a.T, L=a.L, workers=workers,
-                                                       episodes=a.cpu_episodes, epsilon=0.05,
-                                                       min_seconds=a.cpu_seconds)
-        # second, stronger CPU number: the C oracle env, multi-threaded, random policy (env only)
-        c_envs = 4096 if a.n * a.m <= 4096 else 256
-        c_secs, _ = ora.rollout_random(c_envs, a.n, a.m, a.T, a.L, 0.5, a.seed, workers, 1)
-        cpu = {"value": round(rate, 2), "unit": "env-steps/s", "cores": workers + 1, "kind": "port",
-               "sample": f"{steps_done // (workers * a.T)} episodes x {workers} subprocess envs x T={a.T} at "
-                         f"{a.n}x{a.m} ({steps_done} env-steps, {secs:.1f} s): the reference's ParallelRunner design "
-                         f"(Pipe protocol, numpy env, CPU RNN agent + eps-greedy; oracle/cpu_parallel_runner.py)",
-               "c_env_only": {"value": round(c_envs * a.T / c_secs, 1), "unit": "env-steps/s", "cores": workers,
-                              "kind": "port", "sample": f"{c_envs} envs x 1 episode, random policy, C oracle "
-                                                        f"(oracle/asg_rollout.c), no agent network"}}
-
-    local = asg_dist.local_device_index()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    torch.manual_seed(a.seed + rank)
-
     from marl_sap_amd.controllers import REGISTRY as mac_REGISTRY
     from marl_sap_amd.runners import REGISTRY as r_REGISTRY
 
-    E = a.envs
-    args = make_args(a, E)
+    selector = selector or a.selector
+    args = make_args(a, E, selector, agent)
     runner = r_REGISTRY["gpu"](args, NullLogger())
     env = runner.get_env()
+    torch.manual_seed(a.seed)  # identical agent weights on every rank
     mac = mac_REGISTRY["basic_mac"](env.scheme, {"agents": a.n}, args)
     mac.to(dev)
     runner.setup(env.scheme, {"agents": a.n}, env.preprocess, mac)
 
-    ev_pairs = []   # (start, end) HIP events around each env step kernel in the timed region
-    sel_pairs = []  # ... and around each action selection (agent forward + selector)
+    ev_pairs, sel_pairs, lsa_pairs = [], [], []
     state = {"t": a.T, "timing": False}
+    sel_obj = mac.action_selector
+    inner = sel_obj.select_action
+
+    def timed_select(*args_, **kw):  # the selector call alone (SAP: noise + LSA kernel)
+        if not state["timing"]:
+            return inner(*args_, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = inner(*args_, **kw)
+        e1.record()
+        lsa_pairs.append((e0, e1))
+        return out
+
+    if selector == "sap":
+        sel_obj.select_action = timed_select
 
     def one_step():
-        """One transition of all envs; resets / finishes episodes at boundaries."""
         if state["t"] >= a.T:
             if runner.batch is not None and runner.env.k == a.T:
                 runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
@@ -185,33 +251,32 @@ def main():
             state["t"] = 0
         t = state["t"]
         with torch.no_grad():
-            if state["timing"]:
+            timing = state["timing"]
+            if timing:
                 a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a0.record()
-            if a.selector == "random":
+            if selector == "random":
                 env.random_actions(runner.batch, ts=t)
             else:
                 runner.select_into_batch(t)
-            if state["timing"]:
+            if timing:
                 a1.record()
                 sel_pairs.append((a0, a1))
-            if state["timing"]:
-                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s0.record()
-                env.step(runner.batch, ts=t)
+            env.step(runner.batch, ts=t)
+            if timing:
                 s1.record()
                 ev_pairs.append((s0, s1))
-            else:
-                env.step(runner.batch, ts=t)
         state["t"] = t + 1
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         one_step()
     asg_dist.barrier()
     torch.cuda.synchronize()
     state["timing"] = True
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         one_step()
     torch.cuda.synchronize()
     asg_dist.barrier()
@@ -220,50 +285,135 @@ def main():
     if runner.env.k == a.T:
         runner.finish_episode(sync=False)
     runner.flush_pending()  # surfaces any sticky device error of the timed steps
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev_pairs) / max(1, len(ev_pairs))
-    sel_ms = sum(s.elapsed_time(e) for s, e in sel_pairs) / max(1, len(sel_pairs))
-
+    mean = lambda prs: sum(s.elapsed_time(e) for s, e in prs) / len(prs) if prs else 0.0  # noqa: E731
+    res = {"elapsed": elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
+           "lsa_ms": mean(lsa_pairs) if lsa_pairs else None}
+    if count_lsa and selector == "sap" and a.n <= a.m <= 64:
+        # one more selection on the current state, with the step-counting kernel instance
+        sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
+        t = state["t"] if state["t"] < a.T else 0
+        with torch.no_grad():
+            if state["t"] >= a.T:
+                runner.reset()
+                mac.init_hidden(E)
+            mac.select_actions(runner.batch, t_ep=t, t_env=runner.t_env)
+        res["path_steps_per_launch"] = int(sel_obj.count_steps.sum().item())
+        sel_obj.count_steps = None
     if world > 1:
         import torch.distributed as tdist
-        t = torch.tensor([elapsed, kern_ms, sel_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([res["elapsed"], res["kern_ms"], res["sel_ms"]], dtype=torch.float64, device=dev)
         if tdist.get_backend() == "gloo":
             t = t.cpu()
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed, kern_ms, sel_ms = float(t[0]), float(t[1]), float(t[2])
+        res["elapsed"], res["kern_ms"], res["sel_ms"] = float(t[0]), float(t[1]), float(t[2])
+    res["global_envs"] = runner.global_envs
+    runner.close_env()
+    del runner, mac, env
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
-    total_steps = world * E * a.steps
-    value = total_steps / elapsed
+
+def lsa_roofline(a, E, res):
+    """SAP selector efficiency: augmenting-path steps (scipy's inner-loop iterations, counted
+    by the instrumented kernel instance on one selection) per second of the fused
+    noise + LSA kernel, as cycles per step per SIMD; against the VALU issue bound when a
+    PMC summary (SQ_INSTS_VALU of sap_select_kernel) exists in profiles/."""
+    steps, lsa_ms = res.get("path_steps_per_launch"), res.get("lsa_ms")
+    if not steps or not lsa_ms:
+        return None
+    per_s = steps / (lsa_ms * 1e-3)
+    cyc = SIMDS * CLOCK_HZ * lsa_ms * 1e-3 / steps
+    out = {"bound": "valu-issue", "kernel": "asg::sap_select_kernel", "kernel_ms": round(lsa_ms, 4),
+           "path_steps_per_launch": steps, "path_steps_per_s": round(per_s, 1),
+           "cycles_per_step_per_simd": round(cyc, 1), "achieved": None, "peak": None, "frac": None,
+           "unit": "wave-VALU-instr/s", "traffic": None}
+    pm = pmc_lookup("pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
+    if pm and pm.get("valu_insts_per_path_step"):
+        vps = pm["valu_insts_per_path_step"]
+        peak = SIMDS * CLOCK_HZ / VALU_CYCLES_PER_WAVE_INSTR
+        ach = vps * per_s
+        out.update({"achieved": round(ach / 1e9, 2), "peak": round(peak / 1e9, 2), "unit": "G wave-VALU-instr/s",
+                    "frac": round(ach / peak, 4), "valu_insts_per_path_step": round(vps, 2),
+                    "issue_bound_cycles_per_step": round(vps * VALU_CYCLES_PER_WAVE_INSTR, 1)})
+    return out
+
+
+def main():
+    a = parse()
+    from marl_sap_amd import dist as asg_dist
+    rank, world = asg_dist.init_from_env()
+    # CPU baseline first: its worker processes are forked before this process touches the GPU
+    cpu = cpu_baseline(a) if rank == 0 and world == 1 and a.cpu_baseline else None
+
+    local = asg_dist.local_device_index()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    E = a.envs
+    res = run_leg(a, dev, world, E, a.steps, a.warmup, count_lsa=True)
+    G = res["global_envs"]
+    value = G * a.steps / res["elapsed"]
+    kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     per_launch = step_bytes(a.n, a.m, a.L) * E
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("n") == a.n and pm.get("m") == a.m and pm.get("E") == E and pm.get("L") == a.L:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+    pm = pmc_lookup("pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    traffic = pm.get("hbm_bytes_per_launch") if pm else None
 
+    secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))
+    extra = {}
+    if secondary:
+        sk, sw = max(10, a.steps // 2), max(5, a.warmup // 2)
+        if a.selector != "random":
+            r2 = run_leg(a, dev, world, E, sk, sw, selector="eps", agent="rnn")
+            extra["pytorch_agent"] = {
+                "value": round(r2["global_envs"] * sk / r2["elapsed"], 1), "unit": "env-steps/s",
+                "ms_per_step": round(r2["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                "what": "configs[2] read literally: BasicMAC + the PyTorch RNNAgent module (hipBLASLt linears + "
+                        "GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
+                "select_ms": round(r2["sel_ms"], 4), "env_step_ms": round(r2["kern_ms"], 4)}
+        if a.n <= a.m <= 64 and a.selector != "sap":
+            r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn_fused", count_lsa=True)
+            agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)
+            extra["sap"] = {
+                "value": round(r3["global_envs"] * sk / r3["elapsed"], 1), "unit": "env-steps/s",
+                "ms_per_step": round(r3["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                "what": "SequentialAssignmentProblemSelector (eps 0.05): fused RNNAgent forward kernel, then "
+                        "asg_sap_select (per-env Gaussian noise + scipy-exact LSA, one wave64 per env)",
+                "env_step_ms": round(r3["kern_ms"], 4), "agent_ms": round(agent_ms, 4),
+                "roofline_lsa": lsa_roofline(a, E, r3),
+                "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_lds_kernel (forward only)")}
+
+    if a.selector == "random":
+        ra = None
+    elif a.selector == "sap":
+        ra = agent_roofline(a, E, sel_ms - (res["lsa_ms"] or 0.0), f"{a.agent} forward")
+    else:
+        ra = agent_roofline(a, E, sel_ms, "asg::rnn_agent_lds_kernel (forward + eps-greedy)"
+                            if a.agent == "rnn_fused" else "torch RNNAgent + asg_epsilon_greedy")
     if rank == 0:
+        sel_name = {"eps": "epsilon-greedy", "sap": "SAP", "random": "random"}[a.selector]
         line = {
-            "metric": "env steps/sec (whole node), 64-agent assignment env, 1/2/4/8 MI355X",
+            "metric": f"env steps/sec (whole node), {a.n}-agent assignment env, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "warmup": a.warmup, "ms_per_step": round(res["elapsed"] / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (Philox bump benefits, random-init RNN agent)",
-            "config": {"workload": f"{a.n}-agent/{a.m}-task assignment env, {E} envs per GPU, T={a.T}, L={a.L}, "
-                                   f"BasicMAC+{a.agent}(GRU 64, fp32) + {args.action_selector if a.selector != 'random' else 'random'} "
-                                   f"selector, {a.benefits} benefits",
-                       "envs_per_gpu": E, "global_envs": world * E, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
-                       "parallelism": f"env-sharded x{world} (RCCL gather of returns per episode)"},
+            "data": f"synthetic (Philox {a.benefits} benefits, random-init RNN agent)",
+            "config": {"workload": CONFIGS[a.config]["label"] + f"; T={a.T}, L={a.L}, "
+                                   f"BasicMAC+{a.agent}(GRU 64, fp32) + {sel_name} selector, {a.benefits} benefits",
+                       "baseline_config_index": 3 if (a.config == 2 and world > 1) else a.config,
+                       "envs_per_gpu": E, "global_envs": G, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
+                       "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "asg::step_kernel", "kernel_ms": round(kern_ms, 4),
                          "bytes_per_launch": per_launch},
-            "roofline_agent": agent_roofline(a, E, sel_ms),
+            "roofline_agent": ra,
             "cpu_baseline": cpu,
         }
+        if a.selector == "sap":
+            line["roofline_lsa"] = lsa_roofline(a, E, res)
+        if extra:
+            line["secondary"] = extra
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as tdist

@@ -153,8 +153,15 @@ int asg_sync_status(asg_handle *h);
 /* Constant benefit table, reference layout [E][n][m][T] float64 (host or device ptr). */
 int asg_set_benefits(asg_handle *h, const double *table, int64_t count, int on_device);
 /* The current episode's benefit table [E][n][m][T] float64 into a device buffer
- * (materialises Philox/bump draws; a debugging and parity aid). */
+ * (materialises Philox/bump draws in float64; a debugging and parity aid). */
 int asg_export_benefits(asg_handle *h, double *out_dev);
+/* Philox modes: the current episode's bump parameters [E][n][m][3] float32 (scale -- 0 for an
+ * inactive pair --, center, a2) into a device buffer: value(t) = scale * 2^(-(t - center)^2 * a2),
+ * a2 = log2(e) / (2 sigma_2) (mock_constellation_env.py:293).  Observations and beta hold a
+ * float32 evaluation within 1e-6 relative of the float64 value (exp results below FLT_MIN
+ * flush to 0); rewards,
+ * the beta_hat mask and asg_export_benefits use the float64 evaluation. */
+int asg_export_bump_params(asg_handle *h, float *out_dev);
 /* Current internal prev_assigns [E][n] (int64, device buffer). */
 int asg_export_prev_assigns(asg_handle *h, int64_t *out_dev);
 /* Per-env float64 returns accumulated since the last reset [E] (device buffer). */
@@ -192,21 +199,25 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
  * float picked_actions).  Q [B][n][m] f32, any strides.  status_out [B] int32 (0,
  * ASG_E_LSA_INVALID for NaN / +inf entries, ASG_E_LSA_INFEASIBLE), may be NULL; failed envs
  * get -1 rows.  ASG_E_INVALID_ARG when n > m or m > 64 (the Python selector then adds the
- * noise with torch and calls asg_lsa_batched). */
+ * noise with torch and calls asg_lsa_batched).  path_steps_out [B] int32 (may be NULL):
+ * an instrumented instance also writes each env's count of augmenting-path steps (scipy's
+ * inner-loop iterations), for the LSA efficiency figure; same assignments. */
 int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                    double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
-                   float *col_out, int32_t *status_out, void *hip_stream);
+                   float *col_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
 
 /* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
  * per row, with probability epsilon a uniformly random available action, else the first
  * maximal available Q (NaN propagates as in torch.max).  Randomness: Philox keyed by
- * (seed, counter, row).  out [B][n] int64 (strided, e.g. the EpisodeBatch actions row);
+ * (seed, counter, global row = (env_index_base + b) * n + i), so a rank holding envs
+ * [env_index_base, env_index_base + B) draws exactly what a 1-GPU run draws for them.
+ * out [B][n] int64 (strided, e.g. the EpisodeBatch actions row);
  * status [1] int32 device word set to ASG_E_INVALID_ARG if a row with no available action
  * had to explore (torch's Categorical would raise).  May be NULL. */
 int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon,
-                       uint64_t seed, uint64_t counter, int64_t *out, const int64_t out_strides[2],
-                       int32_t *status, void *hip_stream);
+                       uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *out,
+                       const int64_t out_strides[2], int32_t *status, void *hip_stream);
 
 /* RNNAgent forward (inference) for R agent rows in one fused f32-MFMA kernel:
  *   x = relu(X W1^T + b1); GRUCell(x, h) (use_rnn) or relu(x W_ih^T + b_ih); q = h' W2^T + b2.
@@ -235,14 +246,14 @@ int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, co
  * (q_out may be NULL).  Rows are (env, agent) = (row / n, row % n); avail [env][agent][m]
  * bool with strides avail_strides = {env, agent} (task stride 1); actions written to
  * out[env * out_strides[0] + agent * out_strides[1]] (int64).  Same Philox stream as
- * asg_epsilon_greedy for equal (seed, counter): identical actions. */
+ * asg_epsilon_greedy for equal (seed, counter, env_index_base): identical actions. */
 int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,
                          int64_t h_stride, const void *packed, const float *b1, const float *b_ih,
                          const float *b_hh, const float *b2, int hidden, int n_out, int use_rnn,
                          float *h_out, float *q_out, const uint8_t *avail,
                          const int64_t avail_strides[2], int n, double epsilon, uint64_t seed,
-                         uint64_t counter, int64_t *out, const int64_t out_strides[2],
-                         int32_t *status, void *hip_stream);
+                         uint64_t counter, int64_t env_index_base, int64_t *out,
+                         const int64_t out_strides[2], int32_t *status, void *hip_stream);
 
 /* ==== RealConstellationEnv ======================================
  * Batched form of src/envs/real_constellation_env.py with injected benefits

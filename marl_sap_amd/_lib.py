@@ -33,7 +33,7 @@ _DTYPES = {torch.float32: ASG_F32, torch.float64: ASG_F64, torch.int64: ASG_I64,
 # every symbol include/asg.h declares (checked by tests/test_abi.py)
 EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "asg_set_stream",
            "asg_reset", "asg_step", "asg_random_actions", "asg_sync_status", "asg_set_benefits",
-           "asg_export_benefits", "asg_export_prev_assigns", "asg_get_returns", "asg_get_step",
+           "asg_export_benefits", "asg_export_bump_params", "asg_export_prev_assigns", "asg_get_returns", "asg_get_step",
            "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_sap_select", "asg_epsilon_greedy",
            "asg_rnn_agent_packed_size", "asg_rnn_agent_mfma_mode", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
            "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
@@ -105,6 +105,7 @@ def lib():
         L.asg_sync_status.argtypes = [vp]
         L.asg_set_benefits.argtypes = [vp, vp, i64, i32]
         L.asg_export_benefits.argtypes = [vp, vp]
+        L.asg_export_bump_params.argtypes = [vp, vp]
         L.asg_export_prev_assigns.argtypes = [vp, vp]
         L.asg_get_returns.argtypes = [vp, vp]
         L.asg_get_step.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
@@ -112,16 +113,18 @@ def lib():
         L.asg_beta_hat.argtypes = [vp, i32, i64p, vp, i64p, i64, i32, i32, vp, dbl, vp, vp]
         L.asg_lsa_batched.argtypes = [vp, i32, i64p, i64, i32, i32, i32, vp, vp, vp, vp]
         L.asg_haa_select.argtypes = [vp, i64p, vp, i64p, i64, i32, i32, vp, dbl, vp, vp, vp]
-        L.asg_sap_select.argtypes = [vp, i64p, i64, i32, i32, dbl, ctypes.c_uint64, ctypes.c_uint64, i64, vp, vp, vp]
+        L.asg_sap_select.argtypes = [vp, i64p, i64, i32, i32, dbl, ctypes.c_uint64, ctypes.c_uint64, i64, vp, vp, vp,
+                                     vp]
         L.asg_epsilon_greedy.argtypes = [vp, i64p, vp, i64p, i64, i32, i32, dbl, ctypes.c_uint64, ctypes.c_uint64,
-                                         vp, i64p, vp, vp]
+                                         i64, vp, i64p, vp, vp]
         L.asg_rnn_agent_packed_size.argtypes = [i32, i32, i32, i32]
         L.asg_rnn_agent_mfma_mode.restype = i32
         L.asg_rnn_agent_pack.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
         L.asg_rnn_agent_forward.argtypes = [vp, i64, i64, i32, vp, i64] + [vp] * 5 + [i32, i32, i32, vp, vp, vp]
         L.asg_rnn_agent_select.argtypes = [vp, i64, i64, i32, vp, i64] + [vp] * 5 + [i32, i32, i32, vp, vp, vp, i64p,
                                                                                  i32, dbl, ctypes.c_uint64,
-                                                                                 ctypes.c_uint64, vp, i64p, vp, vp]
+                                                                                 ctypes.c_uint64, i64, vp, i64p, vp,
+                                                                                 vp]
         L.asg_real_create.argtypes = [ctypes.POINTER(AsgRealConfig), i32, vp, ctypes.POINTER(vp)]
         L.asg_real_destroy.argtypes = [vp]
         L.asg_real_destroy.restype = None

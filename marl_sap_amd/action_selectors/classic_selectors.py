@@ -9,6 +9,18 @@ from .. import _lib
 from ..components.epsilon_schedules import DecayThenFlatSchedule
 
 
+def selector_seed(args):
+    """64-bit Philox key of a selector: a function of args.seed alone."""
+    return (int(getattr(args, "seed", 0) or 0) * 0x9E3779B97F4A7C15 + 0x2545F4914F6CDD1D) & 0xFFFFFFFFFFFFFFFF
+
+
+def env_index_base(selector):
+    """Global index of this rank's env 0 (the runner's env_index_base), for draws keyed by
+    global env."""
+    envs = getattr(selector, "envs", None)
+    return int(getattr(envs, "env_index_base", getattr(selector.args, "env_index_base", 0)) or 0)
+
+
 class MultinomialActionSelector:
     def __init__(self, args):
         self.args = args
@@ -36,21 +48,28 @@ class EpsilonGreedyActionSelector:
         self.schedule = DecayThenFlatSchedule(args.epsilon_start, args.epsilon_finish, args.epsilon_anneal_time,
                                               decay="linear")
         self.epsilon = self.schedule.eval(0)
-        self.seed = int(getattr(args, "seed", 0) or 0) * 0x9E3779B1 + torch.initial_seed()
+        # the Philox key depends on args.seed only (not on the process's torch seed), and the
+        # draws are keyed by global (env, agent) row: every rank of a sharded rollout draws
+        # what a 1-GPU run draws for the same global envs
+        self.seed = selector_seed(args)
         self.calls = 0
         self.status = None
+        self.envs = None  # set by the runner (reference: run.py sets action_selector.envs)
+
+    def env_index_base(self):
+        return env_index_base(self)
 
     def fused_params(self, t_env, test_mode, device):
-        """Epsilon / seed / call counter / status word for a kernel that fuses this
-        selector into the agent forward (asg_rnn_agent_select); same state updates as
-        select_action."""
+        """Epsilon / seed / call counter / status word / global env base for a kernel that
+        fuses this selector into the agent forward (asg_rnn_agent_select); same state
+        updates as select_action."""
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:
             self.epsilon = self.args.evaluation_epsilon
         if self.status is None or self.status.device != device:
             self.status = torch.zeros(1, dtype=torch.int32, device=device)
         self.calls += 1
-        return self.epsilon, self.seed, self.calls, self.status
+        return self.epsilon, self.seed, self.calls, self.status, self.env_index_base()
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None, out=None):
         self.epsilon = self.schedule.eval(t_env)
@@ -68,7 +87,7 @@ class EpsilonGreedyActionSelector:
             _lib.check(_lib.lib().asg_epsilon_greedy(
                 ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), ctypes.c_void_p(av.data_ptr()),
                 _lib.i64arr(av.stride()), B, n, m, float(self.epsilon), self.seed & 0xFFFFFFFFFFFFFFFF, self.calls,
-                ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), ctypes.c_void_p(self.status.data_ptr()),
+                self.env_index_base(), ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), ctypes.c_void_p(self.status.data_ptr()),
                 _lib.stream_ptr(q.device)))
         return out
 

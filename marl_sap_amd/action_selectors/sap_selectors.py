@@ -7,6 +7,7 @@ import torch
 
 from .. import _lib
 from ..components.epsilon_schedules import DecayThenFlatSchedule
+from .classic_selectors import env_index_base, selector_seed
 from .lsa import DeferredStatus, linear_sum_assignment_batched
 
 
@@ -30,12 +31,15 @@ class SequentialAssignmentProblemSelector:
                                               decay="linear")
         self.epsilon = self.schedule.eval(0)
         self.status = DeferredStatus()
-        self.seed = int(getattr(args, "seed", 0) or 0) * 0x9E3779B1 + torch.initial_seed()
+        self.seed = selector_seed(args)
         self.calls = 0
         self.envs = None  # set by the runner (reference: run.py sets action_selector.envs)
+        # instrumentation (bench.py): an int32 [B] device tensor receives every env's count of
+        # augmenting-path steps of the next fused call
+        self.count_steps = None
 
     def _env_index_base(self):
-        return int(getattr(self.envs, "env_index_base", getattr(self.args, "env_index_base", 0)) or 0)
+        return env_index_base(self)
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None):
         self.epsilon = self.schedule.eval(t_env)
@@ -53,7 +57,9 @@ class SequentialAssignmentProblemSelector:
                 _lib.check(_lib.lib().asg_sap_select(
                     ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), B, n, m, float(self.epsilon),
                     self.seed & 0xFFFFFFFFFFFFFFFF, self.calls, self._env_index_base(),
-                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(q.device)))
+                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                    ctypes.c_void_p(self.count_steps.data_ptr()) if self.count_steps is not None else None,
+                    _lib.stream_ptr(q.device)))
             self.status.add(status)
             return out
         if self.epsilon > 0:

@@ -37,10 +37,10 @@ class BasicMAC:
             out = None  # e.g. the real env's int16 actions: the caller casts through update()
         if out is not None and self._fused_select_ok(bs):
             # agent forward + epsilon-greedy in one HIP kernel: Q never leaves the chip
-            eps, seed, counter, status = self.action_selector.fused_params(t_env, test_mode, out.device)
+            eps, seed, counter, status, base = self.action_selector.fused_params(t_env, test_mode, out.device)
             self.hidden_states = self.selector_agent.forward_select(
                 self._build_inputs(ep_batch, t_ep), self.hidden_states, avail_actions, self.n, eps, seed, counter,
-                out, status)
+                out, status, env_index_base=base)
             return out
         agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode, action_selection_mode=True)
         kw = {"out": out} if out is not None and _accepts_out(self.action_selector) else {}

@@ -274,6 +274,16 @@ int asg_export_benefits(asg_handle *h, double *out_dev) {
     return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_export_benefits");
 }
 
+int asg_export_bump_params(asg_handle *h, float *out_dev) {
+    if (!h || !out_dev) return fail(h, ASG_E_INVALID_ARG, "NULL argument");
+    if (!h->has_reset) return fail(h, ASG_E_STATE, "no episode yet: reset first");
+    if (h->st.rng_mode != ASG_RNG_PHILOX || h->st.benefit_mode == ASG_BENEFIT_INJECTED)
+        return fail(h, ASG_E_INVALID_ARG, "asg_export_bump_params: only Philox bump / dense benefits have parameters");
+    DeviceGuard g(h->device);
+    hipError_t e = asg::launch_export_bump_params(h->st, out_dev, h->stream);
+    return e == hipSuccess ? ASG_OK : hip_fail(h, e, "asg_export_bump_params");
+}
+
 int asg_export_prev_assigns(asg_handle *h, int64_t *out_dev) {
     if (!h || !out_dev) return fail(h, ASG_E_INVALID_ARG, "NULL argument");
     DeviceGuard g(h->device);
@@ -345,28 +355,30 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
 
 int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m, double epsilon,
                    uint64_t seed, uint64_t counter, int64_t env_index_base, float *col_out, int32_t *status_out,
-                   void *hip_stream) {
+                   int32_t *path_steps_out, void *hip_stream) {
     if (!q || !q_strides || !col_out || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select: bad arguments");
     if (n > m || m > 64) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select: needs n <= m <= 64");
     if (!(epsilon >= 0.0)) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select: epsilon must be >= 0");
     if (B == 0) return ASG_OK;
     hipError_t e = asg::launch_sap_select(q, q_strides, B, n, m, (float)epsilon, seed, (uint32_t)counter,
-                                          env_index_base, col_out, status_out, static_cast<hipStream_t>(hip_stream));
+                                          env_index_base, col_out, status_out, path_steps_out,
+                                          static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select");
 }
 
 int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
-                       uint64_t counter, int64_t *out, const int64_t out_strides[2], int32_t *status,
-                       void *hip_stream) {
-    if (!q || !q_strides || !avail || !avail_strides || !out || !out_strides || B < 0 || n <= 0 || m <= 0)
+                       uint64_t counter, int64_t env_index_base, int64_t *out, const int64_t out_strides[2],
+                       int32_t *status, void *hip_stream) {
+    if (!q || !q_strides || !avail || !avail_strides || !out || !out_strides || B < 0 || n <= 0 || m <= 0 ||
+        env_index_base < 0)
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_epsilon_greedy: bad arguments");
     if (!(epsilon >= 0.0 && epsilon <= 1.0))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_epsilon_greedy: epsilon must be in [0, 1]");
     if (B == 0) return ASG_OK;
     hipError_t e = asg::launch_eps_greedy(q, q_strides, avail, avail_strides, B, n, m, (float)epsilon, seed,
-                                          (uint32_t)counter, out, out_strides, status,
+                                          (uint32_t)counter, env_index_base * n, out, out_strides, status,
                                           static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_epsilon_greedy");
 }
@@ -413,9 +425,10 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
                          const void *packed, const float *b1, const float *b_ih, const float *b_hh, const float *b2,
                          int hidden, int n_out, int use_rnn, float *h_out, float *q_out, const uint8_t *avail,
                          const int64_t avail_strides[2], int n, double epsilon, uint64_t seed, uint64_t counter,
-                         int64_t *out, const int64_t out_strides[2], int32_t *status, void *hip_stream) {
+                         int64_t env_index_base, int64_t *out, const int64_t out_strides[2], int32_t *status,
+                         void *hip_stream) {
     if (!x || !packed || !b1 || !b_ih || !b2 || !h_out || !avail || !avail_strides || !out || !out_strides ||
-        !status || R < 0 || n <= 0 || (use_rnn && !b_hh))
+        !status || R < 0 || n <= 0 || env_index_base < 0 || (use_rnn && !b_hh))
         return fail(nullptr, ASG_E_INVALID_ARG, "asg_rnn_agent_select: bad arguments");
     if (!agent_shape_ok(K, hidden, n_out) || (x_stride != 0 && x_stride < K) || h_stride % 4 != 0 ||
         (reinterpret_cast<uintptr_t>(x) % 4) != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
@@ -425,8 +438,8 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
     if (R == 0) return ASG_OK;
     hipError_t e = asg::launch_rnn_agent_select(
         x, x_stride, R, K, h_in, h_stride, static_cast<const float4 *>(packed), b1, b_ih, b_hh, b2, n_out, use_rnn,
-        h_out, q_out, avail, avail_strides[0], avail_strides[1], n, (float)epsilon, seed, (uint32_t)counter, out,
-        out_strides[0], out_strides[1], status, static_cast<hipStream_t>(hip_stream));
+        h_out, q_out, avail, avail_strides[0], avail_strides[1], n, (float)epsilon, seed, (uint32_t)counter,
+        env_index_base * n, out, out_strides[0], out_strides[1], status, static_cast<hipStream_t>(hip_stream));
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_select");
 }
 

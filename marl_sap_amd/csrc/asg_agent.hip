@@ -751,7 +751,8 @@ __device__ __forceinline__ void agent_rows(
     bool explore = false;
     u32x4 rr = u32x4{0u, 0u, 0u, 0u};
     if (sel.epsilon > 0.0f) {
-        rr = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect, sel.counter}, sel.k0, sel.k1);
+        const int64_t grow = row + sel.row_base;  // global (env, agent) row: shard-invariant draws
+        rr = philox4x32_10(u32x4{(uint32_t)grow, (uint32_t)(grow >> 32), kCtrSelect, sel.counter}, sel.k0, sel.k1);
         constexpr float k2m24 = 5.9604644775390625e-08f;
         explore = ok[nt] && q < kNT && (float)(rr.x >> 8) * k2m24 < sel.epsilon;
     }
@@ -1096,9 +1097,10 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
                                    const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                    const float *b2, int nout, int use_rnn, float *Hout, float *Q,
                                    const uint8_t *avail, int64_t a0, int64_t a1, int n, float epsilon, uint64_t seed,
-                                   uint32_t counter, int64_t *out, int64_t o0, int64_t o1, int *err, hipStream_t s) {
+                                   uint32_t counter, int64_t row_base, int64_t *out, int64_t o0, int64_t o1, int *err,
+                                   hipStream_t s) {
     const SelectArgs sa{avail, a0, a1, n, epsilon, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5bd1e995u, counter,
-                        out, o0, o1, err};
+                        row_base, out, o0, o1, err};
     return launch_rnn_agent_fwd(X, xs, R, K, Hin, hs, packed, b1, bih, bhh, b2, nout, use_rnn, Hout, Q, &sa, s);
 }
 

@@ -69,15 +69,18 @@ __device__ __forceinline__ EnvKey env_key(uint64_t seed, int64_t global_env) {
                   (uint32_t)(seed >> 32) ^ (uint32_t)global_env};
 }
 
-// Bump parameters of one (agent i, task j) pair under Philox, evaluated in float32
-// (the distribution of generate_benefits_over_time, mock_constellation_env.py:281-293):
-// active with probability 0.25 (rand() > 0.75), center ~ U(0, T), width ~ U(wmin, wmax),
-// sigma_2 = sqrt(w^2 / -8 / ln 0.05), value(t) = scale * exp(-(t - c)^2 / sigma_2 / 2).
-// One Philox call per pair; the per-task scale (choice([1,1,1,10])) is a per-task draw.
+// Bump parameters of one (agent i, task j) pair under Philox (the distribution of
+// generate_benefits_over_time, mock_constellation_env.py:281-293): active with probability
+// 0.25 (rand() > 0.75), center ~ U(0, T), width ~ U(wmin, wmax),
+// sigma_2 = sqrt(w^2 / -8 / ln 0.05), value(t) = scale * exp(-(t - c)^2 / sigma_2 / 2)
+// = scale * 2^(-(t - c)^2 * a2) with a2 = log2(e) / (2 sigma_2).  One Philox call per pair;
+// the per-task scale (choice([1,1,1,10])) is a per-task draw.  The parameters are float32
+// values; the center is drawn on a grid of 2^-q with q = 24 - bits(T), so t - center is
+// exact in float32 for every integer t < T.
 struct Bump32 {
     float scale;  // 0 when the pair is inactive
     float center;
-    float a;      // 1 / (2 sigma_2)
+    float a2;     // log2(e) / (2 sigma_2)
 };
 
 __device__ __forceinline__ float philox_task_scale(EnvKey key, uint32_t episode, int j) {
@@ -92,16 +95,36 @@ __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, in
     const bool active = dense || r.x >= 0xC0000000u;
     Bump32 b;
     b.scale = active ? scale : 0.0f;
-    b.center = (float)T * ((float)r.y * k2m32);
+    // center = T * u on the 2^-q grid: floor(u * T * 2^q) * 2^-q, u = r.y * 2^-32 (< T * 2^q <= 2^24: exact)
+    const int q = 24 - (32 - __builtin_clz((unsigned)(T > 0 ? T : 1)));
+    b.center = __builtin_ldexpf((float)(((uint64_t)r.y * (uint64_t)(uint32_t)T) >> (32 - q)), -q);
     const float spread = wmin + (wmax - wmin) * ((float)r.z * k2m32);
     const float s2 = sqrtf(spread * spread / -8.0f / (float)kLog005);
-    b.a = 0.5f / s2;
+    b.a2 = 0.72134752044448170f / s2;  // log2(e) / 2 / sigma_2
     return b;
 }
 
+// float32 evaluation with an error that does not grow with the exponent: x = t - center is
+// exact, x^2 * a2 is carried as an unevaluated sum yh + yl (FMA error terms), and
+// 2^-(yh + yl) = 2^-yh * (1 - yl ln 2) to first order (|yl| <= 2^-23 yh).  Within 1e-6
+// relative of the float64 value (bump64_at) wherever 2^-yh >= FLT_MIN; below that
+// v_exp_f32 flushes to 0 (values < 10 FLT_MIN; tests/test_gpu_parity.py).
 __device__ __forceinline__ float bump32_at(const Bump32 &b, int t) {
     const float x = (float)t - b.center;
-    return b.scale * __expf(-(x * x) * b.a);
+    const float p = x * x;
+    const float pe = __builtin_fmaf(x, x, -p);
+    const float yh = p * b.a2;
+    const float yl = __builtin_fmaf(p, b.a2, -yh) + pe * b.a2;
+    constexpr float kLn2 = 0.69314718055994531f;
+    return b.scale * (__builtin_amdgcn_exp2f(-yh) * __builtin_fmaf(-yl, kLn2, 1.0f));
+}
+
+// The same bump in float64 (the reference's arithmetic, mock :293, on these parameters).
+// Used where a value is compared or accumulated in float64 -- the reward's beta_hat and its
+// `beta > 1e-12` mask (n values per step) -- and by the table export.
+__device__ __forceinline__ double bump64_at(const Bump32 &b, int t) {
+    const double x = (double)t - (double)b.center;
+    return (double)b.scale * exp2(-(x * x) * (double)b.a2);
 }
 
 // ---------------------------------------------------------------------------------

@@ -38,6 +38,7 @@ struct BumpSrc {  // Philox, float32 bumps regenerated on the fly (no table in H
         struct Pair {
             Bump32 b;
             __device__ float at(int t) const { return bump32_at(b, t); }
+            __device__ double at64(int t) const { return bump64_at(b, t); }
         };
         __device__ Pair pair(int i, int j) const {
             return Pair{philox_bump32(key, episode, i * m + j, scale[j], T, wmin, wmax, dense)};
@@ -66,6 +67,7 @@ struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
             const double *p;
             int64_t tstride;
             __device__ double at(int t) const { return p[t * tstride]; }
+            __device__ double at64(int t) const { return p[t * tstride]; }
         };
         __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, nm}; }
     };
@@ -274,7 +276,7 @@ __global__ void __launch_bounds__(256) ASG_STEP_VGPR_ATTR step_kernel(Src src, a
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int j = s_act[i];
         const int p = st.prev[e * n + i];
-        const double beta = (double)env.pair(i, j).at(k);
+        const double beta = env.pair(i, j).at64(k);  // float64: mask and reward exact on the parameters
         const double tt = st.T_trans ? st.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
         const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
         const double bh = beta - st.lambda_ * pen;
@@ -328,7 +330,26 @@ __global__ void export_table_kernel(Src src, EnvState st, double *out) {
     for (int p = threadIdx.x; p < n * m; p += blockDim.x) {
         const int i = p / m, j = p - i * m;
         const auto P = env.pair(i, j);
-        for (int t = 0; t < T; ++t) out[((e * n + i) * (int64_t)m + j) * T + t] = (double)P.at(t);
+        for (int t = 0; t < T; ++t) out[((e * n + i) * (int64_t)m + j) * T + t] = P.at64(t);
+    }
+}
+
+// Philox bump parameters [E][n][m][3] float32 = (scale (0: inactive pair), center, a2), the
+// values every bump evaluation uses (value(t) = scale * 2^(-(t - center)^2 * a2))
+__global__ void export_bump_params_kernel(BumpSrc src, EnvState st, float *out) {
+    extern __shared__ int s_dyn[];
+    float *s_scale = reinterpret_cast<float *>(s_dyn);
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m;
+    src.fill_scale(e, s_scale);
+    __syncthreads();
+    const auto env = src.bind(e, s_scale);
+    for (int p = threadIdx.x; p < n * m; p += blockDim.x) {
+        const Bump32 b = env.pair(p / m, p % m).b;
+        float *o = out + (e * n * (int64_t)m + p) * 3;
+        o[0] = b.scale;
+        o[1] = b.center;
+        o[2] = b.a2;
     }
 }
 
@@ -596,6 +617,12 @@ hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int
 
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
     hipLaunchKernelGGL(random_actions_kernel, dim3(st.E), dim3(64), 0, s, bv, st, ts, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_bump_params(const EnvState &st, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(export_bump_params_kernel, dim3(st.E), dim3(256), sizeof(float) * st.m, s, bump_src(st), st,
+                       out);
     return hipGetLastError();
 }
 

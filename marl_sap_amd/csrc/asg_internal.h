@@ -43,6 +43,7 @@ struct SelectArgs {
     int n;                 // agents per env
     float epsilon;
     uint32_t k0, k1, counter;
+    int64_t row_base;      // global row of row 0 (env_index_base * n): Philox keys by global row
     int64_t *out;          // actions (int64), (env, agent) strides o0, o1
     int64_t o0, o1;
     int *err;              // sticky: exploration over a row with no available action
@@ -52,6 +53,7 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s);
+hipError_t launch_export_bump_params(const EnvState &st, float *out, hipStream_t s);
 hipError_t launch_import_table(const double *in, int64_t src_envs, const EnvState &st, hipStream_t s);
 hipError_t launch_export_prev(const EnvState &st, int64_t *out, hipStream_t s);
 hipError_t launch_mt_seed(const EnvState &st, hipStream_t s);
@@ -65,14 +67,14 @@ hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], con
                            double *out, hipStream_t s);
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             hipStream_t s);
+                             int32_t *steps_out, hipStream_t s);
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s);
 
 hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t *avail, const int64_t as[3],
-                             int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter, int64_t *out,
-                             const int64_t os[2], int *err, hipStream_t s);
+                             int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter,
+                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s);
 
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
@@ -85,6 +87,7 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
                                    const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                    const float *b2, int nout, int use_rnn, float *Hout, float *Q,
                                    const uint8_t *avail, int64_t a0, int64_t a1, int n, float epsilon, uint64_t seed,
-                                   uint32_t counter, int64_t *out, int64_t o0, int64_t o1, int *err, hipStream_t s);
+                                   uint32_t counter, int64_t row_base, int64_t *out, int64_t o0, int64_t o1, int *err,
+                                   hipStream_t s);
 
 }  // namespace asg

@@ -175,9 +175,11 @@ hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3]
 // register-resident LSA (maximize).  The reference runs, per env on the host: abs, mean,
 // ones * avg * eps * 2, torch.normal, +=, scipy.
 // ------------------------------------------------------------------------------------
+template <bool kCount>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
-                                                        int64_t env_base, float *col_out, int32_t *status_out) {
+                                                        int64_t env_base, float *col_out, int32_t *status_out,
+                                                        int32_t *steps_out) {
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const float *col = q + b * q0 + (int64_t)lane * q2;
@@ -232,7 +234,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA
     float *co = col_out + b * n;
     if (status == ASG_OK) {
         int c4r[1];
-        status = lsa_solve_reg64(rc, n, m, c4r);
+        int nsteps = 0;
+        status = lsa_solve_reg64<RegCostF32, kCount>(rc, n, m, c4r, &nsteps);
+        if (kCount && lane == 0) steps_out[b] = nsteps;
         if (status == ASG_OK) lsa_emit_wave(c4r, n, m, nullptr, nullptr, nullptr, co);
     }
     if (status != ASG_OK)
@@ -242,9 +246,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA
 
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(sap_select_kernel, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon, seed,
-                       counter, env_base, col_out, status_out);
+                             int32_t *steps_out, hipStream_t s) {
+    if (steps_out)
+        hipLaunchKernelGGL(sap_select_kernel<true>, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon,
+                           seed, counter, env_base, col_out, status_out, steps_out);
+    else
+        hipLaunchKernelGGL(sap_select_kernel<false>, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon,
+                           seed, counter, env_base, col_out, status_out, steps_out);
     return hipGetLastError();
 }
 

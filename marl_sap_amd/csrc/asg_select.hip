@@ -16,7 +16,8 @@ template <bool VEC4>
 __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2,
                                                          const uint8_t *avail, int64_t a0, int64_t a1, int64_t a2,
                                                          int64_t B, int n, int m, float epsilon, uint32_t k0,
-                                                         uint32_t k1, uint32_t counter, int64_t *out, int64_t o0,
+                                                         uint32_t k1, uint32_t counter, int64_t row_base,
+                                                         int64_t *out, int64_t o0,
                                                          int64_t o1, int *err) {
     const int lane16 = threadIdx.x & 15;
     const int64_t rows = B * n;
@@ -68,7 +69,8 @@ __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t
     if (bj == 0x7fffffff) bj = 0;
     int action = bj;
     if (epsilon > 0.0f) {
-        const u32x4 r = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(row >> 32), kCtrSelect, counter}, k0, k1);
+        const int64_t grow = row + row_base;  // global (env, agent) row: shard-invariant draws
+        const u32x4 r = philox4x32_10(u32x4{(uint32_t)grow, (uint32_t)(grow >> 32), kCtrSelect, counter}, k0, k1);
         constexpr float k2m24 = 5.9604644775390625e-08f;  // 2^-24
         const bool pick = (float)(r.x >> 8) * k2m24 < epsilon;
         if (pick && cnt > 0) {
@@ -120,8 +122,8 @@ __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t
 }
 
 hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t *avail, const int64_t as[3],
-                             int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter, int64_t *out,
-                             const int64_t os[2], int *err, hipStream_t s) {
+                             int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter,
+                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s) {
     const int64_t threads = B * n * 16;
     const int64_t blocks = (threads + 255) / 256;
     const bool v4 = qs[2] == 1 && as[2] == 1 && (reinterpret_cast<uintptr_t>(q) % 16) == 0 &&
@@ -130,10 +132,10 @@ hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t 
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
     if (v4)
         hipLaunchKernelGGL(eps_greedy_kernel<true>, dim3(blocks), dim3(256), 0, s, q, qs[0], qs[1], qs[2], avail,
-                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, out, os[0], os[1], err);
+                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, row_base, out, os[0], os[1], err);
     else
         hipLaunchKernelGGL(eps_greedy_kernel<false>, dim3(blocks), dim3(256), 0, s, q, qs[0], qs[1], qs[2], avail,
-                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, out, os[0], os[1], err);
+                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, row_base, out, os[0], os[1], err);
     return hipGetLastError();
 }
 

@@ -267,11 +267,15 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
 // is a uniform branch plus one indexed move, and column removal is scalar mask work.
 // Identical decisions to lsa_solve_wave<1> (same keys, same tie rule, same float64
 // operation order); ~30 vector instructions per augmenting-path step instead of ~42.
-template <class Acc>
-__device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]) {
+// kCount: also count the augmenting-path steps (iterations of scipy's inner loop, the
+// figure ora_lsa_iterations reports) into *steps -- an instrumentation instance for the
+// LSA efficiency figure; the product instances compile it out.
+template <class Acc, bool kCount = false>
+__device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1], int *steps = nullptr) {
 #ifdef ASG_LSA_GENERIC_REG
     return lsa_solve_wave<1>(acc, nr, nc, col4row);
 #else
+    int nsteps = 0;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t colmask = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);  // lanes that hold a column
     const float kInfF = __builtin_inff();
@@ -287,6 +291,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
         bool infeasible = false;
         do {
             i = __builtin_amdgcn_readfirstlane(i);
+            if (kCount) ++nsteps;
             const double ui = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
                                                               (int)(uint32_t)__builtin_bit_cast(uint64_t, u), i)) |
                                                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
@@ -366,6 +371,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
         }
     }
     col4row[0] = c4r;
+    if (kCount) *steps = nsteps;
     return ASG_OK;
 #endif
 }

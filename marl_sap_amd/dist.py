@@ -36,16 +36,45 @@ def local_device_index():
     return int(os.environ.get("LOCAL_RANK", "0")) % max(1, n)
 
 
-def all_gather_returns(local):
-    """[E] per-rank returns -> [world * E] in global env order."""
+def all_gather_returns(local, counts=None):
+    """[E_r] per-rank returns -> [sum_r E_r] in global env order.  counts: every rank's
+    E_r (from envs_per_rank); equal counts (the sharded rollout) take one
+    all_gather_into_tensor, ragged ones are padded to the largest shard and stripped."""
     rank, world = rank_world()
     if world == 1:
         return local
     if dist.get_backend() == "gloo" and local.is_cuda:
         local = local.cpu()
-    out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, local.contiguous())
-    return out
+    local = local.contiguous()
+    if counts is None or len(set(counts)) == 1:
+        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local)
+        return out
+    mx = max(counts)
+    pad = torch.zeros(mx, dtype=local.dtype, device=local.device)
+    pad[:local.numel()] = local
+    out = torch.empty(world * mx, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    return torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
+
+
+def envs_per_rank(local_envs):
+    """Every rank's env count (one all-gather at runner construction): the env-step
+    counter of an episode is T * sum(E_r), the reference's per-env accounting
+    (parallel_runner.py:178-179, :220-221) summed over ranks."""
+    rank, world = rank_world()
+    if world == 1:
+        return [int(local_envs)]
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([int(local_envs)], dtype=torch.int64, device=dev)
+    out = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return [int(x) for x in out.tolist()]
+
+
+def env_index_base(counts, rank):
+    """Global index of this rank's env 0: envs [sum(counts[:rank]), ... + counts[rank])."""
+    return int(sum(counts[:rank]))
 
 
 def all_reduce_sum(value):

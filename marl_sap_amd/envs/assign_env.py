@@ -173,6 +173,12 @@ class AssignEnvBatch(MultiAgentEnv):
         self._call("asg_export_benefits", ctypes.c_void_p(out.data_ptr()))
         return out
 
+    def export_bump_params(self):
+        """Philox modes: float32 [E, n, m, 3] (scale, center, a) of the current episode."""
+        out = torch.empty((self.num_envs, self.n, self.m, 3), dtype=torch.float32, device=self.device)
+        self._call("asg_export_bump_params", ctypes.c_void_p(out.data_ptr()))
+        return out
+
     def export_prev_assigns(self):
         out = torch.empty((self.num_envs, self.n), dtype=torch.int64, device=self.device)
         self._call("asg_export_prev_assigns", ctypes.c_void_p(out.data_ptr()))

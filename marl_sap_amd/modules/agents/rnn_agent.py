@@ -81,9 +81,11 @@ class RNNFusedAgent(RNNAgent):
             _lib.check(_lib.lib().asg_rnn_agent_forward(*args, p(q), _lib.stream_ptr(x.device)))
         return q, h_out
 
-    def forward_select(self, inputs, hidden_state, avail, n, epsilon, seed, counter, out, status, q_out=None):
+    def forward_select(self, inputs, hidden_state, avail, n, epsilon, seed, counter, out, status, q_out=None,
+                       env_index_base=0):
         """forward + epsilon-greedy in one kernel (asg_rnn_agent_select): actions into `out`
-        ([B, n] int64 view, e.g. the EpisodeBatch actions row); avail [B, n, m] bool.
+        ([B, n] int64 view, e.g. the EpisodeBatch actions row); avail [B, n, m] bool;
+        env_index_base: global index of env 0 (exploration draws are keyed by global row).
         Returns the new hidden state [B*n, hidden]."""
         x, h, hs = self._prep(inputs, hidden_state)
         if avail.dtype != torch.bool or avail.stride(-1) != 1:
@@ -92,7 +94,7 @@ class RNNFusedAgent(RNNAgent):
             h_out, args, p = self._common(x, h, hs)
             _lib.check(_lib.lib().asg_rnn_agent_select(
                 *args, p(q_out), p(avail), _lib.i64arr(avail.stride()[:2]), n, float(epsilon),
-                seed & 0xFFFFFFFFFFFFFFFF, counter, p(out), _lib.i64arr(out.stride()), p(status),
+                seed & 0xFFFFFFFFFFFFFFFF, counter, int(env_index_base), p(out), _lib.i64arr(out.stride()), p(status),
                 _lib.stream_ptr(x.device)))
         return h_out
 

@@ -9,9 +9,11 @@ in HBM behind one C-ABI handle and every step is:
     mac.select_actions (PyTorch-ROCm)  ->  actions row write  ->  asg_step (one HIP kernel)
 
 with the EpisodeBatch kept resident on the GPU in time-major storage.  Under
-torch.distributed (one process per GPU, RCCL) each rank owns envs
-[rank*E, (rank+1)*E); the only collective is once per episode: an all-gather of the
-float64 episode returns and an all-reduce of the env-step counter.
+torch.distributed (one process per GPU, RCCL) each rank owns the contiguous global envs
+[sum(E_<r), sum(E_<r) + E_r) -- [rank*E, (rank+1)*E) for equal shards; the rank env counts
+are all-gathered once at construction, so the env-step counter of an episode is
+T * sum_r E_r on every rank without a per-episode collective.  The only per-episode
+collective is an all-gather of the float64 episode returns.
 
 Protocols (args.runner_protocol):
   "episode"  EpisodeRunner semantics per env: T selection passes, true terminated flag,
@@ -36,15 +38,20 @@ class GpuVecRunner:
         self.batch_size = args.batch_size_run
         self.rank, self.world = asg_dist.rank_world()
         self.device = torch.device("cuda", torch.cuda.current_device())
+        self.rank_envs = asg_dist.envs_per_rank(self.batch_size)
+        self.global_envs = sum(self.rank_envs)
         env_args = dict(args.env_args)
         env_args.pop("seed", None)
         self.env = BATCHED_REGISTRY[args.env](
             **env_args, seed=args.env_args.get("seed", 0) or 0, num_envs=self.batch_size,
-            env_index_base=self.rank * self.batch_size, device=self.device,
+            env_index_base=asg_dist.env_index_base(self.rank_envs, self.rank), device=self.device,
             rng=getattr(args, "env_rng", "philox"), quirks=tuple(getattr(args, "env_quirks", ())))
         self.T = self.env.T
         self.protocol = getattr(args, "runner_protocol", "episode")
-        self.reuse_batch = getattr(args, "reuse_batch", True)
+        # reuse_batch: one EpisodeBatch allocated once and overwritten by every run() (the
+        # throughput loops opt in); off by default, so run() returns a fresh batch per
+        # episode as the reference runners' new_batch() does
+        self.reuse_batch = getattr(args, "reuse_batch", False)
         self.t = 0
         self.t_env = 0
         self.train_returns, self.test_returns = [], []
@@ -115,11 +122,12 @@ class GpuVecRunner:
         snapshot and its all-gather and advance the counters; the host sync, error checks
         and host-side statistics wait for flush_pending() (the GPU never idles at episode
         boundaries)."""
-        returns = asg_dist.all_gather_returns(self.env.get_returns())
+        returns = asg_dist.all_gather_returns(self.env.get_returns(), self.rank_envs)
         self._pending.append((returns, test_mode))
-        # every rank steps batch_size envs for T steps (the all-reduced counter of the
-        # reference's per-env accounting, parallel_runner.py:178-179, without a sync)
-        steps = self.batch_size * self.world * self.T
+        # every env of every rank ran T steps (the reference's per-env accounting,
+        # parallel_runner.py:178-179, summed over ranks: the env counts were all-gathered
+        # at construction, so no per-episode collective or sync is needed)
+        steps = self.global_envs * self.T
         if not test_mode:
             self.t_env += steps
         self._pending_steps.append(steps)
@@ -140,7 +148,7 @@ class GpuVecRunner:
             cur_stats = self.test_stats if test_mode else self.train_stats
             cur_returns = self.test_returns if test_mode else self.train_returns
             log_prefix = "test_" if test_mode else ""
-            n_eps = self.batch_size * self.world
+            n_eps = self.global_envs
             cur_stats["n_episodes"] = n_eps + cur_stats.get("n_episodes", 0)
             cur_stats["ep_length"] = steps + cur_stats.get("ep_length", 0)
             cur_returns.extend(returns.cpu().tolist())

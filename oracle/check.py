@@ -11,18 +11,31 @@ import numpy as np
 
 from . import oracle as ora
 
+# Philox mode: float32 bump values vs float32 of their float64 evaluation
+PHILOX_RTOL = 1e-6
+# v_exp_f32 flushes results below FLT_MIN (2^-126) to 0; times the task scale (<= 10)
+PHILOX_ATOL = 10.0 * float(np.finfo(np.float32).tiny)
+
 
 def replay_and_compare(n, m, T, L, lam, table, prev0, td, returns, T_trans=None, quirks=(),
-                       rtol_reward=0.0, obs_atol=0.0):
+                       rtol_reward=0.0, obs_atol=0.0, philox=False):
     """table [E,n,m,T] f64, prev0 [E,n] i64, td: dict of numpy arrays [E, T+1, ...] read
-    back from the GPU batch, returns [E] f64.  Raises AssertionError on any mismatch."""
+    back from the GPU batch, returns [E] f64.  Raises AssertionError on any mismatch.
+
+    philox=True (native Philox mode): `table` is the float64 evaluation of the episode's
+    bump parameters (asg_export_benefits) while obs / beta hold the kernel's float32
+    evaluation of the same bumps, checked within 1e-6 relative (atol 10 FLT_MIN: exp results
+    below FLT_MIN flush to 0 before the task scale); rewards, masks, one-hots and returns stay exact."""
     E = table.shape[0]
+    obs_rtol = PHILOX_RTOL if philox else 0.0
+    if philox:
+        obs_atol = max(obs_atol, PHILOX_ATOL)
     for e in range(E):
         env = ora.OracleMockEnv(n, m, T, L, lam, sat_prox_mat=table[e], T_trans=T_trans, mt=ora.MT(0))
         env.reset()
         env.prev_assigns[:] = prev0[e]
-        _cmp(td["obs"][e, 0], env._obs.astype(np.float32), f"env {e} obs row 0", obs_atol)
-        _cmp(td["beta"][e, 0], env.beta.astype(np.float32), f"env {e} beta row 0", obs_atol)
+        _cmp(td["obs"][e, 0], env._obs.astype(np.float32), f"env {e} obs row 0", obs_atol, obs_rtol)
+        _cmp(td["beta"][e, 0], env.beta.astype(np.float32), f"env {e} beta row 0", obs_atol, obs_rtol)
         ret = 0.0
         for t in range(T):
             a = td["actions"][e, t].reshape(n).astype(np.int64)
@@ -30,8 +43,8 @@ def replay_and_compare(n, m, T, L, lam, table, prev0, td, returns, T_trans=None,
             ret += sum(r)
             _cmp(td["rewards"][e, t], np.asarray(r).astype(np.float32), f"env {e} rewards t={t}",
                  rtol=rtol_reward)
-            _cmp(td["obs"][e, t + 1], env._obs.astype(np.float32), f"env {e} obs t={t + 1}", obs_atol)
-            _cmp(td["beta"][e, t + 1], env.beta.astype(np.float32), f"env {e} beta t={t + 1}", obs_atol)
+            _cmp(td["obs"][e, t + 1], env._obs.astype(np.float32), f"env {e} obs t={t + 1}", obs_atol, obs_rtol)
+            _cmp(td["beta"][e, t + 1], env.beta.astype(np.float32), f"env {e} beta t={t + 1}", obs_atol, obs_rtol)
             onehot = np.zeros((n, m), dtype=np.int64)
             onehot[np.arange(n), a] = 1
             if "actions_onehot" in td:
@@ -43,6 +56,16 @@ def replay_and_compare(n, m, T, L, lam, table, prev0, td, returns, T_trans=None,
         assert td["avail_actions"][e].all(), f"env {e} avail_actions"
         assert (td["filled"][e] == 1).all(), f"env {e} filled"
         assert abs(returns[e] - ret) <= 1e-9 * max(1.0, abs(ret)), f"env {e} return {returns[e]} vs {ret}"
+
+
+def bump_table_from_params(params, T):
+    """float64 benefit table [E, n, m, T] from Philox bump parameters [E, n, m, 3]
+    (scale, center, a2) as asg_export_bump_params returns them: the reference's
+    scale * exp(-(t - c)^2 / sigma_2 / 2) (mock_constellation_env.py:293) evaluated in
+    float64 on those parameters, written scale * 2^(-(t - c)^2 a2), a2 = log2(e) / (2 sigma_2)."""
+    p = np.asarray(params, dtype=np.float64)
+    x = np.arange(T, dtype=np.float64)[None, None, None, :] - p[..., 1:2]
+    return p[..., 0:1] * np.exp2(-(x * x) * p[..., 2:3])
 
 
 def _cmp(got, want, what, atol=0.0, rtol=0.0):

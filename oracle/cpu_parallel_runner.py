@@ -115,8 +115,10 @@ def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episode
                           epsilon=0.05, seed=0, min_seconds=0.0, max_episodes=10000):
     """Runs ParallelRunner-protocol episodes of `workers` envs -- `episodes` of them, or
     more until `min_seconds` have elapsed (bounded by max_episodes); returns
-    (env_steps_per_s, env_steps, seconds) over the step loops (resets included, as the
-    reference runner's wall time includes them)."""
+    (env_steps_per_s, env_steps, seconds, reset_seconds): the rate over the whole loop
+    (resets amortised, as the reference runner's wall time includes them) and the time
+    spent in the reset round trips, so the step-loop-only rate is
+    env_steps / (seconds - reset_seconds) (SURVEY §8(d) asks for both)."""
     import torch
 
     from marl_sap_amd.components import EpisodeBatch
@@ -136,11 +138,13 @@ def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episode
     args = SimpleNamespace(hidden_dim=hidden, use_rnn=True, m=m)
     agent = RNNAgent(m * (L + 1), args)
     steps = 0
+    reset_secs = 0.0
     t0 = time.perf_counter()
     with torch.no_grad():
         ep = 0
         while ep < episodes or (time.perf_counter() - t0 < min_seconds and ep < max_episodes):
             ep += 1
+            r0 = time.perf_counter()
             batch = EpisodeBatch(scheme, {"agents": n}, workers, T + 1, preprocess=preprocess, device="cpu")
             for c in parents:
                 c.send(("reset", None))
@@ -149,6 +153,7 @@ def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episode
                 for k, v in c.recv().items():
                     pre[k].extend(v)
             batch.update(pre, ts=0)
+            reset_secs += time.perf_counter() - r0
             h = agent.init_hidden().unsqueeze(0).expand(workers, n, -1)
             for t in range(T):
                 q, h = agent(batch["obs"][:, t].reshape(workers * n, -1), h)
@@ -177,4 +182,4 @@ def run_parallel_baseline(n=64, m=64, T=20, L=3, lambda_=0.5, workers=8, episode
         c.send(("close", None))
     for p in procs:
         p.join(timeout=5)
-    return steps / secs, steps, secs
+    return steps / secs, steps, secs, reset_secs

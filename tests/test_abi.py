@@ -73,7 +73,7 @@ def test_kernel_entry_points_validate_without_gpu(L):
     assert L.asg_lsa_batched(None, 0, st, 1, 2000, 4, 0, None, None, None, None) == _lib.ASG_E_INVALID_ARG
     assert L.asg_lsa_batched(None, 0, st, 0, 4, 4, 0, None, None, None, None) == _lib.ASG_OK  # empty batch
     assert L.asg_haa_select(None, st, None, st, 1, 4, 4, None, 0.5, None, None, None) == _lib.ASG_E_INVALID_ARG
-    assert L.asg_epsilon_greedy(None, st, None, st, 1, 4, 4, 0.1, 0, 0, None, st, None, None) == \
+    assert L.asg_epsilon_greedy(None, st, None, st, 1, 4, 4, 0.1, 0, 0, 0, None, st, None, None) == \
         _lib.ASG_E_INVALID_ARG
     assert L.asg_reset(None, None, 0) == _lib.ASG_E_INVALID_ARG
     assert L.asg_step(None, None, 0) == _lib.ASG_E_INVALID_ARG

@@ -26,10 +26,17 @@ def _worker(rank, world, port, E, q):
     assert (r, w) == (rank, world)
     base = r * E  # GpuVecRunner: env_index_base = rank * batch_size_run
     local = torch.arange(base, base + E, dtype=torch.float64) * 0.5 + 0.25
-    allr = asg_dist.all_gather_returns(local)
+    counts = asg_dist.envs_per_rank(E)
+    assert counts == [E] * world and asg_dist.env_index_base(counts, r) == base
+    allr = asg_dist.all_gather_returns(local, counts)
     steps = asg_dist.all_reduce_sum(E * 20)
+    # ragged shards (rank r owns E + r envs): padded gather, stripped in global env order
+    Er = E + r
+    counts = asg_dist.envs_per_rank(Er)
+    rb = asg_dist.env_index_base(counts, r)
+    ragged = asg_dist.all_gather_returns(torch.arange(rb, rb + Er, dtype=torch.float64), counts)
     asg_dist.barrier()
-    q.put((rank, allr.tolist(), steps))
+    q.put((rank, allr.tolist(), steps, counts, ragged.tolist()))
     dist.destroy_process_group()
 
 
@@ -47,9 +54,11 @@ def test_gather_returns_and_counters(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = [e * 0.5 + 0.25 for e in range(world * E)]
-    for rank, allr, steps in res:
+    for rank, allr, steps, counts, ragged in res:
         assert allr == expect
         assert steps == world * E * 20
+        assert counts == [E + r for r in range(world)]
+        assert ragged == [float(i) for i in range(sum(counts))]
 
 
 def test_single_process_is_identity():

@@ -124,13 +124,55 @@ def test_fused_select_equals_forward_then_selector(eps, B, n, m, K, use_rnn):
         q, h1 = agent(x, h)
         a1 = sel.select_action(q.view(B, n, m), avail, 0)
         sel2 = EpsilonGreedyActionSelector(args)
-        e, seed, counter, status = sel2.fused_params(0, False, DEV)
-        assert (seed, counter) == (sel.seed, sel.calls)
+        e, seed, counter, status, base = sel2.fused_params(0, False, DEV)
+        assert (seed, counter, base) == (sel.seed, sel.calls, 0)
         out = torch.full((B, n), -7, dtype=torch.int64, device=DEV)
         h2 = agent.forward_select(x, h, avail, n, e, seed, counter, out, status)
     assert torch.equal(h2, h1)
     assert torch.equal(out, a1)
     assert int(status.item()) == 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_select_draws_are_shard_invariant(fused):
+    """epsilon > 0: the exploration draws are keyed by global (env, agent) row, so two
+    shards (envs [0, B/2) and [B/2, B), env_index_base = 0 and B/2) pick exactly the actions
+    of one call over all B envs -- fused agent + selection and the standalone selector."""
+    from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector
+    torch.manual_seed(3)
+    B, n, m, K, eps = 64, 16, 64, 256, 0.5
+    args = SimpleNamespace(hidden_dim=64, use_rnn=True, m=m, epsilon_start=eps, epsilon_finish=eps,
+                           epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=11)
+    agent = RNNFusedAgent(K, args).to(DEV)
+    x = torch.randn((B * n, K), device=DEV)
+    h = torch.randn((B * n, 64), device=DEV)
+    avail = torch.rand((B, n, m), device=DEV) > 0.3
+    avail[..., 0] = True
+    half = B // 2
+
+    def run(lo, hi):
+        sel = EpsilonGreedyActionSelector(args)
+        sel.envs = SimpleNamespace(env_index_base=lo)
+        out = torch.full((hi - lo, n), -7, dtype=torch.int64, device=DEV)
+        with torch.no_grad():
+            if fused:
+                e, seed, counter, status, base = sel.fused_params(0, False, DEV)
+                agent.forward_select(x[lo * n:hi * n], h[lo * n:hi * n], avail[lo:hi], n, e, seed, counter, out,
+                                     status, env_index_base=base)
+            else:
+                q, _ = agent(x[lo * n:hi * n], h[lo * n:hi * n])
+                out = sel.select_action(q.view(hi - lo, n, m), avail[lo:hi], 0)
+        return out
+
+    full = run(0, B)
+    shards = torch.cat([run(0, half), run(half, B)])
+    assert torch.equal(shards, full)
+    greedy = torch.zeros_like(full)
+    with torch.no_grad():
+        q, _ = agent(x, h)
+        greedy = q.view(B, n, m).masked_fill(~avail, -float("inf")).max(2)[1]
+    frac = (full != greedy).float().mean().item()
+    assert 0.2 < frac < 0.6, frac  # about eps * (1 - 1/available) of the rows explore off the argmax
 
 
 @pytest.mark.parametrize("use_rnn", [True])

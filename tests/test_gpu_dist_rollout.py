@@ -1,0 +1,99 @@
+"""Multi-rank rollout on one GPU: GpuVecRunner sharded over 2 ranks
+(one process per rank, gloo, both on cuda:0) gathers exactly the returns of a 1-rank run
+over the same global envs, bitwise -- env draws, epsilon-greedy exploration and SAP noise
+are all keyed by global env index -- and every rank's EpisodeBatch shard equals the
+matching slice of the 1-rank batch.  Also runs bench.py's multi-rank branch under
+torch.distributed.run.  Reference: runners/parallel_runner.py:178-179 (t_env over all
+envs), :173-176 (per-env returns)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "dist_rollout_worker.py")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(tmp, counts, eps, selector, episodes=2, tag="run"):
+    world = len(counts)
+    port = _free_port()
+    procs, outs = [], []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+        out = os.path.join(tmp, f"{tag}_w{world}_r{r}.pt")
+        outs.append(out)
+        procs.append(subprocess.Popen(
+            [sys.executable, WORKER, out, ",".join(map(str, counts)), str(eps), selector, str(episodes)],
+            env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        logs.append(o.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    return [torch.load(o, weights_only=True) for o in outs]
+
+
+@pytest.mark.parametrize("selector,eps,counts", [
+    ("epsilon_greedy", 0.3, [24, 24]),
+    ("epsilon_greedy", 0.0, [24, 24]),
+    ("sap", 0.2, [24, 24]),
+    ("epsilon_greedy", 0.3, [10, 38]),  # ragged shards: padded all-gather, sum(E_r) t_env
+])
+def test_two_rank_rollout_equals_one_rank(tmp_path, selector, eps, counts):
+    total = sum(counts)
+    (one,) = _launch(str(tmp_path), [total], eps, selector, tag="one")
+    shards = _launch(str(tmp_path), counts, eps, selector, tag="two")
+    base = 0
+    for r, sh in enumerate(shards):
+        assert sh["env_index_base"] == base and sh["rank_envs"] == counts
+        for a, b in zip(sh["returns"], one["returns"]):
+            assert a.dtype == torch.float64 and torch.equal(a, b)  # gathered = 1-rank returns, bitwise
+        assert sh["t_env"] == one["t_env"] == [total * 6 * (e + 1) for e in range(len(one["t_env"]))]
+        assert sh["train_returns"] == one["train_returns"]
+        for k, v in one["batch"].items():
+            assert torch.equal(sh["batch"][k], v[base:base + counts[r]]), k
+        base += counts[r]
+    if eps > 0 and selector == "epsilon_greedy":
+        # exploration really happened and differs between envs (global keying, not per-rank copies)
+        acts = one["batch"]["actions"][:, :6, :, 0]
+        assert not torch.equal(acts[:counts[0]], acts[counts[0]:2 * counts[0]])
+
+
+def test_bench_multi_rank_branch(tmp_path):
+    """bench.py --gpus 2 through torch.distributed.run (gloo on one GPU): rank 0 prints one
+    JSON line with the whole-job value over both ranks."""
+    env = dict(os.environ, ASG_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "10", "--warmup", "3", "--envs", "256", "--cpu-baseline", "0",
+           "--secondary", "0"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 512 and line["value"] > 0
+    assert line["scaling"] == "weak" and line["cpu_baseline"] is None

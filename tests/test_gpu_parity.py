@@ -279,7 +279,7 @@ def test_philox_rollout_vs_oracle(n, m, T, L, lam, custom_T, time_major):
             env.step(b, t)
         env.sync()
         replay_and_compare(n, m, T, L, lam, table, prev0, host(b), env.get_returns().cpu().numpy(),
-                           T_trans=T_trans)
+                           T_trans=T_trans, philox=True)
 
 
 def test_philox_quirks_and_dense():
@@ -296,7 +296,7 @@ def test_philox_quirks_and_dense():
         env.step(b, t)
     env.sync()
     replay_and_compare(n, m, T, L, 0.5, table, prev0, host(b), env.get_returns().cpu().numpy(),
-                       quirks=("prev_assigns_zero", "parallel_terminated"))
+                       quirks=("prev_assigns_zero", "parallel_terminated"), philox=True)
 
 
 def test_sharding_is_bitwise_equivalent():
@@ -359,7 +359,103 @@ def test_full_size_episode_properties():
     idx = np.array([0, 1, 777, 4095, 8191, 12000, 16383])
     table = env.export_benefits()[idx].cpu().numpy()
     td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
-    replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy())
+    replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy(), philox=True)
+
+
+def test_native_bump_precision_vs_float64():
+    """Philox mode evaluates the bumps of obs / beta in float32 (v_exp_f32 with an exact
+    argument split); against the float64 evaluation of the SAME bump parameters (the
+    reference's arithmetic, mock_constellation_env.py:293, on asg_export_bump_params) every
+    obs / beta entry is within 1e-6 relative (atol 10 FLT_MIN: exp results below FLT_MIN
+    flush to 0 before the task scale of <= 10), and
+    the rewards -- computed on the GPU from the float64 values, including the beta > 1e-12
+    penalty mask (mock :266) -- equal float32 of the host's float64 reward to float32
+    rounding."""
+    from oracle.check import PHILOX_ATOL, PHILOX_RTOL, bump_table_from_params
+    n, m, T, L, E = 64, 64, 20, 3, 512
+    env = AssignEnvBatch(n, m, T, L, 0.5, seed=31, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    params = env.export_bump_params().cpu().numpy()
+    tab = bump_table_from_params(params, T)                          # [E, n, m, T] float64
+    np.testing.assert_allclose(env.export_benefits().cpu().numpy(), tab, rtol=4e-16, atol=0)
+    prev = env.export_prev_assigns().cpu().numpy()
+    for t in range(T):
+        env.random_actions(b, t)
+        env.step(b, t)
+    env.sync()
+    h = host(b)
+    worst = 0.0
+    for t in range(T + 1):
+        for l in range(L):
+            want = tab[..., t + l].astype(np.float32) if t + l < T else np.zeros((E, n, m), np.float32)
+            got = h["obs"][:, t, :, m * (l + 1):m * (l + 2)]
+            np.testing.assert_allclose(got, want, rtol=PHILOX_RTOL, atol=PHILOX_ATOL, err_msg=f"obs t={t} l={l}")
+            nz = want >= PHILOX_ATOL
+            if nz.any():
+                worst = max(worst, float(np.max(np.abs(got[nz] / want[nz] - 1.0))))
+        want_b = tab[..., t].astype(np.float32) if t < T else np.zeros((E, n, m), np.float32)
+        np.testing.assert_allclose(h["beta"][:, t], want_b, rtol=PHILOX_RTOL, atol=PHILOX_ATOL, err_msg=f"beta t={t}")
+    # rewards on the host in float64 from the float64 table (mock :126-138)
+    acts = h["actions"][:, :T, :, 0]
+    ret = np.zeros(E)
+    for t in range(T):
+        a = acts[:, t]
+        beta = np.take_along_axis(tab[..., t], a[..., None], axis=2)[..., 0]        # [E, n]
+        pen = (a != prev).astype(np.float64) * (beta > 1e-12)
+        bh = beta - 0.5 * pen
+        cnt = np.stack([np.bincount(a[e], minlength=m)[a[e]] for e in range(E)])
+        r = np.where(bh > 0, bh / cnt, bh)
+        np.testing.assert_allclose(h["rewards"][:, t], r.astype(np.float32), rtol=2e-7, atol=0, err_msg=f"t={t}")
+        ret += r.sum(1)
+        prev = a
+    np.testing.assert_allclose(env.get_returns().cpu().numpy(), ret, rtol=1e-12)
+    print(f"max relative error of float32 bump values vs float64: {worst:.3g}")
+    assert worst < PHILOX_RTOL
+
+
+def test_full_size_dense_256_episode_properties():
+    """BASELINE configs[4] size (256 x 256 dense benefits, 2,048 envs, T=20): invariants on
+    every env of a full episode plus an oracle replay of sampled envs (benefits from the
+    exported bump parameters in float64).  Reference anchor: mock_constellation_env.py:228-274
+    (beta_hat), :116-162 (step)."""
+    from oracle.check import bump_table_from_params
+    n, m, T, L, E = 256, 256, 20, 3, 2048
+    env = AssignEnvBatch(n, m, T, L, 0.5, seed=4096, num_envs=E, device=DEV, benefits="dense")
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    prev0 = env.export_prev_assigns()
+    idx = np.array([0, 1, 1000, 2047])
+    params = env.export_bump_params()
+    assert bool((params[..., 0] > 0).all())  # dense: every (i, j) pair has a bump
+    params = params[idx].cpu().numpy()
+    for t in range(T):
+        env.random_actions(b, t)
+        env.step(b, t)
+    env.sync()
+    obs, beta = b["obs"], b["beta"]
+    for t in range(T):  # per row: keeps the int64 one-hot temporaries at ~1 GB
+        a = b["actions"][:, t, :, 0]
+        oh = torch.zeros((E, n, m), dtype=torch.int64, device=DEV).scatter_(-1, a.unsqueeze(-1), 1)
+        assert torch.equal(obs[:, t + 1, :, :m].to(torch.int64), oh), t
+        assert torch.equal(b["actions_onehot"][:, t], oh), t
+        assert torch.equal(beta[:, t], obs[:, t, :, m:2 * m]), t
+        if t + 1 < T:
+            assert torch.equal(obs[:, t + 1, :, 2 * m:3 * m], obs[:, t + 2, :, m:2 * m]), t
+        assert torch.equal(b["prev_assigns"][:, t + 1], a), t
+        del oh
+    assert (beta[:, T] == 0).all() and (obs[:, T, :, m:] == 0).all()
+    assert b["avail_actions"].all() and (b["filled"] == 1).all()
+    assert torch.equal(b["terminated"][:, :, 0].sum(1), torch.ones(E, dtype=torch.int64, device=DEV))
+    assert torch.equal(b["prev_assigns"][:, 0], prev0)
+    srt = prev0.sort(dim=1)[0]
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+    r = env.get_returns()
+    assert torch.allclose(b["rewards"][:, :T].double().sum((1, 2)), r, rtol=1e-5, atol=1e-3)
+    table = bump_table_from_params(params, T)
+    td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
+    replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy(),
+                       philox=True, rtol_reward=2e-7)
 
 
 def test_action_range_error():

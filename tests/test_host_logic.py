@@ -102,7 +102,7 @@ def test_cpu_baseline_port_matches_golden(golden):
 
 def test_cpu_baseline_runs():
     from oracle.cpu_parallel_runner import run_parallel_baseline
-    rate, steps, secs = run_parallel_baseline(n=4, m=4, T=3, L=1, workers=2, episodes=1)
+    rate, steps, secs, reset_secs = run_parallel_baseline(n=4, m=4, T=3, L=1, workers=2, episodes=1)
     assert steps == 6 and rate > 0
 
 
