@@ -24,7 +24,7 @@ The JSON line also carries:
                   the stream it is launched on, against the 8 TB/s HBM3E peak; `traffic` is the
                   PMC-measured HBM bytes per launch from profiles/pmc_step_kernel*.json when one
                   matches the workload.
-  roofline_agent  the agent forward (fused RNNAgent kernel) against its MFMA roof.
+  roofline_agent  the agent forward (fused RNNAgent kernel) against its MFMA roof and HBM.
   cpu_baseline    rank 0 at N = 1 only: the reference's CPU design (subprocess-per-env
                   ParallelRunner + numpy env + CPU RNN agent, oracle/cpu_parallel_runner.py) on
                   a bounded sample of the same workload: step-loop-only and reset-amortised
@@ -77,10 +77,18 @@ def step_bytes(n, m, L):
     return n * m * (4 * (L + 1) + 4 + 1 + 8) + n * (8 + 4 + 8) + 1 + 8
 
 
+F16_MFMA_PEAK_TFS = 2500.0  # dense f16 MFMA = bf16 rate (MI355X_MICROARCH.md)
+# f32 products as two-way-split f16 MFMAs cost three f16 products each
+H2_PEAK_TFS = F16_MFMA_PEAK_TFS / 3
+
+
 def agent_peak(n, m, L, mode, hidden=64, use_rnn=True, onehot=True):
     """f32-equivalent MFMA roof of the agent forward: each layer's flops at the peak of the
-    MFMA it runs on (asg_rnn_agent_mfma_mode: bit 0 GRU, bit 1 fc1 on split bf16), combined
-    as the time-weighted harmonic mean (flops / sum of per-layer minimum times)."""
+    MFMA it runs on (asg_rnn_agent_mode: 4 = every layer on split f16; else bit 0 GRU, bit 1
+    fc1 on split bf16), combined as the time-weighted harmonic mean (flops / sum of
+    per-layer minimum times)."""
+    if mode == 4:
+        return H2_PEAK_TFS
     K = m * (L + 1) - (m if onehot else 0)
     fc1, rec, fc2 = 2 * K * hidden, 2 * (2 * 3 * hidden * hidden if use_rnn else hidden * hidden), 2 * hidden * m
     t = (fc1 / (X3_PEAK_TFS if mode & 2 else F32_MFMA_PEAK_TFS) + rec / (X3_PEAK_TFS if mode & 1 else F32_MFMA_PEAK_TFS)
@@ -98,8 +106,16 @@ def agent_flops(n, m, L, hidden=64, use_rnn=True, onehot=True):
     return 2 * (K * hidden + rec + hidden * m)
 
 
+def agent_bytes(n, m, L, hidden=64):
+    """Algorithmic HBM bytes of one agent row of the fused forward + selection: the obs row
+    (f32 m(L+1)), h in and h' out (f32 hidden each), the availability row (bool m) and the
+    int64 action written."""
+    return 4 * m * (L + 1) + 2 * 4 * hidden + m + 8
+
+
 def agent_roofline(a, E, agent_ms, kernel):
-    """The agent forward (timed with HIP events on its stream) against its MFMA roof."""
+    """The agent forward (timed with HIP events on its stream) against its MFMA roof and
+    against HBM (both reported; `bound` names the larger fraction)."""
     if agent_ms is None or agent_ms <= 0:
         return None
     fused = a.agent == "rnn_fused"
@@ -107,12 +123,21 @@ def agent_roofline(a, E, agent_ms, kernel):
     flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
     tfs = flops / (agent_ms * 1e-3) / 1e12
     from marl_sap_amd import _lib
-    mode = int(_lib.lib().asg_rnn_agent_mfma_mode()) if fused else 0
+    K = a.m * (a.L + 1)
+    mode = int(_lib.lib().asg_rnn_agent_mode(K, 64, a.m, 1)) if fused else 0
     peak = agent_peak(a.n, a.m, a.L, mode, onehot=onehot)
-    return {"bound": "mfma", "achieved": round(tfs, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(tfs / peak, 4), "traffic": None,
-            "peak_note": ("f32-equivalent: GRU products on three-way-split bf16 MFMAs (2.5 PF / 6), fc1/fc2 "
-                          "on f32 MFMAs (157.3 TF), time-weighted" if mode else "f32 MFMA peak"),
+    nbytes = agent_bytes(a.n, a.m, a.L) * E * a.n
+    gbs = nbytes / (agent_ms * 1e-3) / 1e9
+    mfma = {"achieved": round(tfs, 2), "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
+            "peak_note": {4: "f32-equivalent: every layer's products on two-way-split f16 MFMAs (2.5 PF / 3)",
+                          0: "f32 MFMA peak"}.get(mode, "f32-equivalent: GRU products on three-way-split bf16 "
+                                                        "MFMAs (2.5 PF / 6), fc1/fc2 on f32 MFMAs (157.3 TF), "
+                                                        "time-weighted")}
+    hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "bytes_per_launch": nbytes}
+    top = hbm if hbm["frac"] >= mfma["frac"] else mfma
+    return {"bound": "hbm" if top is hbm else "mfma", "achieved": top["achieved"], "peak": top["peak"],
+            "unit": top["unit"], "frac": top["frac"], "traffic": None, "mfma": mfma, "hbm": hbm,
             "kernel": kernel, "kernel_ms": round(agent_ms, 4), "flops_per_launch": flops}
 
 
@@ -381,14 +406,14 @@ def main():
                         "asg_sap_select (per-env Gaussian noise + scipy-exact LSA, one wave64 per env)",
                 "env_step_ms": round(r3["kern_ms"], 4), "agent_ms": round(agent_ms, 4),
                 "roofline_lsa": lsa_roofline(a, E, r3),
-                "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_lds_kernel (forward only)")}
+                "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_h2_kernel (forward only)")}
 
     if a.selector == "random":
         ra = None
     elif a.selector == "sap":
         ra = agent_roofline(a, E, sel_ms - (res["lsa_ms"] or 0.0), f"{a.agent} forward")
     else:
-        ra = agent_roofline(a, E, sel_ms, "asg::rnn_agent_lds_kernel (forward + eps-greedy)"
+        ra = agent_roofline(a, E, sel_ms, "asg::rnn_agent_h2_kernel (forward + eps-greedy)"
                             if a.agent == "rnn_fused" else "torch RNNAgent + asg_epsilon_greedy")
     if rank == 0:
         sel_name = {"eps": "epsilon-greedy", "sap": "SAP", "random": "random"}[a.selector]

@@ -236,6 +236,11 @@ int64_t asg_rnn_agent_packed_size(int K, int hidden, int n_out, int use_rnn);
  * products, fp32-level accuracy; asg_agent.hip): bit 0 = GRU (default), bit 1 = fc1.  The
  * rest run f32 MFMAs.  For roofline accounting (bench.py); results match either way. */
 int asg_rnn_agent_mfma_mode(void);
+/* The MFMA mode of the kernel asg_rnn_agent_forward / _select run for this shape (16-B
+ * aligned rows): 4 = every layer's f32 products on two-way-split f16 MFMAs (the split-f16
+ * kernel: GRU, K % 32 == 0, n_out % 16 == 0, 16 <= n_out <= 256; accuracy vs float64 at or
+ * below PyTorch fp32's, tests/test_gpu_agent.py), else asg_rnn_agent_mfma_mode(). */
+int asg_rnn_agent_mode(int K, int hidden, int n_out, int use_rnn);
 int asg_rnn_agent_pack(const float *W1, const float *W_ih, const float *W_hh, const float *W2, int K,
                        int hidden, int n_out, int use_rnn, void *packed, void *hip_stream);
 int asg_rnn_agent_forward(const float *x, int64_t x_stride, int64_t R, int K, const float *h_in,

@@ -35,7 +35,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_reset", "asg_step", "asg_random_actions", "asg_sync_status", "asg_set_benefits",
            "asg_export_benefits", "asg_export_bump_params", "asg_export_prev_assigns", "asg_get_returns", "asg_get_step",
            "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_sap_select", "asg_epsilon_greedy",
-           "asg_rnn_agent_packed_size", "asg_rnn_agent_mfma_mode", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
+           "asg_rnn_agent_packed_size", "asg_rnn_agent_mfma_mode", "asg_rnn_agent_mode", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
            "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
            "asg_real_set_benefits", "asg_real_set_initial_assignments", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
            "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size"]
@@ -119,6 +119,8 @@ def lib():
                                          i64, vp, i64p, vp, vp]
         L.asg_rnn_agent_packed_size.argtypes = [i32, i32, i32, i32]
         L.asg_rnn_agent_mfma_mode.restype = i32
+        L.asg_rnn_agent_mode.argtypes = [i32, i32, i32, i32]
+        L.asg_rnn_agent_mode.restype = i32
         L.asg_rnn_agent_pack.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]
         L.asg_rnn_agent_forward.argtypes = [vp, i64, i64, i32, vp, i64] + [vp] * 5 + [i32, i32, i32, vp, vp, vp]
         L.asg_rnn_agent_select.argtypes = [vp, i64, i64, i32, vp, i64] + [vp] * 5 + [i32, i32, i32, vp, vp, vp, i64p,

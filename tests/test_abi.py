@@ -92,5 +92,9 @@ def test_agent_pack_layout_without_gpu(L):
         w1 = ((K + 15) // 16) * 4 * 64
         w2 = 4 * ((m + 15) // 16) * 64
         P = m if (m % 16 == 0 and m < K and K % 32 == 0) else 0
-        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K)), (K, m, rnn)
+        # split-f16 section (GRU, K % 32 == 0, 16 <= n_out <= 256, n_out % 16 == 0): header +
+        # two planes of W1, W_ih, W_hh, W2
+        h2 = (1 + (K // 32) * 512 + 2 * 3072 + (m // 16) * 256) if (rnn and K % 32 == 0 and m % 16 == 0
+                                                                    and 16 <= m <= 256) else 0
+        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K) + h2), (K, m, rnn)
     assert L.asg_rnn_agent_packed_size(256, 32, 64, 1) < 0  # hidden must be 64
