@@ -38,6 +38,11 @@
  *                              BasicMAC.forward for action selection (basic_controller.py:26-48)
  *   asg_get_returns            the runners' episode_return accumulation
  *                              (episode_runner.py:84, parallel_runner.py:173-176)
+ *   asg_filtered_*             FilteredSAPActionSelector / FilteredEpsGrSAPTestActionSelector
+ *                              (action_selectors/filtered_sap_selectors.py:7-148),
+ *                              FilteredEpsilonGreedyActionSelector / FilteredSoftPoliciesSelector
+ *                              (action_selectors/filtered_classic_selectors.py:6-103)
+ *   asg_real_haal_select       HAALSelector.select_action (action_selectors/non_rl_selectors.py:54-118)
  */
 #ifndef ASG_H
 #define ASG_H
@@ -260,6 +265,43 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
                          uint64_t counter, int64_t env_index_base, int64_t *out,
                          const int64_t out_strides[2], int32_t *status, void *hip_stream);
 
+/* ---- filtered selectors (the real-env algorithms' action_selector) -------------------------
+ * The agent emits M + 1 values per agent: its top-M tasks by total benefit and a baseline.
+ * asg_filtered_topm: per (env, agent) row, total[j] = beta[b][i][j][:].sum() in beta's dtype
+ * (float16: float32 accumulation left to right, rounded to half -- torch's Half sum; float32 /
+ * float64 left to right), and the M largest task ids in descending order, ties to the lower
+ * index (th.topk(total_beta, k=M).indices, filtered_sap_selectors.py:24,52; torch leaves tie
+ * order unspecified; NaN ranks first).  beta strides {env, agent, task, l} in elements;
+ * topm_out [B][n][M] int64 contiguous.  m <= 1024, 1 <= M <= min(m, 64). */
+int asg_filtered_topm(const void *beta, int beta_dtype, const int64_t beta_strides[4], int64_t B, int n, int m,
+                      int L, int M, int64_t *topm_out, void *hip_stream);
+/* The filtered selectors' benefit matrix (filtered_sap_selectors.py:37-55,
+ * filtered_classic_selectors.py:37-54): mat[b][i][j] = q[b][i][M] + float32(u * 1e-8f), then
+ * mat[b][i][topm[b][i][s]] = q[b][i][s] for s < M.  u: tie_noise [B][n][m] f32 (the reference's
+ * th.rand_like draws, parity mode) or NULL = Philox uniforms keyed (seed, env_index_base + b,
+ * counter).  FilteredSAPActionSelector's exploration: gauss_noise [B][n][m] f32 added as given,
+ * or, when NULL and gauss_epsilon > 0, N(0, std^2) per env with std = float32(mean|mat[b]| *
+ * eps) * 2 (Philox Box-Muller).  q [B][n][M+1] f32 any strides; mat_out [B][n][m] contiguous. */
+int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int64_t *topm, int64_t B, int n, int m,
+                          int M, const float *tie_noise, double gauss_epsilon, const float *gauss_noise,
+                          uint64_t seed, uint64_t counter, int64_t env_index_base, float *mat_out,
+                          void *hip_stream);
+/* asg_epsilon_greedy over the benefit matrix with the argmax NOT masked by availability
+ * (benefit_matrix.max(dim=2)[1], filtered_classic_selectors.py:57-61); exploration draws a
+ * uniformly random available task (Categorical(avail)) exactly as asg_epsilon_greedy. */
+int asg_filtered_epsilon_greedy(const float *mat, const int64_t mat_strides[3], const uint8_t *avail,
+                                const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon,
+                                uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *out,
+                                const int64_t out_strides[2], int32_t *status, void *hip_stream);
+/* FilteredSoftPoliciesSelector's index -> task map (filtered_classic_selectors.py:79-101):
+ * picked [B][n] int64 in [0, M]: p < M -> topm[b][i][p]; p == M -> a uniformly random task
+ * outside the top M (Philox keyed (seed, env_index_base + b, counter, agent)).  out [B][n]
+ * int64; status [1] int32 device word set to ASG_E_INVALID_ARG for a picked index outside
+ * [0, M]. */
+int asg_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B, int n, int m, int M,
+                          uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *out,
+                          int32_t *status, void *hip_stream);
+
 /* ==== RealConstellationEnv ======================================
  * Batched form of src/envs/real_constellation_env.py with injected benefits
  * (sat_prox_mat + graphs given: the constant-benefit path, :55-61).  Replaces
@@ -319,6 +361,20 @@ int asg_real_get_step(const asg_real_handle *h, int *k_out);
 /* get_obs_size (real_constellation_env.py:251-253): M*L + N*M*L + (N*M//2)*L + M; the
  * power variants add N + 1 (real_power_constellation_env.py:286-290) */
 int asg_real_obs_size(int N, int M, int L);
+/* HAALSelector (non_rl_selectors.py:54-118) on every env of a plain-variant handle at its
+ * current step k: for each time-interval sequence of the window eff = min(L, T - k)
+ * (build_time_interval_sequences, utils/methods.py:309-349; S = 2^(eff-1) sequences in the
+ * reference's order, eff <= 6) the env is forked, and per interval LSA(maximize) of
+ * beta_hat summed over L (float64, numpy's order) is stepped interval-length times; a
+ * sequence's value is the sum of the steps' sum(rewards).  The action is the first
+ * interval's assignment of the first best sequence (col_out [E][n] float32 task ids, the
+ * selector's float picked_actions).  values_out [E][S] float64, best_out [E] int32 (index of
+ * the winning sequence) and status_out [E] int32 (0 or the scipy error code of any LSA of
+ * that env) may be NULL.  Stream-ordered; a device workspace is kept in the handle. */
+int asg_real_haal_select(asg_real_handle *h, float *col_out, double *values_out, int32_t *best_out,
+                         int32_t *status_out);
+/* S = 2^(eff-1) at the handle's current step (0 once the episode is done) */
+int asg_real_haal_num_sequences(const asg_real_handle *h);
 
 #ifdef __cplusplus
 }

@@ -38,7 +38,9 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_rnn_agent_packed_size", "asg_rnn_agent_mfma_mode", "asg_rnn_agent_mode", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
            "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
            "asg_real_set_benefits", "asg_real_set_initial_assignments", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
-           "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size"]
+           "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size", "asg_filtered_topm",
+           "asg_filtered_benefits", "asg_filtered_epsilon_greedy", "asg_filtered_soft_map", "asg_real_haal_select",
+           "asg_real_haal_num_sequences"]
 
 
 class AsgField(ctypes.Structure):
@@ -139,6 +141,14 @@ def lib():
         L.asg_real_get_returns.argtypes = [vp, vp]
         L.asg_real_get_step.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
         L.asg_real_obs_size.argtypes = [i32, i32, i32]
+        u64 = ctypes.c_uint64
+        L.asg_filtered_topm.argtypes = [vp, i32, i64p, i64, i32, i32, i32, i32, vp, vp]
+        L.asg_filtered_benefits.argtypes = [vp, i64p, vp, i64, i32, i32, i32, vp, dbl, vp, u64, u64, i64, vp, vp]
+        L.asg_filtered_epsilon_greedy.argtypes = [vp, i64p, vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, i64p,
+                                                  vp, vp]
+        L.asg_filtered_soft_map.argtypes = [vp, vp, i64, i32, i32, i32, u64, u64, i64, vp, vp, vp]
+        L.asg_real_haal_select.argtypes = [vp, vp, vp, vp, vp]
+        L.asg_real_haal_num_sequences.argtypes = [vp]
         for f in EXPORTS:
             if f not in ("asg_last_error", "asg_real_destroy"):
                 getattr(L, f).restype = i32

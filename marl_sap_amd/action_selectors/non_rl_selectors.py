@@ -73,4 +73,31 @@ def haa_select_batched(beta, prev, lambda_, T_trans=None, return_status=False):
     return out
 
 
+class HAALSelector:
+    """HAAL: HAA with an L-step lookahead over time-interval sequences (reference:
+    non_rl_selectors.py:54-118).  The reference deep-copies each env once per sequence and
+    steps the copies on the CPU; here the batched real env evaluates every sequence of every
+    env on the GPU from its own state (asg_real_haal_select: one batched LSA per level of
+    the sequences' decision tree, the rewards in the reference's order).  Returns float32
+    task ids [B, n].  The reference requires the episode runner (its envs must be in
+    lockstep with the batch); the batched env always is, so any protocol works."""
+
+    def __init__(self, args):
+        self.args = args
+        self.envs = None
+        self.status = DeferredStatus()
+        self.last_values = None  # [B, S] float64 sequence values of the last call
+        self.last_best = None    # [B] index of the winning sequence
+
+    def select_action(self, batch):
+        env = self.envs
+        if env is None or not hasattr(env, "haal_select"):
+            raise ValueError("HAALSelector needs the batched RealConstellationEnv (selector.envs)")
+        out, values, best, status = env.haal_select(return_values=True)
+        self.last_values, self.last_best = values, best
+        self.status.add(status)
+        return out
+
+
 REGISTRY["haa_selector"] = HAASelector
+REGISTRY["haal_selector"] = HAALSelector

@@ -443,4 +443,75 @@ int asg_rnn_agent_select(const float *x, int64_t x_stride, int64_t R, int K, con
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_rnn_agent_select");
 }
 
+// ---- filtered selectors (asg_filtered.hip) ------------------------------------------------
+int asg_filtered_topm(const void *beta, int beta_dtype, const int64_t beta_strides[4], int64_t B, int n, int m, int L,
+                      int M, int64_t *topm_out, void *hip_stream) {
+    if (!beta || !beta_strides || !topm_out || B < 0 || n <= 0 || m <= 0 || L <= 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_topm: bad arguments");
+    if (beta_dtype != ASG_F16 && beta_dtype != ASG_F32 && beta_dtype != ASG_F64)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_topm: beta must be float16 / float32 / float64");
+    if (M <= 0 || M > m) return fail(nullptr, ASG_E_INVALID_ARG, "selected index k out of range");
+    if (m > 1024 || M > 64) return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_topm: needs m <= 1024, M <= 64");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_filtered_topm(beta, beta_dtype, beta_strides, B, n, m, L, M, topm_out,
+                                             static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_topm");
+}
+
+int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int64_t *topm, int64_t B, int n, int m,
+                          int M, const float *tie_noise, double gauss_epsilon, const float *gauss_noise,
+                          uint64_t seed, uint64_t counter, int64_t env_index_base, float *mat_out,
+                          void *hip_stream) {
+    if (!q || !q_strides || !topm || !mat_out || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: bad arguments");
+    if (M <= 0 || M > m || M > 64 || m > 1024)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: needs 1 <= M <= min(m, 64), m <= 1024");
+    if (!(gauss_epsilon >= 0.0)) return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: epsilon >= 0");
+    if (B == 0) return ASG_OK;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const bool gauss = gauss_noise != nullptr || gauss_epsilon > 0.0;
+    double *rowabs = nullptr;
+    hipError_t e = hipSuccess;
+    if (gauss && !gauss_noise) e = hipMallocAsync(reinterpret_cast<void **>(&rowabs), sizeof(double) * B * n, s);
+    if (e == hipSuccess)
+        e = asg::launch_filtered_matrix(q, q_strides, topm, B, n, m, M, tie_noise, seed, (uint32_t)counter,
+                                        env_index_base, mat_out, rowabs, s);
+    if (e == hipSuccess && gauss)
+        e = asg::launch_filtered_gauss(mat_out, rowabs, B, n, m, (float)gauss_epsilon, gauss_noise, seed,
+                                       (uint32_t)counter, env_index_base, s);
+    if (rowabs) {
+        const hipError_t e2 = hipFreeAsync(rowabs, s);
+        if (e == hipSuccess) e = e2;
+    }
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_benefits");
+}
+
+int asg_filtered_epsilon_greedy(const float *mat, const int64_t mat_strides[3], const uint8_t *avail,
+                                const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
+                                uint64_t counter, int64_t env_index_base, int64_t *out, const int64_t out_strides[2],
+                                int32_t *status, void *hip_stream) {
+    if (!mat || !mat_strides || !avail || !avail_strides || !out || !out_strides || B < 0 || n <= 0 || m <= 0 ||
+        env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_epsilon_greedy: bad arguments");
+    if (!(epsilon >= 0.0 && epsilon <= 1.0))
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_epsilon_greedy: epsilon must be in [0, 1]");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_eps_greedy(mat, mat_strides, avail, avail_strides, B, n, m, (float)epsilon, seed,
+                                          (uint32_t)counter, env_index_base * n, out, out_strides, status,
+                                          static_cast<hipStream_t>(hip_stream), /*mask=*/false);
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_epsilon_greedy");
+}
+
+int asg_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B, int n, int m, int M, uint64_t seed,
+                          uint64_t counter, int64_t env_index_base, int64_t *out, int32_t *status, void *hip_stream) {
+    if (!picked || !topm || !out || !status || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_soft_map: bad arguments");
+    if (M <= 0 || M >= m) return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_soft_map: needs 1 <= M < m");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_filtered_soft_map(picked, topm, B, n, m, M, seed, (uint32_t)counter, env_index_base,
+                                                 out, status, static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_soft_map");
+}
+
 }  // extern "C"
+

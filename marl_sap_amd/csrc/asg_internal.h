@@ -74,7 +74,20 @@ hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64
 
 hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t *avail, const int64_t as[3],
                              int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter,
-                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s);
+                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s,
+                             bool mask = true);
+
+// filtered selectors (asg_filtered.hip)
+hipError_t launch_filtered_topm(const void *beta, int dtype, const int64_t bs[4], int64_t B, int n, int m, int L, int M,
+                                int64_t *topm, hipStream_t s);
+hipError_t launch_filtered_matrix(const float *q, const int64_t qs[3], const int64_t *topm, int64_t B, int n, int m,
+                                  int M, const float *tie, uint64_t seed, uint32_t counter, int64_t env_base,
+                                  float *mat, double *rowabs, hipStream_t s);
+hipError_t launch_filtered_gauss(float *mat, const double *rowabs, int64_t B, int n, int m, float epsilon,
+                                 const float *gauss, uint64_t seed, uint32_t counter, int64_t env_base, hipStream_t s);
+hipError_t launch_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B, int n, int m, int M,
+                                    uint64_t seed, uint32_t counter, int64_t env_base, int64_t *out, int *err,
+                                    hipStream_t s);
 
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,

@@ -23,7 +23,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <algorithm>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -584,6 +586,129 @@ __global__ void real_table_transpose_kernel(const double *src, double *dst, int6
     }
 }
 
+// ---- HAALSelector (action_selectors/non_rl_selectors.py:54-118) ---------------------------
+// The reference forks (deepcopy) every env once per time-interval sequence of the lookahead
+// window, and per interval solves scipy's LSA on beta_hat summed over L and steps the fork
+// interval-length times.  A fork's state is (step, previous assignment): the benefits are the
+// constant table.  Sequences share prefixes, so the distinct LSA states form a tree of
+// decision nodes (decision time t, the assignment in force before it = the parent node's):
+// 2^(eff-1) nodes, solved level by level as batched LSAs over all envs, then every
+// sequence's value is the reference's sum of per-step reward sums.
+constexpr int kHaalMaxL = 6;                     // 2^(6-1) = 32 nodes / sequences
+struct HaalPlan {
+    int nodes, seqs, eff;
+    int8_t node_t[1 << (kHaalMaxL - 1)];         // decision time offset of each node
+    int8_t node_parent[1 << (kHaalMaxL - 1)];    // parent node or -1 (root: the env's prev)
+    int8_t seq_len[1 << (kHaalMaxL - 1)];        // intervals per sequence
+    int8_t seq_node[1 << (kHaalMaxL - 1)][kHaalMaxL];  // the decision node of each interval
+};
+
+// total beta_hat of one (node, env, agent) row: ((b0 - lambda * pen) + b1) + ... in numpy's
+// order (real_constellation_env.py:309-326, then .sum(axis=-1) left to right)
+__global__ void __launch_bounds__(256) haal_matrix_kernel(RealState st, int k, HaalPlan plan, int node0, int nodes,
+                                                          const int64_t *assign, double *mats) {
+    const int lane = threadIdx.x & 63;
+    const int64_t gr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row over [nodes][E][n]
+    const int n = st.n, m = st.m;
+    if (gr >= (int64_t)nodes * st.E * n) return;
+    const int i = (int)(gr % n);
+    const int64_t ne = gr / n;
+    const int64_t e = ne % st.E;
+    const int node = node0 + (int)(ne / st.E);
+    const int t = plan.node_t[node], par = plan.node_parent[node];
+    const int prev = par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i];
+    const double *tab = st.table + e * st.table_env_stride;
+    double *row = mats + gr * m;
+    for (int j = lane; j < m; j += 64) {
+        double s = real_beta(st, tab, k + t, i, j, 0);
+        const double b0 = s;
+        for (int l = 1; l < st.L; ++l) s = s + real_beta(st, tab, k + t, i, j, l);
+        const double cond = s > 1e-12 ? 1.0 : 0.0;
+        const double pen = st.T_trans[(int64_t)prev * m + j] * cond;
+        double tot = b0 - st.lambda_ * pen;
+        for (int l = 1; l < st.L; ++l) tot = tot + real_beta(st, tab, k + t, i, j, l);
+        row[j] = tot;
+    }
+}
+
+// value of every (env, sequence): sum over its steps of Python's sum(rewards) (agent order,
+// float64), one workgroup per (sequence, env); then (sequence 0's workgroup, after all are
+// done in a second launch) the best sequence per env
+__global__ void __launch_bounds__(256) haal_values_kernel(RealState st, int k, HaalPlan plan, const int64_t *assign,
+                                                          double *values) {
+    extern __shared__ double s_rew[];  // [n] rewards, then [m] int counts
+    int *scnt = reinterpret_cast<int *>(s_rew + st.n);
+    const int s = blockIdx.x % plan.seqs;
+    const int64_t e = blockIdx.x / plan.seqs;
+    const int n = st.n, m = st.m;
+    const double *tab = st.table + e * st.table_env_stride;
+    double tot = 0.0;
+    for (int iv = 0; iv < plan.seq_len[s]; ++iv) {
+        const int node = plan.seq_node[s][iv];
+        const int t0 = plan.node_t[node];
+        const int t1 = iv + 1 < plan.seq_len[s] ? plan.node_t[plan.seq_node[s][iv + 1]] - 1 : plan.eff - 1;
+        const int64_t *A = assign + ((int64_t)node * st.E + e) * n;
+        const int par = plan.node_parent[node];
+        for (int t = t0; t <= t1; ++t) {
+            for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[(int)A[i]], 1);
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                // the previous assignment: the parent's on the interval's first step, then A
+                const int p = t > t0 ? (int)A[i]
+                                     : (par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i]);
+                const int c = (int)A[i];
+                double sum = real_beta(st, tab, k + t, i, c, 0);
+                const double b0 = sum;
+                for (int l = 1; l < st.L; ++l) sum = sum + real_beta(st, tab, k + t, i, c, l);
+                const double cond = sum > 1e-12 ? 1.0 : 0.0;
+                const double bh = b0 - st.lambda_ * (st.T_trans[(int64_t)p * m + c] * cond);
+                s_rew[i] = bh > 0 ? bh / (double)scnt[c] : bh;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double r = 0.0;
+                for (int i = 0; i < n; ++i) r += s_rew[i];  // sum(rewards), left to right
+                tot += r;                                   // total_tis_value += sum(rewards)
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) values[e * plan.seqs + s] = tot;
+}
+
+// per env: the first sequence with the largest value (strict >), its first-interval
+// assignment (the root node's: every sequence starts at the fork state) as float task ids
+__global__ void haal_pick_kernel(int64_t E, int n, int seqs, const double *values, const int64_t *assign,
+                                 const int32_t *lsa_status, float *col_out, int32_t *best_out, int32_t *status_out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    double best = -INFINITY;
+    int bs = -1;
+    for (int s = 0; s < seqs; ++s) {
+        const double v = values[e * seqs + s];
+        if (v > best) {
+            best = v;
+            bs = s;
+        }
+    }
+    if (best_out) best_out[e] = bs;
+    int32_t st = lsa_status ? lsa_status[e] : 0;
+    if (st == 0 && bs < 0) st = ASG_E_INVALID_ARG;  // every value NaN: the reference's best_assignment is None
+    if (status_out) status_out[e] = st;
+    for (int i = 0; i < n; ++i) col_out[e * n + i] = (st == 0) ? (float)assign[e * n + i] : -1.0f;
+}
+
+// min over the levels' LSA status words of each env ([levels' B] -> [E])
+__global__ void haal_status_kernel(const int32_t *st_all, int64_t rows, int64_t E, int32_t *st_env) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    int32_t v = 0;
+    for (int64_t r = e; r < rows; r += E) v = st_all[r] < v ? st_all[r] : v;
+    st_env[e] = v;
+}
+
 }  // namespace asg
 
 using asg::RealState;
@@ -596,6 +721,8 @@ struct asg_real_handle {
     bool has_reset = false;
     bool table_ready = false;
     double *table_buf = nullptr;
+    void *haal_ws = nullptr;  // HAAL workspace (grown on demand)
+    size_t haal_ws_bytes = 0;
     std::string err;
 };
 
@@ -799,6 +926,7 @@ void asg_real_destroy(asg_real_handle *h) {
     hipFree(h->st.topD);
     hipFree(h->st.err);
     hipFree(h->table_buf);
+    hipFree(h->haal_ws);
     delete h;
 }
 
@@ -934,4 +1062,144 @@ int asg_real_get_step(const asg_real_handle *h, int *k_out) {
 
 int asg_real_obs_size(int N, int M, int L) { return M * L + N * M * L + ((N * M) / 2) * L + M; }
 
+// the decision tree and sequence list of HAALSelector's window (utils/methods.py:309-349:
+// sequences depth first, the shorter first interval first)
+static void haal_plan(int eff, asg::HaalPlan &p) {
+    std::vector<std::vector<int>> seqs;  // decision times of each sequence
+    std::vector<int> cur;
+    std::function<void(int)> rec = [&](int last) {
+        if (last == eff - 1) {
+            seqs.push_back(cur);
+            return;
+        }
+        for (int j = last + 1; j < eff; ++j) {
+            cur.push_back(last + 1);
+            rec(j);
+            cur.pop_back();
+        }
+    };
+    rec(-1);
+    // nodes = distinct decision-time prefixes, numbered level by level
+    std::vector<std::vector<int>> nodes;
+    for (int lev = 1; lev <= eff; ++lev)
+        for (const auto &sq : seqs)
+            if ((int)sq.size() >= lev) {
+                std::vector<int> pre(sq.begin(), sq.begin() + lev);
+                if (std::find(nodes.begin(), nodes.end(), pre) == nodes.end()) nodes.push_back(pre);
+            }
+    p.eff = eff;
+    p.nodes = (int)nodes.size();
+    p.seqs = (int)seqs.size();
+    for (int a = 0; a < p.nodes; ++a) {
+        p.node_t[a] = (int8_t)nodes[a].back();
+        std::vector<int> par(nodes[a].begin(), nodes[a].end() - 1);
+        p.node_parent[a] = (int8_t)(par.empty() ? -1 : std::find(nodes.begin(), nodes.end(), par) - nodes.begin());
+    }
+    for (int s = 0; s < p.seqs; ++s) {
+        p.seq_len[s] = (int8_t)seqs[s].size();
+        for (size_t j = 0; j < seqs[s].size(); ++j) {
+            std::vector<int> pre(seqs[s].begin(), seqs[s].begin() + j + 1);
+            p.seq_node[s][j] = (int8_t)(std::find(nodes.begin(), nodes.end(), pre) - nodes.begin());
+        }
+    }
+}
+
+int asg_real_haal_num_sequences(const asg_real_handle *h) {
+    if (!h) return rfail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    const int eff = std::min(h->st.L, h->st.T - h->k);
+    return eff > 0 ? 1 << (eff - 1) : 0;
+}
+
+int asg_real_haal_select(asg_real_handle *h, float *col_out, double *values_out, int32_t *best_out,
+                         int32_t *status_out) {
+    if (!h || !col_out) return rfail(h, ASG_E_INVALID_ARG, "NULL handle or output");
+    if (!h->has_reset) return rfail(h, ASG_E_STATE, "asg_real_haal_select before asg_real_reset");
+    const asg::RealState &st = h->st;
+    if (st.variant != ASG_REAL_PLAIN)
+        return rfail(h, ASG_E_INVALID_ARG, "asg_real_haal_select: RealConstellationEnv (plain variant) only");
+    const int eff = std::min(st.L, st.T - h->k);
+    if (eff <= 0) return rfail(h, ASG_E_STATE, "asg_real_haal_select: the episode is done");
+    if (eff > asg::kHaalMaxL) return rfail(h, ASG_E_INVALID_ARG, "asg_real_haal_select: lookahead window > 6");
+    asg::HaalPlan plan{};
+    haal_plan(eff, plan);
+    RDeviceGuard g(h->device);
+    const int n = st.n, m = st.m;
+    const int64_t E = st.E;
+    int max_level = 0;  // nodes per level: level = prefix length
+    {
+        std::vector<int> per(eff + 1, 0);
+        for (int a = 0; a < plan.nodes; ++a) {
+            int d = 0;
+            for (int x = a; x >= 0; x = plan.node_parent[x]) ++d;
+            ++per[d];
+        }
+        for (int d = 1; d <= eff; ++d) max_level = std::max(max_level, per[d]);
+    }
+    // workspace: matrices of the largest level, all nodes' assignments, values, LSA status
+    const size_t mats_b = sizeof(double) * (size_t)max_level * E * n * m;
+    const size_t asg_b = sizeof(int64_t) * (size_t)plan.nodes * E * n;
+    const size_t val_b = sizeof(double) * (size_t)E * plan.seqs;
+    const size_t st_b = sizeof(int32_t) * (size_t)plan.nodes * E;
+    const size_t need = mats_b + asg_b + val_b + st_b + 4 * 256;
+    hipError_t e = hipSuccess;
+    if (h->haal_ws_bytes < need) {
+        e = hipStreamSynchronize(h->stream);
+        hipFree(h->haal_ws);
+        h->haal_ws = nullptr;
+        h->haal_ws_bytes = 0;
+        if (e == hipSuccess) e = hipMalloc(&h->haal_ws, need);
+        if (e != hipSuccess) return rhip(h, e, "asg_real_haal_select (workspace)");
+        h->haal_ws_bytes = need;
+    }
+    auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char *base = static_cast<char *>(h->haal_ws);
+    double *mats = reinterpret_cast<double *>(base);
+    int64_t *assign = reinterpret_cast<int64_t *>(base + align(mats_b));
+    double *values = reinterpret_cast<double *>(base + align(mats_b) + align(asg_b));
+    int32_t *lsa_st = reinterpret_cast<int32_t *>(base + align(mats_b) + align(asg_b) + align(val_b));
+    // nodes are numbered level by level: [node0, node0 + cnt) is one level
+    int node0 = 0;
+    while (node0 < plan.nodes && e == hipSuccess) {
+        int d0 = 0;
+        for (int x = node0; x >= 0; x = plan.node_parent[x]) ++d0;
+        int cnt = 0;
+        while (node0 + cnt < plan.nodes) {
+            int d = 0;
+            for (int x = node0 + cnt; x >= 0; x = plan.node_parent[x]) ++d;
+            if (d != d0) break;
+            ++cnt;
+        }
+        const int64_t rows = (int64_t)cnt * E * n;
+        hipLaunchKernelGGL(asg::haal_matrix_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, h->stream, st,
+                           h->k, plan, node0, cnt, assign, mats);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            const int64_t strides[3] = {(int64_t)n * m, m, 1};
+            e = asg::launch_lsa_batched(mats, ASG_F64, strides, (int64_t)cnt * E, n, m, 1, nullptr,
+                                        assign + (int64_t)node0 * E * n, lsa_st + (int64_t)node0 * E, h->stream);
+        }
+        node0 += cnt;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(asg::haal_values_kernel, dim3((unsigned)(E * plan.seqs)), dim3(256),
+                           sizeof(double) * n + sizeof(int) * m, h->stream, st, h->k, plan, assign, values);
+        e = hipGetLastError();
+    }
+    int32_t *st_env = lsa_st;  // reduced in place into the first E words (row e is env e of level 0)
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(asg::haal_status_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, h->stream, lsa_st,
+                           (int64_t)plan.nodes * E, E, st_env);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(asg::haal_pick_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, h->stream, E, n,
+                           plan.seqs, values, assign, st_env, col_out, best_out, status_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && values_out)
+        e = hipMemcpyAsync(values_out, values, val_b, hipMemcpyDeviceToDevice, h->stream);
+    return e == hipSuccess ? ASG_OK : rhip(h, e, "asg_real_haal_select");
+}
+
 }  // extern "C"
+

@@ -12,7 +12,9 @@
 
 namespace asg {
 
-template <bool VEC4>
+// MASK = false: the argmax ignores availability (the filtered selectors' benefit matrix,
+// filtered_classic_selectors.py:57-61); exploration still draws over the available tasks
+template <bool VEC4, bool MASK>
 __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2,
                                                          const uint8_t *avail, int64_t a0, int64_t a1, int64_t a2,
                                                          int64_t B, int n, int m, float epsilon, uint32_t k0,
@@ -52,7 +54,7 @@ __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t
         for (int c = 0; c < 4; ++c) {
             const int j = j0 + c;
             if (j >= m) continue;
-            const float x = av[c] ? v[c] : -__builtin_inff();
+            const float x = (!MASK || av[c]) ? v[c] : -__builtin_inff();
             if (better(x, j, best, bj)) { best = x; bj = j; }
             cnt += av[c] != 0;
             if (nchunk < 16 && av[c]) availmask_lo |= 1ull << (nchunk * 4 + c);
@@ -123,19 +125,25 @@ __global__ void __launch_bounds__(256) eps_greedy_kernel(const float *q, int64_t
 
 hipError_t launch_eps_greedy(const float *q, const int64_t qs[3], const uint8_t *avail, const int64_t as[3],
                              int64_t B, int n, int m, float epsilon, uint64_t seed, uint32_t counter,
-                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s) {
+                             int64_t row_base, int64_t *out, const int64_t os[2], int *err, hipStream_t s,
+                             bool mask) {
     const int64_t threads = B * n * 16;
     const int64_t blocks = (threads + 255) / 256;
     const bool v4 = qs[2] == 1 && as[2] == 1 && (reinterpret_cast<uintptr_t>(q) % 16) == 0 &&
                     (reinterpret_cast<uintptr_t>(avail) % 4) == 0 && qs[0] % 4 == 0 && qs[1] % 4 == 0 &&
                     as[0] % 4 == 0 && as[1] % 4 == 0;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
-    if (v4)
-        hipLaunchKernelGGL(eps_greedy_kernel<true>, dim3(blocks), dim3(256), 0, s, q, qs[0], qs[1], qs[2], avail,
-                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, row_base, out, os[0], os[1], err);
-    else
-        hipLaunchKernelGGL(eps_greedy_kernel<false>, dim3(blocks), dim3(256), 0, s, q, qs[0], qs[1], qs[2], avail,
-                           as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, row_base, out, os[0], os[1], err);
+#define EG_(V4, MK)                                                                                             \
+    hipLaunchKernelGGL((eps_greedy_kernel<V4, MK>), dim3(blocks), dim3(256), 0, s, q, qs[0], qs[1], qs[2], avail, \
+                       as[0], as[1], as[2], B, n, m, epsilon, k0, k1, counter, row_base, out, os[0], os[1], err)
+    if (v4) {
+        if (mask) EG_(true, true);
+        else EG_(true, false);
+    } else {
+        if (mask) EG_(false, true);
+        else EG_(false, false);
+    }
+#undef EG_
     return hipGetLastError();
 }
 

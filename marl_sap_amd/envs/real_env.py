@@ -175,6 +175,26 @@ class RealAssignEnvBatch(MultiAgentEnv):
         self._call("asg_real_get_returns", ctypes.c_void_p(out.data_ptr()))
         return out
 
+    def haal_select(self, return_values=False):
+        """HAALSelector.select_action (non_rl_selectors.py:54-118) for every env at the
+        current step, on the handle's own state (asg_real_haal_select): float32 [E, n] task
+        ids; with return_values also the float64 [E, S] value of every time-interval
+        sequence (the reference's order) and the int32 [E] index of the winning one.
+        Raises ValueError with scipy's message when an LSA fails (deferred: a status tensor
+        is returned for the runner to flush)."""
+        S = int(_lib.lib().asg_real_haal_num_sequences(self._h))
+        if S <= 0:
+            raise ValueError("HAAL selection after the episode's last step")
+        out = torch.empty((self.num_envs, self.n), dtype=torch.float32, device=self.device)
+        values = torch.empty((self.num_envs, S), dtype=torch.float64, device=self.device)
+        best = torch.empty((self.num_envs,), dtype=torch.int32, device=self.device)
+        status = torch.empty((self.num_envs,), dtype=torch.int32, device=self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._call("asg_real_haal_select", p(out), p(values), p(best), p(status))
+        if return_values:
+            return out, values, best, status
+        return out, status
+
     # ------------------------------------------------------------------ env surface
     def beta_hat(self, beta, prev_assigns):
         """RealConstellationEnv.beta_hat (:259-327): penalty on the l = 0 slice where the

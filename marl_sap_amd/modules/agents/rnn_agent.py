@@ -10,15 +10,16 @@ from ... import _lib
 
 
 class RNNAgent(nn.Module):
-    def __init__(self, input_shape, args):
+    def __init__(self, input_shape, args, n_out=None):
         super().__init__()
         self.args = args
+        self.n_out = args.m if n_out is None else int(n_out)
         self.fc1 = nn.Linear(input_shape, args.hidden_dim)
         if self.args.use_rnn:
             self.rnn = nn.GRUCell(args.hidden_dim, args.hidden_dim)
         else:
             self.rnn = nn.Linear(args.hidden_dim, args.hidden_dim)
-        self.fc2 = nn.Linear(args.hidden_dim, args.m)
+        self.fc2 = nn.Linear(args.hidden_dim, self.n_out)
 
     def init_hidden(self):
         return self.fc1.weight.new(1, self.args.hidden_dim).zero_()
@@ -41,10 +42,10 @@ class RNNFusedAgent(RNNAgent):
     size, n_out = m up to 512 -- the real envs' m = 450 included).  With autograd enabled
     (learner training) it is the plain PyTorch module, so gradients are unchanged."""
 
-    def __init__(self, input_shape, args):
-        super().__init__(input_shape, args)
-        if args.hidden_dim != 64 or not 1 <= args.m <= 512 or input_shape < 1:
-            raise ValueError("rnn_fused needs hidden_dim == 64 and 1 <= m <= 512; use agent 'rnn'")
+    def __init__(self, input_shape, args, n_out=None):
+        super().__init__(input_shape, args, n_out)
+        if args.hidden_dim != 64 or not 1 <= self.n_out <= 512 or input_shape < 1:
+            raise ValueError("rnn_fused needs hidden_dim == 64 and 1 <= n_out <= 512; use agent 'rnn'")
 
     def _prep(self, inputs, hidden_state):
         x = inputs
@@ -68,7 +69,7 @@ class RNNFusedAgent(RNNAgent):
         h_out = torch.empty((R, self.args.hidden_dim), dtype=torch.float32, device=x.device)
         args = [p(x), x.stride(0), R, K, p(h), hs, p(self._packed(K, x.device)), p(self.fc1.bias),
                 p(self.rnn.bias_ih if rnn else self.rnn.bias), p(self.rnn.bias_hh) if rnn else None,
-                p(self.fc2.bias), self.args.hidden_dim, self.args.m, int(rnn), p(h_out)]
+                p(self.fc2.bias), self.args.hidden_dim, self.n_out, int(rnn), p(h_out)]
         return h_out, args, p
 
     def forward(self, inputs, hidden_state):
@@ -77,7 +78,7 @@ class RNNFusedAgent(RNNAgent):
         x, h, hs = self._prep(inputs, hidden_state)
         with torch.cuda.device(x.device):
             h_out, args, p = self._common(x, h, hs)
-            q = torch.empty((x.shape[0], self.args.m), dtype=torch.float32, device=x.device)
+            q = torch.empty((x.shape[0], self.n_out), dtype=torch.float32, device=x.device)
             _lib.check(_lib.lib().asg_rnn_agent_forward(*args, p(q), _lib.stream_ptr(x.device)))
         return q, h_out
 
@@ -107,11 +108,27 @@ class RNNFusedAgent(RNNAgent):
         key = (K, str(device), tuple((w.data_ptr(), w._version) for w in ws if w is not None))
         if getattr(self, "_pack_key", None) != key:
             L = _lib.lib()
-            nbytes = L.asg_rnn_agent_packed_size(K, self.args.hidden_dim, self.args.m, int(bool(rnn)))
+            nbytes = L.asg_rnn_agent_packed_size(K, self.args.hidden_dim, self.n_out, int(bool(rnn)))
             _lib.check(int(nbytes) if nbytes < 0 else 0)
             buf = torch.empty(int(nbytes) // 4, dtype=torch.float32, device=device)
             p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
             _lib.check(L.asg_rnn_agent_pack(p(ws[0]), p(ws[1]), p(ws[2]), p(ws[3]), K, self.args.hidden_dim,
-                                            self.args.m, int(bool(rnn)), p(buf), _lib.stream_ptr(device)))
+                                            self.n_out, int(bool(rnn)), p(buf), _lib.stream_ptr(device)))
             self._pack_buf, self._pack_key = buf, key
         return self._pack_buf
+
+
+class FlatConstAgent(RNNAgent):
+    """FlatConstellationAgent (reference: modules/agents/flat_const_agent.py:9-34): the
+    RNNAgent network with M + 1 outputs (one per top-M task and the baseline), the agent of
+    the filtered real-env algorithms (filtered_reda.yaml, iql_sap.yaml)."""
+
+    def __init__(self, input_shape, args):
+        super().__init__(input_shape, args, n_out=int(args.env_args["M"]) + 1)
+
+
+class FlatConstFusedAgent(RNNFusedAgent):
+    """FlatConstAgent whose no-grad rollout forward is the fused HIP kernel."""
+
+    def __init__(self, input_shape, args):
+        super().__init__(input_shape, args, n_out=int(args.env_args["M"]) + 1)

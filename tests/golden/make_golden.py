@@ -22,6 +22,11 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
   real_variants.npz   RealPowerConstellationEnv / InterferenceConstellationEnv reset/step
   real_runner_dumps.npz  EpisodeRunner + BasicMAC EpisodeBatch dumps over RealConstellationEnv
+  filtered_selectors.npz the filtered selectors' actions with their recorded random draws
+  haal.npz            HAALSelector actions + every time-interval sequence's value
+  replay_buffer.npz   ReplayBuffer ring inserts, counters and seeded samples
+
+  python tests/golden/make_golden.py round2   (only the last three)
 """
 import os
 import sys
@@ -544,12 +549,237 @@ def gen_real_runner_dumps():
     np.savez_compressed(os.path.join(OUT, "real_runner_dumps.npz"), **out)
 
 
+def _f16_topm_tiefree(rng, n, m, L, M, zero_frac):
+    """float16 beta [n, m, L] whose float16 L-sums (torch's Half sum) have M + 1 distinct
+    leading values per agent, so torch.topk's unspecified tie order cannot matter; a
+    `zero_frac` share of each agent's other tasks is all-zero (the real env's invisible
+    tasks, which tie at 0 below the top M)."""
+    import torch as th
+    beta = np.zeros((n, m, L), dtype=np.float16)
+    for i in range(n):
+        while True:
+            row = rng.uniform(0.0, 1.5, size=(m, L)).astype(np.float16)
+            zero = rng.uniform(size=m) < zero_frac
+            zero[rng.choice(m, M + 1, replace=False)] = False
+            row[zero] = 0
+            tot = th.from_numpy(row).sum(-1).numpy().astype(np.float64)
+            top = np.sort(tot)[::-1][:M + 1]
+            if np.all(np.diff(top) < 0):
+                beta[i] = row
+                break
+    return beta
+
+
+def gen_filtered_selectors():
+    """FilteredSAPActionSelector / FilteredEpsGrSAPTestActionSelector
+    (filtered_sap_selectors.py:7-148) and FilteredEpsilonGreedyActionSelector
+    (filtered_classic_selectors.py:6-67) called on seeded Q-values [B, n, M+1] and float16
+    beta [B, n, m, L].  Every torch.rand_like / torch.normal draw the selectors make is
+    recorded (the 1e-8 tie-breaking noise, the Gaussian exploration noise), so the GPU
+    selectors can be fed the same draws and compared bit for bit.  The top-M boundary of
+    every row is tie-free (torch.topk leaves tie order unspecified)."""
+    import torch as th
+    th.set_num_threads(1)
+    import action_selectors.filtered_sap_selectors as fsap
+    import action_selectors.filtered_classic_selectors as fcls
+
+    rec = {"rand_like": [], "normal": []}
+    real_rand_like, real_normal = th.rand_like, th.normal
+
+    def rand_like(*a, **k):
+        r = real_rand_like(*a, **k)
+        rec["rand_like"].append(r.clone())
+        return r
+
+    def normal(*a, **k):
+        r = real_normal(*a, **k)
+        rec["normal"].append(r.clone())
+        return r
+
+    out = {}
+    rng = np.random.RandomState(777)
+    # (tag, selector class, B, n, m, M, L, epsilon, test_mode, q scale, zero_frac)
+    cases = [("sap_e0", "sap", 3, 10, 24, 4, 3, 0.0, False, 1.0, 0.5),
+             ("sap_e03", "sap", 3, 12, 30, 6, 3, 0.3, False, 1.0, 0.3),
+             ("sap_small_q", "sap", 2, 9, 20, 4, 2, 0.0, False, 1e-3, 0.6),
+             ("sap_eval", "sap", 2, 8, 16, 4, 3, 0.7, True, 1.0, 0.0),
+             ("egsap_test", "egsap", 3, 10, 24, 4, 3, 0.5, True, 1.0, 0.5),
+             ("egsap_train_e0", "egsap", 3, 10, 24, 4, 3, 0.0, False, 1e-2, 0.5),
+             ("eg_e0", "eg", 4, 12, 40, 6, 3, 0.0, False, 1.0, 0.4),
+             ("eg_eval", "eg", 2, 7, 18, 5, 2, 0.9, True, 1e-3, 0.0),
+             ("sap_big", "sap", 2, 36, 60, 10, 3, 0.0, False, 1.0, 0.7)]
+    with mock.patch.object(th, "rand_like", rand_like), mock.patch.object(th, "normal", normal):
+        for tag, kind, B, n, m, M, L, eps, test_mode, qs, zf in cases:
+            q = (rng.standard_normal((B, n, M + 1)) * qs).astype(np.float32)
+            # the baseline (column M) near the other values: exact float32 ties among the
+            # "do nothing" columns where the 1e-8 noise rounds away
+            beta = np.stack([_f16_topm_tiefree(rng, n, m, L, M, zf) for _ in range(B)])
+            avail = np.ones((B, n, m), dtype=np.int64)
+            args = SimpleNamespace(epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1000,
+                                   evaluation_epsilon=0.0, use_mps_action_selection=False, device="cpu",
+                                   env_args={"M": M})
+            cls = {"sap": fsap.FilteredSAPActionSelector, "egsap": fsap.FilteredEpsGrSAPTestActionSelector,
+                   "eg": fcls.FilteredEpsilonGreedyActionSelector}[kind]
+            sel = cls(args)
+            rec["rand_like"].clear()
+            rec["normal"].clear()
+            th.manual_seed(1234)
+            acts = sel.select_action(th.from_numpy(q), th.from_numpy(avail), 0, test_mode=test_mode,
+                                     beta=th.from_numpy(beta))
+            out[f"{tag}__q"] = q
+            out[f"{tag}__beta"] = beta
+            out[f"{tag}__cfg"] = np.array([B, n, m, M, L, int(test_mode)])
+            out[f"{tag}__kind"] = np.array(kind)
+            out[f"{tag}__epsilon"] = np.array(eps)
+            out[f"{tag}__actions"] = acts.numpy()
+            out[f"{tag}__actions_dtype"] = np.array(str(acts.dtype))
+            # tie noise: one [n, m] draw per env (the SAP loops) or one [B, n, m] draw
+            tie = [r.numpy() for r in rec["rand_like"] if r.dim() >= 2 and r.shape[-1] == m]
+            out[f"{tag}__tie_noise"] = np.stack(tie).reshape(B, n, m)
+            gauss = [r.numpy() for r in rec["normal"]]
+            if gauss:
+                out[f"{tag}__gauss_noise"] = np.stack(gauss).reshape(B, n, m)
+    out["cases"] = np.array([c[0] for c in cases])
+    np.savez_compressed(os.path.join(OUT, "filtered_selectors.npz"), **out)
+
+
+def gen_haal():
+    """HAALSelector (non_rl_selectors.py:54-118) over RealConstellationEnv (injected
+    benefits): the reference's own selector on deep-copied envs at several steps, plus the
+    value of every time-interval sequence computed by the same deepcopy + step loop (the
+    selector discards them; the GPU form reports them)."""
+    import copy
+    import torch as th
+    from envs.real_constellation_env import RealConstellationEnv
+    from action_selectors.non_rl_selectors import HAALSelector
+    from utils.methods import generate_all_time_intervals, build_time_interval_sequences
+    import scipy.optimize as so
+    rng = np.random.RandomState(99)
+    out = {}
+    # (n, m, T, L, N, M, lambda, prios, T_trans, steps before the selection)
+    specs = [(6, 10, 5, 3, 2, 4, 0.5, False, False, 0),
+             (8, 14, 6, 3, 2, 4, 0.5, True, False, 2),
+             (7, 12, 6, 4, 2, 4, 0.3, False, True, 1),
+             (5, 9, 5, 3, 2, 4, 1.5, True, False, 3),
+             (9, 16, 7, 2, 3, 6, 0.5, False, False, 4)]
+    for idx, (n, m, T, L, N, M, lam, use_prios, use_tt, pre) in enumerate(specs):
+        B = 3
+        envs, tables, prev_l = [], [], []
+        prios = rng.uniform(0.5, 2.0, size=m) if use_prios else None
+        T_trans = (rng.uniform(size=(m, m)) > 0.4).astype(np.float64) if use_tt else None
+        for b in range(B):
+            table = rng.uniform(0.01, 1.0, size=(n, m, T))
+            table[rng.uniform(size=table.shape) < 0.3] = 0.0  # invisible pairs: beta_hat mask
+            env = RealConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(), graphs=[None] * T,
+                                       T_trans=None if T_trans is None else T_trans.copy(),
+                                       task_prios=None if prios is None else prios.copy())
+            env.reset()
+            for t in range(pre):
+                env.step(list(rng.randint(0, m, size=n)))
+            envs.append(env)
+            tables.append(table)
+            prev_l.append(np.asarray(env.prev_assigns, dtype=np.int64))
+        args = SimpleNamespace(runner="episode", use_mps_action_selection=False, device="cpu")
+        sel = HAALSelector(args)
+        sel.envs = envs
+        scheme = {"beta": {"vshape": (n, m, L), "part_of_state": True},
+                  "prev_assigns": {"vshape": (n,), "part_of_state": True}}
+        batch = SimpleNamespace(scheme=scheme)
+        beta5 = th.zeros((B, 1, n, m, envs[0].L))
+        batch_get = {"beta": beta5}
+        batch = type("B", (), {"scheme": scheme, "__getitem__": lambda self, k: batch_get[k]})()
+        acts = sel.select_action(batch).numpy()
+        # the discarded per-sequence values: the selector's own loop, recorded
+        eff = min(envs[0].L, envs[0].T - envs[0].k)
+        seqs = build_time_interval_sequences(generate_all_time_intervals(eff), eff)
+        vals = np.zeros((B, len(seqs)))
+        for b in range(B):
+            for s, tis in enumerate(seqs):
+                e = copy.deepcopy(envs[b])
+                tot = 0
+                for ti in tis:
+                    bh = e.beta_hat(e.beta, e.prev_assigns)
+                    _, a = so.linear_sum_assignment(bh.sum(axis=-1), maximize=True)
+                    for _ in range(ti[1] - ti[0] + 1):
+                        r, _, _ = e.step(a)
+                        tot += sum(r)
+                vals[b, s] = tot
+        out[f"h{idx}_spec"] = np.array([B, n, m, T, envs[0].L, N, M, pre, envs[0].k])
+        out[f"h{idx}_lambda"] = np.array(lam)
+        out[f"h{idx}_tables"] = np.stack(tables)
+        out[f"h{idx}_prios"] = prios if prios is not None else np.ones(m)
+        out[f"h{idx}_T_trans"] = T_trans if T_trans is not None else np.ones((m, m)) - np.eye(m)
+        out[f"h{idx}_prev"] = np.stack(prev_l)
+        out[f"h{idx}_actions"] = acts
+        out[f"h{idx}_values"] = vals
+        out[f"h{idx}_seqs"] = np.array([[t for ti in tis for t in ti] + [-1] * (2 * eff - 2 * len(tis))
+                                        for tis in seqs])
+    out["n_cases"] = np.array(len(specs))
+    np.savez_compressed(os.path.join(OUT, "haal.npz"), **out)
+
+
+def gen_replay_buffer():
+    """ReplayBuffer (components/episode_buffer.py:237-277): ring inserts of EpisodeBatches
+    of 2, 2 and 3 episodes into a 5-episode buffer (the last one wraps: split insert), the
+    buffer's contents and counters after each insert, then sample(3) under
+    np.random.seed(7) and sample(5) (= the whole buffer)."""
+    import torch as th
+    from components.episode_buffer import EpisodeBatch, ReplayBuffer
+    from components.transforms import OneHot
+    n, m, T = 3, 5, 4
+    scheme = {"obs": {"vshape": 7, "group": "agents"},
+              "actions": {"vshape": (1,), "group": "agents", "dtype": th.long},
+              "avail_actions": {"vshape": (m,), "group": "agents", "dtype": th.int},
+              "rewards": {"vshape": (n,)},
+              "terminated": {"vshape": (1,), "dtype": th.uint8},
+              "beta": {"vshape": (n, m)}}
+    groups = {"agents": n}
+    pre = {"actions": ("actions_onehot", [OneHot(out_dim=m)])}
+    rng = np.random.RandomState(5)
+    buf = ReplayBuffer(scheme, groups, 5, T + 1, preprocess=pre, device="cpu")
+    out = {}
+    for k, bs in enumerate([2, 2, 3]):
+        eb = EpisodeBatch(scheme, groups, bs, T + 1, preprocess=pre, device="cpu")
+        inp = {}
+        for t in range(T + 1):
+            d = {"obs": rng.standard_normal((bs, n, 7)).astype(np.float32),
+                 "avail_actions": rng.randint(0, 2, size=(bs, n, m)).astype(np.int32),
+                 "beta": rng.uniform(size=(bs, n, m)).astype(np.float32)}
+            if t < T:
+                d.update(actions=rng.randint(0, m, size=(bs, n, 1)).astype(np.int64),
+                         rewards=rng.standard_normal((bs, n)).astype(np.float32),
+                         terminated=np.full((bs, 1), t == T - 1, dtype=np.uint8))
+            eb.update({kk: th.from_numpy(v) for kk, v in d.items()}, ts=t)
+            for kk, v in d.items():
+                inp.setdefault(kk, []).append(v)
+        for kk, v in inp.items():
+            out[f"ins{k}__{kk}"] = np.stack(v, axis=1)
+        buf.insert_episode_batch(eb)
+        for kk, v in buf.data.transition_data.items():
+            out[f"after{k}__{kk}"] = v.numpy().copy()  # the buffer is overwritten in place later
+        out[f"after{k}__counters"] = np.array([buf.buffer_index, buf.episodes_in_buffer])
+    np.random.seed(7)
+    s = buf.sample(3)
+    for kk, v in s.data.transition_data.items():
+        out[f"sample3__{kk}"] = v.numpy().copy()
+    s = buf.sample(5)
+    for kk, v in s.data.transition_data.items():
+        out[f"sample5__{kk}"] = v.numpy().copy()
+    out["cfg"] = np.array([n, m, T, 5])
+    np.savez_compressed(os.path.join(OUT, "replay_buffer.npz"), **out)
+
+
 if __name__ == "__main__":
     _install_stubs()
     if sys.argv[1:] == ["real_env"]:  # regenerate only the RealConstellationEnv fixtures
         gen_real_env()
         gen_real_variants()
         gen_real_runner_dumps()
+        sys.exit(0)
+    if sys.argv[1:] == ["round2"]:  # the selector / buffer fixtures added in round 2
+        gen_filtered_selectors()
+        gen_haal()
+        gen_replay_buffer()
         sys.exit(0)
     gen_real_env()
     gen_real_variants()
@@ -559,6 +789,9 @@ if __name__ == "__main__":
     gen_lsa()
     gen_runner_dumps()
     gen_real_runner_dumps()
+    gen_filtered_selectors()
+    gen_haal()
+    gen_replay_buffer()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

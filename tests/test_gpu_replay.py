@@ -45,3 +45,12 @@ def test_device_replay_buffer_matches_cpu_buffer():
     cs = cbuf.sample(5, rng=np.random.RandomState(7))
     for k in cs.data.transition_data:
         assert gs[k].is_cuda and torch.equal(gs[k].cpu(), cs[k]), k
+
+
+@pytest.mark.parametrize("time_major", [False, True])
+def test_device_replay_buffer_matches_reference(golden, time_major):
+    """The device buffer against the reference ReplayBuffer's own dump: contents and
+    counters after ring inserts (a split insert included), and sample() under
+    np.random.seed(7) (tests/golden/replay_buffer.npz)."""
+    from tests.replay_fixture import check_against_reference
+    check_against_reference(golden("replay_buffer"), "cuda", time_major)

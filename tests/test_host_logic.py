@@ -138,3 +138,24 @@ def test_bench_accounting():
     # roof: f32 MFMA everywhere, or the GRU's 49,152 flops at 2.5 PF / 6 (split bf16)
     assert bench.agent_peak(64, 64, 3, 0) == pytest.approx(157.3)
     assert bench.agent_peak(64, 64, 3, 1) == pytest.approx(81920 / (32768 / 157.3 + 49152 / (2500 / 6)))
+
+
+@pytest.mark.parametrize("time_major", [False, True])
+def test_replay_buffer_matches_reference(golden, time_major):
+    """Ring inserts (a split insert included), counters and seeded sample() against the
+    reference ReplayBuffer's own outputs (tests/golden/replay_buffer.npz)."""
+    from tests.replay_fixture import check_against_reference
+    check_against_reference(golden("replay_buffer"), "cpu", time_major)
+
+
+def test_continuous_selector_cpu():
+    from types import SimpleNamespace
+    import torch
+    from marl_sap_amd.action_selectors import REGISTRY
+    args = SimpleNamespace(epsilon_start=0.5, epsilon_finish=0.1, epsilon_anneal_time=100, evaluation_epsilon=0.0)
+    sel = REGISTRY["continuous"](args)
+    x = torch.randn(4, 3, 5)
+    assert torch.equal(sel.select_action(x, None, 0, test_mode=True), x)
+    torch.manual_seed(0)
+    y = sel.select_action(x, None, 200)  # annealed to epsilon_finish
+    assert sel.variance == 0.1 and 0.05 < float((y - x).std()) < 0.15

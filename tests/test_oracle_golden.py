@@ -139,3 +139,44 @@ def test_real_variant_oracle_matches_reference_fixture(golden, oracle):
             np.testing.assert_array_equal(env.beta, d[f"v{c}_beta"][t])
             np.testing.assert_array_equal(env.prev_assigns, d[f"v{c}_prev"][t])
             assert done == bool(d[f"v{c}_done"][t])
+
+
+# ---- round 2: filtered selectors, HAALSelector (oracle/selectors.py) -------------------
+def test_f16_total_beta_matches_torch(golden):
+    """The oracle's float16 L-sum is torch's Half sum (float32 accumulation, one rounding)."""
+    import torch
+    from oracle.selectors import total_beta_f16
+    g = golden("filtered_selectors")
+    for c in g["cases"]:
+        beta = g[f"{c}__beta"]
+        np.testing.assert_array_equal(total_beta_f16(beta), torch.from_numpy(beta).sum(-1).numpy())
+
+
+def test_filtered_selectors_oracle(golden, oracle):
+    from oracle import selectors as osel
+    g = golden("filtered_selectors")
+    for c in g["cases"]:
+        B, n, m, M, L, test_mode = [int(x) for x in g[f"{c}__cfg"]]
+        kind = str(g[f"{c}__kind"])
+        q, beta, tie = g[f"{c}__q"], g[f"{c}__beta"], g[f"{c}__tie_noise"]
+        if kind == "sap" or (kind == "egsap" and test_mode):
+            gauss = g[f"{c}__gauss_noise"] if f"{c}__gauss_noise" in g else None
+            got = osel.filtered_sap(q, beta, M, tie, gauss)
+        else:
+            got = osel.filtered_greedy(q, beta, M, tie)
+        np.testing.assert_array_equal(got, g[f"{c}__actions"], err_msg=str(c))
+
+
+def test_haal_oracle(golden, oracle):
+    from oracle import selectors as osel
+    g = golden("haal")
+    for c in range(int(g["n_cases"])):
+        B, n, m, T, L, N, M, pre, k = [int(x) for x in g[f"h{c}_spec"]]
+        for b in range(B):
+            a, vals = osel.haal(g[f"h{c}_tables"][b], g[f"h{c}_prios"], g[f"h{c}_T_trans"], float(g[f"h{c}_lambda"]),
+                                k, g[f"h{c}_prev"][b], L, T)
+            np.testing.assert_array_equal(a, g[f"h{c}_actions"][b])
+            np.testing.assert_array_equal(vals, g[f"h{c}_values"][b])
+        seqs = osel.time_interval_sequences(min(L, T - k))
+        flat = [[t for ti in s for t in ti] for s in seqs]
+        assert [list(r[r >= 0]) for r in g[f"h{c}_seqs"]] == flat
