@@ -24,6 +24,17 @@
 #include "asg_device.h"
 #include "asg_internal.h"
 
+// The library builds with -ffp-contract=off so the env and LSA kernels round every float64
+// add/mul as numpy does.  The agent's results are fp32-accurate, not bit-matched to a
+// reference order, so its elementwise math (bias epilogues, GRU gates, Q unscaling) may
+// fuse into FMAs: fewer VALU instructions, one rounding instead of two.
+#ifndef ASG_AGENT_CONTRACT
+#define ASG_AGENT_CONTRACT 1
+#endif
+#if ASG_AGENT_CONTRACT
+#pragma clang fp contract(fast)
+#endif
+
 namespace asg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -936,6 +947,44 @@ __device__ __forceinline__ void split2(const float (&x)[8], u32x4v &h, u32x4v &l
         l[p] = __builtin_bit_cast(uint32_t, ll);
     }
 }
+// The split of 8 UNSCALED values at scale sc (a power of two): h = RNE_f16(x * sc) and
+// l = RNE_f16(x * sc - h), the same planes as split2 of the scaled values.  ASG_H2_MIX: the
+// residual is one v_fma_mix{lo,hi}_f16 per value (fma(x, sc, -h) is exact in f32, rounded
+// once to f16) instead of convert-back + subtract + convert.
+#ifndef ASG_H2_MIX
+#define ASG_H2_MIX 1
+#endif
+__device__ __forceinline__ void split2s(const float (&x)[8], float sc, u32x4v &h, u32x4v &l) {
+#if ASG_H2_MIX
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f16x2v hh = {(_Float16)(x[2 * p] * sc), (_Float16)(x[2 * p + 1] * sc)};
+        const uint32_t hv = __builtin_bit_cast(uint32_t, hh);
+        uint32_t lv = 0;
+        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "+v"(lv) : "v"(x[2 * p]), "v"(sc), "v"(hv));
+        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "+v"(lv)
+            : "v"(x[2 * p + 1]), "v"(sc), "v"(hv));
+        h[p] = hv;
+        l[p] = lv;
+    }
+#else
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[j] * sc;
+    split2(v, h, l);
+#endif
+}
+// max(m, |a|, |b|) in one v_max3_f32 (fmaxf on |x| otherwise canonicalises every input)
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+#if ASG_H2_MIX
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+#else
+    return fmaxf(m, fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)));
+#endif
+}
 // 2^s as a float (s clamped to the normal range [-126, 127])
 __device__ __forceinline__ float pow2f(int s) {
     s = s < -126 ? -126 : (s > 127 ? 127 : s);
@@ -951,12 +1000,10 @@ __device__ __forceinline__ float wave_max_f32(float v) {
     return wave_allreduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 __device__ __forceinline__ float absmax4(float m, const float4 &v) {
-    return fmaxf(fmaxf(m, fmaxf(__builtin_fabsf(v.x), __builtin_fabsf(v.y))),
-                 fmaxf(__builtin_fabsf(v.z), __builtin_fabsf(v.w)));
+    return max3_abs(max3_abs(m, v.x, v.y), v.z, v.w);
 }
 __device__ __forceinline__ float absmax4(float m, const f32x4 &v) {
-    return fmaxf(fmaxf(m, fmaxf(__builtin_fabsf(v[0]), __builtin_fabsf(v[1]))),
-                 fmaxf(__builtin_fabsf(v[2]), __builtin_fabsf(v[3])));
+    return max3_abs(max3_abs(m, v[0], v[1]), v[2], v[3]);
 }
 
 // packed h2 section (u32x4v units): [header 1: int sw1, sw_ih, sw_hh, sw2]
@@ -995,6 +1042,14 @@ constexpr int kH2XBuf = ASG_H2_XBUF;
 #define ASG_H2_WAVES 2
 #endif
 constexpr int kH2NT = ASG_H2_NT, kH2WavesPerSimd = ASG_H2_WAVES, kH2Waves = 4 * ASG_H2_WAVES;
+#ifndef ASG_H2_LATE_H
+#define ASG_H2_LATE_H 1
+#endif
+// one-hot columns gathered at the tile start into the fc1 accumulators (0) or added at the
+// fc1 tail (1)
+#ifndef ASG_H2_GATHER_TAIL
+#define ASG_H2_GATHER_TAIL 0
+#endif
 // keep h_in as f32 through the GRU for its update (1) or rebuild it from its f16 planes (0)
 #ifndef ASG_H2_KEEP_H
 #define ASG_H2_KEEP_H 0
@@ -1074,14 +1129,20 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
 #pragma unroll
     for (int b = 0; b < kH2XBuf; ++b)
         if (s0 + b < nsl) load_x(s0 + b, xbuf[b]);
-    // h_in fragments: needed from the GRU on, so issued behind the observations
+    // h_in fragments: needed from the GRU on, so issued behind the observations (or, with
+    // ASG_H2_LATE_H, after the fc1 main loop: 32 fewer VGPRs live through fc1)
     float4 hB[4][NT];
+    auto load_h = [&]() {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs + 16 * t + 4 * q)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int nt = 0; nt < NT; ++nt)
+                hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs + 16 * t + 4 * q)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+#if !ASG_H2_LATE_H
+    load_h();
+#endif
 
     // ---- one-hot prefix (see agent_rows): rows whose first P inputs are onehot(a) or zero
     // add W1[:, a] (W1T, f32) instead of running those slices' MFMAs
@@ -1123,6 +1184,18 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
     f32x4 acc[4][NT];
     int sx = sx_obs;
     float tmax = 0.f;
+#if ASG_H2_GATHER_TAIL
+    // the one-hot columns W1[:, a] are gathered now and added after the main loop: their
+    // L2 latency hides under the observation MFMAs instead of delaying the first one
+    float4 g1[4][NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+            g1[mt][nt] = (onehot && pos[nt] >= 0)
+                             ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     for (int attempt = 0;; ++attempt) {
         if (attempt > 0) {
 #pragma unroll
@@ -1130,6 +1203,13 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
                 if (s0 + b < nsl) load_x(s0 + b, xbuf[b]);
         }
         const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
+#if ASG_H2_GATHER_TAIL
+        (void)scS;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -1139,6 +1219,7 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                 acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
             }
+#endif
 #ifdef ASG_STAMP_FC1
         if (attempt == 0) {
             // wait for the gathered W1 columns here so the stamp measures their latency
@@ -1155,9 +1236,9 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 m = absmax4(absmax4(m, xv[0][nt]), xv[1][nt]);
-                const float v8[8] = {xv[0][nt].x * scx, xv[0][nt].y * scx, xv[0][nt].z * scx, xv[0][nt].w * scx,
-                                     xv[1][nt].x * scx, xv[1][nt].y * scx, xv[1][nt].z * scx, xv[1][nt].w * scx};
-                split2(v8, xp[nt][0], xp[nt][1]);
+                const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
+                                     xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
+                split2s(x8, scx, xp[nt][0], xp[nt][1]);
             }
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
@@ -1191,6 +1272,9 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
                 }
             }
         }
+#if ASG_H2_LATE_H
+        if (attempt == 0) load_h();
+#endif
         tmax = wave_max_f32(m);
 #ifdef ASG_STAMP_FC1
         if (attempt == 0) ASG_STAMP(6);
@@ -1209,8 +1293,15 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
             const f32x4 bb = Bs[4 * mt + q];  // b1[16 mt + 4 q ..]
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
+#if ASG_H2_GATHER_TAIL
+                // unscaled products + the gathered one-hot column + bias
+                const f32x4 gv = f32x4{g1[mt][nt].x, g1[mt][nt].y, g1[mt][nt].z, g1[mt][nt].w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + gv[v] + bb[v], 0.f);
+#else
 #pragma unroll
                 for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
+#endif
             }
         }
     }
@@ -1281,11 +1372,11 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
                 for (int c = 0; c < 2; ++c)
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
-                        v8[4 * c + v] = xB[2 * sl + c][nt][v] * cx;
-                        h8[4 * c + v] = comp(hB[2 * sl + c][nt], v) * ch;
+                        v8[4 * c + v] = xB[2 * sl + c][nt][v];
+                        h8[4 * c + v] = comp(hB[2 * sl + c][nt], v);
                     }
-                split2(v8, xP[sl][nt][0], xP[sl][nt][1]);
-                split2(h8, hP[sl][nt][0], hP[sl][nt][1]);
+                split2s(v8, cx, xP[sl][nt][0], xP[sl][nt][1]);
+                split2s(h8, ch, hP[sl][nt][0], hP[sl][nt][1]);
             }
     }
     // sigmoid(g * 2^-Sg) = 1 / (1 + 2^(g * c1)), tanh(y * 2^-Sg) = 2 / (1 + 2^(y * c2)) - 1
@@ -1382,8 +1473,8 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) v8[4 * c + v] = hp[2 * sl + c][nt][v] * c3;
-                split2(v8, hq[sl][nt][0], hq[sl][nt][1]);
+                    for (int v = 0; v < 4; ++v) v8[4 * c + v] = hp[2 * sl + c][nt][v];
+                split2s(v8, c3, hq[sl][nt][0], hq[sl][nt][1]);
             }
     }
     float best[NT];
@@ -1433,9 +1524,11 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
                 if (SEL) {
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
+                        // a lane meets its tasks in increasing j, so torch.max order reduces
+                        // to: the first candidate, then strictly greater, or the first NaN
                         const int j = j0 + v;
                         const float x = ((av[nt] >> v) & 1u) ? qv[v] : -__builtin_inff();
-                        const bool b = better(x, j, best[nt], bj[nt]);
+                        const bool b = (bj[nt] == 0x7fffffff) | ((best[nt] == best[nt]) & !(x <= best[nt]));
                         best[nt] = b ? x : best[nt];
                         bj[nt] = b ? j : bj[nt];
                     }
@@ -1745,7 +1838,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     const bool fc2x3 = use_rnn && !gen && W2x3g && w2_lds == wr_f4 && w2hm_f4 <= w2_f4;
     if (!gen && h2_shape(K, nout, use_rnn) && use_h2_kernel()) {
         int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         ncu = stream_cus(s, ncu);
         H2Args ha;
         ha.X = X;
@@ -1790,7 +1883,7 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
     }
     if (use_lds_weights() && lds <= 160 * 1024) {
         int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         ncu = stream_cus(s, ncu);
         const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
