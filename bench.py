@@ -135,20 +135,30 @@ def agent_roofline(a, E, agent_ms, kernel):
                                                         "time-weighted")}
     hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
            "bytes_per_launch": nbytes}
+    # PMC HBM bytes of the same kernel at this workload (FETCH_SIZE doubled for its 16-B/lane
+    # streaming reads, + WRITE_SIZE; tools/pmc_summary.py), when profiled
+    pm = pmc_lookup("*pmc_agent_hbm*.json", n=a.n, m=a.m, E=E) if fused else None
+    traffic = None
+    if pm and pm.get("kernel") in pm.get("kernels", {}):
+        traffic = round(pm["kernels"][pm["kernel"]]["hbm_bytes_fetch_doubled"])
+        hbm["traffic"] = traffic
     top = hbm if hbm["frac"] >= mfma["frac"] else mfma
     return {"bound": "hbm" if top is hbm else "mfma", "achieved": top["achieved"], "peak": top["peak"],
-            "unit": top["unit"], "frac": top["frac"], "traffic": None, "mfma": mfma, "hbm": hbm,
+            "unit": top["unit"], "frac": top["frac"], "traffic": traffic if top is hbm else None, "mfma": mfma,
+            "hbm": hbm,
             "kernel": kernel, "kernel_ms": round(agent_ms, 4), "flops_per_launch": flops}
 
 
 def pmc_lookup(pattern, **match):
     """First profiles/ summary matching the workload keys (n, m, E, L), else None."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+    # newest round first: profiles are named r<round>_..., the round-1 files carry no prefix
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
         try:
             pm = json.load(open(path))
         except (ValueError, OSError):
             continue
         if all(pm.get(k) == v for k, v in match.items()):
+            pm["_path"] = path
             return pm
     return None
 
@@ -353,14 +363,19 @@ def lsa_roofline(a, E, res):
            "path_steps_per_launch": steps, "path_steps_per_s": round(per_s, 1),
            "cycles_per_step_per_simd": round(cyc, 1), "achieved": None, "peak": None, "frac": None,
            "unit": "wave-VALU-instr/s", "traffic": None}
-    pm = pmc_lookup("pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
+    pm = pmc_lookup("*pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
     if pm and pm.get("valu_insts_per_path_step"):
         vps = pm["valu_insts_per_path_step"]
         peak = SIMDS * CLOCK_HZ / VALU_CYCLES_PER_WAVE_INSTR
         ach = vps * per_s
         out.update({"achieved": round(ach / 1e9, 2), "peak": round(peak / 1e9, 2), "unit": "G wave-VALU-instr/s",
                     "frac": round(ach / peak, 4), "valu_insts_per_path_step": round(vps, 2),
-                    "issue_bound_cycles_per_step": round(vps * VALU_CYCLES_PER_WAVE_INSTR, 1)})
+                    "issue_bound_cycles_per_step": round(vps * VALU_CYCLES_PER_WAVE_INSTR, 1),
+                    "pmc": os.path.basename(pm.get("_path", "")) or None})
+        if pm.get("salu_insts_per_path_step"):
+            # the scalar unit is shared by a CU's 4 SIMDs: one SALU issue per SIMD per 4 cycles
+            out["salu_insts_per_path_step"] = round(pm["salu_insts_per_path_step"], 2)
+            out["salu_bound_cycles_per_step"] = round(pm["salu_insts_per_path_step"] * 4, 1)
     return out
 
 
@@ -381,7 +396,7 @@ def main():
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     per_launch = step_bytes(a.n, a.m, a.L) * E
     achieved = per_launch / (kern_ms * 1e-3) / 1e9
-    pm = pmc_lookup("pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    pm = pmc_lookup("*pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
     traffic = pm.get("hbm_bytes_per_launch") if pm else None
 
     secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))

@@ -71,10 +71,10 @@ def main():
     torch.cuda.set_device(dev)
     g = torch.Generator(device=dev).manual_seed(0)
     if a.scan:
-        prof = torch.randn((16384, 1, 64), generator=g, device=dev)
-        q = prof + 0.05 * torch.randn((16384, 64, 64), generator=g, device=dev)
+        prof = torch.randn((65536, 1, 64), generator=g, device=dev)
+        q = prof + 0.05 * torch.randn((65536, 64, 64), generator=g, device=dev)
         res = {}
-        for B in (256, 1024, 2048, 4096, 5120, 8192, 16384):
+        for B in (256, 1024, 2048, 4096, 5120, 8192, 10240, 15360, 16384, 20480, 32768, 65536):
             ms = timed(lambda: linear_sum_assignment_batched(q[:B], maximize=True, return_status=True), a.iters)
             res[B] = round(ms, 4)
         print(json.dumps({"scan_sap64_corr_ms": res}))

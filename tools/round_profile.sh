@@ -19,4 +19,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_256" -o run -- python3 $B --config 4 --steps 20 --warmup 5 > "$OUT/fetch_256.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_256" -o run -- python3 $B --config 4 --steps 20 --warmup 5 > "$OUT/write_256.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5 > "$OUT/kt_sap.log" 2>&1 &&
+timeout -k 10 300 python bench.py --selector sap --cpu-baseline 0 --secondary 0 --steps 20 --warmup 5 > "$OUT/bench_sap.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5 > "$OUT/sq_sap.log" 2>&1 &&
 timeout -k 10 300 python tools/bench_lsa.py > "$OUT/bench_lsa.json" 2>&1
