@@ -185,6 +185,8 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--fused-rollout", type=int, default=0,
+                   help="1: env step t + agent/eps-greedy t+1 in one kernel (asg_step_select)")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -205,7 +207,7 @@ def make_args(a, E, selector=None, agent=None):
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
         agent=agent or a.agent, seed=a.seed,
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac",
-        reuse_batch=True)
+        reuse_batch=True, fused_rollout=bool(a.fused_rollout))
 
 
 class NullLogger:
@@ -277,6 +279,13 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     if selector == "sap":
         sel_obj.select_action = timed_select
 
+    # the runner's schedule (GpuVecRunner.rollout): with the fused agent + epsilon-greedy, env.step(t)
+    # and the selection for t + 1 are one kernel (asg_step_select) for t < T - 1; the first selection
+    # of an episode and its last step are the separate kernels.  Either way one "step" = one env
+    # transition plus one selection (over an episode: T of each).
+    fused_pairs = []
+    state["selected"] = False
+
     def one_step():
         if state["t"] >= a.T:
             if runner.batch is not None and runner.env.k == a.T:
@@ -284,25 +293,33 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
             runner.reset()
             mac.init_hidden(E)
             state["t"] = 0
+            state["selected"] = False
         t = state["t"]
         with torch.no_grad():
             timing = state["timing"]
-            if timing:
-                a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a0.record()
+            if "fused" not in state:
+                state["fused"] = selector != "random" and mac.fused_step_ok(env, runner.batch)
+            fused = state["fused"]
+
+            def timed(pairs, fn):
+                if not timing:
+                    return fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                pairs.append((e0, e1))
+
             if selector == "random":
-                env.random_actions(runner.batch, ts=t)
+                timed(sel_pairs, lambda: env.random_actions(runner.batch, ts=t))
+            elif not state["selected"]:
+                timed(sel_pairs, lambda: runner.select_into_batch(t))
+            if fused and t + 1 < a.T:
+                timed(fused_pairs, lambda: mac.fused_step_select(env, runner.batch, t, runner.t_env))
+                state["selected"] = True
             else:
-                runner.select_into_batch(t)
-            if timing:
-                a1.record()
-                sel_pairs.append((a0, a1))
-                s0.record()
-            env.step(runner.batch, ts=t)
-            if timing:
-                s1.record()
-                ev_pairs.append((s0, s1))
+                timed(ev_pairs, lambda: env.step(runner.batch, ts=t))
+                state["selected"] = False
         state["t"] = t + 1
 
     for _ in range(warmup):
@@ -322,7 +339,8 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     runner.flush_pending()  # surfaces any sticky device error of the timed steps
     mean = lambda prs: sum(s.elapsed_time(e) for s, e in prs) / len(prs) if prs else 0.0  # noqa: E731
     res = {"elapsed": elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
-           "lsa_ms": mean(lsa_pairs) if lsa_pairs else None}
+           "lsa_ms": mean(lsa_pairs) if lsa_pairs else None,
+           "fused_ms": mean(fused_pairs) if fused_pairs else None, "fused": bool(state.get("fused"))}
     if count_lsa and selector == "sap" and a.n <= a.m <= 64:
         # one more selection on the current state, with the step-counting kernel instance
         sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
@@ -394,9 +412,17 @@ def main():
     G = res["global_envs"]
     value = G * a.steps / res["elapsed"]
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
-    per_launch = step_bytes(a.n, a.m, a.L) * E
-    achieved = per_launch / (kern_ms * 1e-3) / 1e9
-    pm = pmc_lookup("*pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    if res.get("fused_ms"):
+        # the dominant kernel is the fused rollout step: the env step's bytes plus the agent's
+        # h in / h out and the action written -- its observations are never read back
+        roof_kernel, roof_ms = "asg::rollout_h2_kernel (env step t + agent/eps-greedy t+1)", res["fused_ms"]
+        per_launch = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
+        pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    else:
+        roof_kernel, roof_ms = "asg::step_kernel", kern_ms
+        per_launch = step_bytes(a.n, a.m, a.L) * E
+        pm = pmc_lookup("*pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    achieved = per_launch / (roof_ms * 1e-3) / 1e9
     traffic = pm.get("hbm_bytes_per_launch") if pm else None
 
     secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))
@@ -445,8 +471,13 @@ def main():
                        "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "asg::step_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": roof_kernel, "kernel_ms": round(roof_ms, 4),
                          "bytes_per_launch": per_launch},
+            "kernels_ms": {"fused_step_select": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
+                           "env_step": round(kern_ms, 4) if kern_ms else None,
+                           "select": round(sel_ms, 4) if sel_ms else None,
+                           "note": "fused: T-1 fused launches + 1 select + 1 step per episode"
+                                   if res.get("fused_ms") else "one select + one step per step"},
             "roofline_agent": ra,
             "cpu_baseline": cpu,
         }

@@ -43,6 +43,8 @@
  *                              FilteredEpsilonGreedyActionSelector / FilteredSoftPoliciesSelector
  *                              (action_selectors/filtered_classic_selectors.py:6-103)
  *   asg_real_haal_select       HAALSelector.select_action (action_selectors/non_rl_selectors.py:54-118)
+ *   asg_step_select            the runner's env.step(t) + mac.select_actions(t + 1) fused
+ *                              (episode_runner.py:76-95 / parallel_runner.py:113-200)
  */
 #ifndef ASG_H
 #define ASG_H
@@ -301,6 +303,23 @@ int asg_filtered_epsilon_greedy(const float *mat, const int64_t mat_strides[3], 
 int asg_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B, int n, int m, int M,
                           uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *out,
                           int32_t *status, void *hip_stream);
+
+/* Fused rollout step: asg_step at row ts (actions_t) and then asg_rnn_agent_select for row
+ * ts + 1 (the actions of step t + 1) in ONE kernel -- the runner's env.step(t) followed by
+ * mac.select_actions(t + 1) (episode_runner.py:80-95 then :76-79).  The observation rows of
+ * t + 1 are generated in the agent's operand layout, written to the batch and consumed
+ * without being read back; batch contents, returns, hidden state and actions are
+ * bit-identical to the two separate calls with the same arguments.  Requirements: Philox
+ * bump/dense benefits, integer actions, n % 32 == 0, m % 32 == 0, m <= 256, the GRU agent
+ * (hidden 64, K = m (L + 1), weights packed by asg_rnn_agent_pack for n_out = m), a
+ * contiguous time-major EpisodeBatch, and k + 1 < T (the episode's last step is a plain
+ * asg_step).  h_in [E n][64] (row stride h_stride, 0 = one broadcast row, NULL = zeros),
+ * h_out [E n][64]; selection: epsilon / seed / counter / status as asg_rnn_agent_select
+ * (global rows keyed by env_index_base).  hip_stream NULL = the handle's stream. */
+int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                    const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
+                    int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
+                    int32_t *status, void *hip_stream);
 
 /* ==== RealConstellationEnv ======================================
  * Batched form of src/envs/real_constellation_env.py with injected benefits

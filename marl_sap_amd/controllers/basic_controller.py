@@ -55,6 +55,24 @@ class BasicMAC:
                 and isinstance(self.selector_agent, RNNFusedAgent)
                 and not getattr(self.args, "unfused_selection", False))
 
+    def fused_step_ok(self, env, ep_batch):
+        """The runner may fuse env.step(t) with select_actions(t + 1) (asg_step_select):
+        the fused agent + epsilon-greedy selection on plain observation inputs, a time-major
+        batch and an env that takes it."""
+        from ..modules.agents.rnn_agent import RNNFusedAgent
+        return (self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select") and env.can_step_select()
+                and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
+                and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
+                and bool(self.args.use_rnn) and self.selector_agent.n_out == env.m
+                and bool(getattr(self.args, "fused_rollout", False)))
+
+    def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
+        """env.step at row t_ep and select_actions for row t_ep + 1 in one kernel; the
+        hidden state advances as select_actions would advance it."""
+        eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device)
+        self.hidden_states = env.step_select(ep_batch, t_ep, self.selector_agent, self.hidden_states, eps, seed,
+                                             counter, status)
+
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)
         net = self.selector_agent if action_selection_mode else self.agent

@@ -1045,6 +1045,13 @@ constexpr int kH2NT = ASG_H2_NT, kH2WavesPerSimd = ASG_H2_WAVES, kH2Waves = 4 * 
 #ifndef ASG_H2_LATE_H
 #define ASG_H2_LATE_H 1
 #endif
+// fc1 input scale: every tile starts from the launch's guess 2^11 (|x| < 16 needs no retry),
+// so a tile's result depends on its own rows only (the fused rollout kernel reproduces it
+// bit for bit); ASG_H2_CARRY_SX=1 carries the previous tile's scale instead
+#ifndef ASG_H2_CARRY_SX
+#define ASG_H2_CARRY_SX 0
+#endif
+constexpr int kH2SxInit = 11;
 // one-hot columns gathered at the tile start into the fc1 accumulators (0) or added at the
 // fc1 tail (1)
 #ifndef ASG_H2_GATHER_TAIL
@@ -1081,232 +1088,17 @@ __host__ __device__ static inline int64_t h2_w1_off(int nout, bool w2l) {
 typedef const u32x4v __attribute__((address_space(3))) * lds_u4p;
 typedef const f32x4 __attribute__((address_space(3))) * lds_f4v;
 
-// One wave, 32 agent rows (NT = 2 row tiles of 16): fc1 -> GRU -> fc2 (+ selection).
-// Wl: the LDS stage; W2L: W2 planes staged (else read through L2).  sx_obs: the wave's
-// running fc1 input scale.
-template <int NT, bool SEL, bool W2L>
-__device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, const u32x4v *Wl, int &sx_obs,
-                                              const int (&sw)[4]) {
+// The GRU, fc2 and selection of one 32-row wave tile on split-f16 MFMAs (shared by the
+// agent kernel and the fused rollout kernel): xB = relu(fc1) fragments, hB = h_in rows.
+// ALLAV: every task is available (the fused rollout wrote avail = 1 itself).
+template <int NT, bool SEL, bool W2L, bool ALLAV>
+__device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
+                                        const int64_t (&rows)[NT], const bool (&ok)[NT], const float4 (&hB)[4][NT],
+                                        const f32x4 (&xB)[4][NT]) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    if (row0 >= a.R) return;
-    ASG_STAMP(0);
-    int64_t rows[NT];
-    bool ok[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        rows[nt] = row0 + 16 * nt + r;
-        ok[nt] = rows[nt] < a.R;
-    }
+    (void)r;
     const lds_u4p Wih = (lds_u4p)Wl, Whh = (lds_u4p)(Wl + kH2GruF4);
     const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);  // biases
-    const u32x4v *W1g = a.pk + 1;
-    const float *xr[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) xr[nt] = a.X + (ok[nt] ? rows[nt] : 0) * a.xs;
-    const int nsl = a.K >> 5;
-
-    // observation slices of the main fc1 loop (k >= P): a ring of ASG_H2_XBUF slices in
-    // flight per wave, the first ones issued right behind the one-hot prefix loads
-    auto load_x = [&](int sl, float4 (&xv)[2][NT]) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                xv[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + 32 * sl + 16 * c + 4 * q);
-    };
-    auto load_pa = [&](int t4, float4 (&pa)[4][NT]) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                pa[c][nt] = (t4 + c < a.P / 16) ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-    const int s0 = a.P >> 5;
-    float4 xbuf[kH2XBuf][2][NT];
-    float4 pa[4][NT];
-    if (a.P > 0) load_pa(0, pa);
-#pragma unroll
-    for (int b = 0; b < kH2XBuf; ++b)
-        if (s0 + b < nsl) load_x(s0 + b, xbuf[b]);
-    // h_in fragments: needed from the GRU on, so issued behind the observations (or, with
-    // ASG_H2_LATE_H, after the fc1 main loop: 32 fewer VGPRs live through fc1)
-    float4 hB[4][NT];
-    auto load_h = [&]() {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs + 16 * t + 4 * q)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-#if !ASG_H2_LATE_H
-    load_h();
-#endif
-
-    // ---- one-hot prefix (see agent_rows): rows whose first P inputs are onehot(a) or zero
-    // add W1[:, a] (W1T, f32) instead of running those slices' MFMAs
-    int pos[NT];
-    bool onehot = false;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) pos[nt] = -1;
-    if (a.P > 0) {
-        bool bad = false;
-        for (int t4 = 0; t4 < a.P / 16; t4 += 4) {  // P % 64 == 0, or P / 16 < 4 guarded
-            if (t4 > 0) load_pa(t4, pa);
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float v = comp(pa[c][nt], e);
-                        const bool one = v == 1.0f;
-                        bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
-                        pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
-                    }
-        }
-        bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const uint64_t mk = __ballot(pos[nt] >= 0);
-            const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull, g3 = mk >> 48;
-            rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
-            int p = pos[nt];
-            p = max(p, __shfl_xor(p, 16));
-            p = max(p, __shfl_xor(p, 32));
-            pos[nt] = p;
-        }
-        onehot = rows_ok && __ballot(bad) == 0;
-    }
-    // ---- fc1 on split f16 MFMAs (accumulators from the one-hot column W1[:, a] scaled like
-    // the products; the bias is added unscaled at the end) -------------------------------
-    f32x4 acc[4][NT];
-    int sx = sx_obs;
-    float tmax = 0.f;
-#if ASG_H2_GATHER_TAIL
-    // the one-hot columns W1[:, a] are gathered now and added after the main loop: their
-    // L2 latency hides under the observation MFMAs instead of delaying the first one
-    float4 g1[4][NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-            g1[mt][nt] = (onehot && pos[nt] >= 0)
-                             ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-    for (int attempt = 0;; ++attempt) {
-        if (attempt > 0) {
-#pragma unroll
-            for (int b = 0; b < kH2XBuf; ++b)
-                if (s0 + b < nsl) load_x(s0 + b, xbuf[b]);
-        }
-        const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
-#if ASG_H2_GATHER_TAIL
-        (void)scS;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#else
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const float4 g = (onehot && pos[nt] >= 0)
-                                     ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
-            }
-#endif
-#ifdef ASG_STAMP_FC1
-        if (attempt == 0) {
-            // wait for the gathered W1 columns here so the stamp measures their latency
-            float z = 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) z += acc[mt][0][0];
-            if (z == 12345.f) acc[0][0][1] += 1.f;
-            ASG_STAMP(5);
-        }
-#endif
-        float m = 0.f;
-        auto slice = [&](int sl, const float4 (&xv)[2][NT], bool lds) {
-            u32x4v xp[NT][2];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                m = absmax4(absmax4(m, xv[0][nt]), xv[1][nt]);
-                const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
-                                     xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
-                split2s(x8, scx, xp[nt][0], xp[nt][1]);
-            }
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                u32x4v w[2];
-                if (lds) {
-                    const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
-#pragma unroll
-                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
-                } else {
-#pragma unroll
-                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
-                }
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
-            }
-        };
-        // slices below P / 32 (a tile whose prefix is not one-hot): W1 planes through L2
-        for (int sl = 0; sl < (onehot ? 0 : s0); ++sl) {
-            float4 xv[2][NT];
-            load_x(sl, xv);
-            slice(sl, xv, false);
-        }
-        const int s_l2 = s0 + a.w1_lds;  // first slice read through L2
-        for (int sl = s0; sl < nsl; sl += kH2XBuf) {
-#pragma unroll
-            for (int b = 0; b < kH2XBuf; ++b) {
-                if (sl + b < nsl) {
-                    if (sl + b < s_l2) slice(sl + b, xbuf[b], true);
-                    else slice(sl + b, xbuf[b], false);
-                    if (sl + b + kH2XBuf < nsl) load_x(sl + b + kH2XBuf, xbuf[b]);
-                }
-            }
-        }
-#if ASG_H2_LATE_H
-        if (attempt == 0) load_h();
-#endif
-        tmax = wave_max_f32(m);
-#ifdef ASG_STAMP_FC1
-        if (attempt == 0) ASG_STAMP(6);
-#endif
-        // the split needs |x| * 2^sx < 2^15 (|h| <= 65504): otherwise redo at a smaller scale
-        if (!(tmax * scx >= 32768.f) || attempt > 0) break;
-        sx = h2_scale(tmax, -90, 90 - sw[0]);
-    }
-    // next tile's guess: this tile's own scale (grows back when values shrink)
-    sx_obs = h2_scale(tmax, -90, 90 - sw[0]);
-    f32x4 xB[4][NT];
-    {
-        const float un = pow2f(-(sw[0] + sx));
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const f32x4 bb = Bs[4 * mt + q];  // b1[16 mt + 4 q ..]
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-#if ASG_H2_GATHER_TAIL
-                // unscaled products + the gathered one-hot column + bias
-                const f32x4 gv = f32x4{g1[mt][nt].x, g1[mt][nt].y, g1[mt][nt].z, g1[mt][nt].w};
-#pragma unroll
-                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + gv[v] + bb[v], 0.f);
-#else
-#pragma unroll
-                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
-#endif
-            }
-        }
-    }
-    ASG_STAMP(1);
-
     // availability words of fc2's first four output tiles: issued now, used after the GRU
     const SelectArgs &sel = a.sel;
     const int nct = a.nout >> 4;
@@ -1336,6 +1128,7 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
     }
     auto load_av = [&](int c, int nt) -> uint32_t {
         if (!SEL || !ok[nt]) return 0u;
+        if (ALLAV) return 0x01010101u;
         const uint8_t *ap = arow[nt] + 16 * c + 4 * q;
         return av4 ? *reinterpret_cast<const uint32_t *>(ap)
                    : ((uint32_t)ap[0] | ((uint32_t)ap[1] << 8) | ((uint32_t)ap[2] << 16) | ((uint32_t)ap[3] << 24));
@@ -1542,13 +1335,250 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
     ASG_STAMP(7);
 }
 
-// Persistent: one 512-thread workgroup per CU stages the LDS image (h2_w1_off), then its 8
-// waves walk 256-row tiles.
-template <bool SEL, bool W2L>
-__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
-rnn_agent_h2_kernel(H2Args a) {
-    constexpr int NT = kH2NT;
-    extern __shared__ u32x4v s_h2[];
+// One wave, 32 agent rows (NT = 2 row tiles of 16): fc1 -> GRU -> fc2 (+ selection).
+// Wl: the LDS stage; W2L: W2 planes staged (else read through L2).  sx_obs: the wave's
+// running fc1 input scale.
+template <int NT, bool SEL, bool W2L>
+__device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, const u32x4v *Wl, int &sx_obs,
+                                              const int (&sw)[4]) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    if (row0 >= a.R) return;
+    ASG_STAMP(0);
+    int64_t rows[NT];
+    bool ok[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        rows[nt] = row0 + 16 * nt + r;
+        ok[nt] = rows[nt] < a.R;
+    }
+    const lds_u4p Wih = (lds_u4p)Wl, Whh = (lds_u4p)(Wl + kH2GruF4);
+    const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);  // biases
+    const u32x4v *W1g = a.pk + 1;
+    const float *xr[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) xr[nt] = a.X + (ok[nt] ? rows[nt] : 0) * a.xs;
+    const int nsl = a.K >> 5;
+
+    // observation slices of the main fc1 loop (k >= P): a ring of ASG_H2_XBUF slices in
+    // flight per wave, the first ones issued right behind the one-hot prefix loads
+    auto load_x = [&](int sl, float4 (&xv)[2][NT]) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                xv[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + 32 * sl + 16 * c + 4 * q);
+    };
+    auto load_pa = [&](int t4, float4 (&pa)[4][NT]) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                pa[c][nt] = (t4 + c < a.P / 16) ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    const int s0 = a.P >> 5;
+    float4 xbuf[kH2XBuf][2][NT];
+    float4 pa[4][NT];
+    if (a.P > 0) load_pa(0, pa);
+    // main-loop slice order: with the mock env's obs layout [onehot | B(k+1) | .. | B(k+L)]
+    // (K = P (L + 1)), task chunk u outer and lookahead block l inner -- the order in which
+    // the fused rollout kernel generates them (one set of bump parameters per chunk)
+    const int nmain = nsl - s0;
+    const bool perm = s0 > 0 && nmain % s0 == 0;
+    const int nblk = perm ? nmain / s0 : 1;
+    auto sl_of = [&](int idx) { return perm ? (idx % nblk + 1) * s0 + idx / nblk : s0 + idx; };
+#pragma unroll
+    for (int b = 0; b < kH2XBuf; ++b)
+        if (b < nmain) load_x(sl_of(b), xbuf[b]);
+    // h_in fragments: needed from the GRU on, so issued behind the observations (or, with
+    // ASG_H2_LATE_H, after the fc1 main loop: 32 fewer VGPRs live through fc1)
+    float4 hB[4][NT];
+    auto load_h = [&]() {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs + 16 * t + 4 * q)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+#if !ASG_H2_LATE_H
+    load_h();
+#endif
+
+    // ---- one-hot prefix (see agent_rows): rows whose first P inputs are onehot(a) or zero
+    // add W1[:, a] (W1T, f32) instead of running those slices' MFMAs
+    int pos[NT];
+    bool onehot = false;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) pos[nt] = -1;
+    if (a.P > 0) {
+        bool bad = false;
+        for (int t4 = 0; t4 < a.P / 16; t4 += 4) {  // P % 64 == 0, or P / 16 < 4 guarded
+            if (t4 > 0) load_pa(t4, pa);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float v = comp(pa[c][nt], e);
+                        const bool one = v == 1.0f;
+                        bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
+                        pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
+                    }
+        }
+        bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const uint64_t mk = __ballot(pos[nt] >= 0);
+            const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull, g3 = mk >> 48;
+            rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
+            int p = pos[nt];
+            p = max(p, __shfl_xor(p, 16));
+            p = max(p, __shfl_xor(p, 32));
+            pos[nt] = p;
+        }
+        onehot = rows_ok && __ballot(bad) == 0;
+    }
+    // ---- fc1 on split f16 MFMAs (accumulators from the one-hot column W1[:, a] scaled like
+    // the products; the bias is added unscaled at the end) -------------------------------
+    f32x4 acc[4][NT];
+    int sx = sx_obs;
+    float tmax = 0.f;
+#if ASG_H2_GATHER_TAIL
+    // the one-hot columns W1[:, a] are gathered now and added after the main loop: their
+    // L2 latency hides under the observation MFMAs instead of delaying the first one
+    float4 g1[4][NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+            g1[mt][nt] = (onehot && pos[nt] >= 0)
+                             ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 0) {
+#pragma unroll
+            for (int b = 0; b < kH2XBuf; ++b)
+                if (b < nmain) load_x(sl_of(b), xbuf[b]);
+        }
+        const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
+#if ASG_H2_GATHER_TAIL
+        (void)scS;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float4 g = (onehot && pos[nt] >= 0)
+                                     ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
+            }
+#endif
+#ifdef ASG_STAMP_FC1
+        if (attempt == 0) {
+            // wait for the gathered W1 columns here so the stamp measures their latency
+            float z = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) z += acc[mt][0][0];
+            if (z == 12345.f) acc[0][0][1] += 1.f;
+            ASG_STAMP(5);
+        }
+#endif
+        float m = 0.f;
+        auto slice = [&](int sl, const float4 (&xv)[2][NT], bool lds) {
+            u32x4v xp[NT][2];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                m = absmax4(absmax4(m, xv[0][nt]), xv[1][nt]);
+                const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
+                                     xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
+                split2s(x8, scx, xp[nt][0], xp[nt][1]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                u32x4v w[2];
+                if (lds) {
+                    const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
+#pragma unroll
+                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
+                } else {
+#pragma unroll
+                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
+            }
+        };
+        // slices below P / 32 (a tile whose prefix is not one-hot): W1 planes through L2
+        for (int sl = 0; sl < (onehot ? 0 : s0); ++sl) {
+            float4 xv[2][NT];
+            load_x(sl, xv);
+            slice(sl, xv, false);
+        }
+        const int s_l2 = s0 + a.w1_lds;  // first slice read through L2
+        for (int i0 = 0; i0 < nmain; i0 += kH2XBuf) {
+#pragma unroll
+            for (int b = 0; b < kH2XBuf; ++b) {
+                if (i0 + b < nmain) {
+                    const int sl = sl_of(i0 + b);
+                    if (sl < s_l2) slice(sl, xbuf[b], true);
+                    else slice(sl, xbuf[b], false);
+                    if (i0 + b + kH2XBuf < nmain) load_x(sl_of(i0 + b + kH2XBuf), xbuf[b]);
+                }
+            }
+        }
+#if ASG_H2_LATE_H
+        if (attempt == 0) load_h();
+#endif
+        tmax = wave_max_f32(m);
+#ifdef ASG_STAMP_FC1
+        if (attempt == 0) ASG_STAMP(6);
+#endif
+        // the split needs |x| * 2^sx < 2^15 (|h| <= 65504): otherwise redo at a smaller scale
+        if (!(tmax * scx >= 32768.f) || attempt > 0) break;
+        sx = h2_scale(tmax, -90, 90 - sw[0]);
+    }
+#if ASG_H2_CARRY_SX
+    // next tile's guess: this tile's own scale (grows back when values shrink)
+    sx_obs = h2_scale(tmax, -90, 90 - sw[0]);
+#endif
+    f32x4 xB[4][NT];
+    {
+        const float un = pow2f(-(sw[0] + sx));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const f32x4 bb = Bs[4 * mt + q];  // b1[16 mt + 4 q ..]
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+#if ASG_H2_GATHER_TAIL
+                // unscaled products + the gathered one-hot column + bias
+                const f32x4 gv = f32x4{g1[mt][nt].x, g1[mt][nt].y, g1[mt][nt].z, g1[mt][nt].w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + gv[v] + bb[v], 0.f);
+#else
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
+#endif
+            }
+        }
+    }
+    ASG_STAMP(1);
+
+    h2_tail<NT, SEL, W2L, false>(a, Wl, sw, row0, rows, ok, hB, xB);
+}
+
+// LDS image of the persistent h2 kernels (h2_w1_off): GRU planes, biases (b1 | b_ir+b_hr |
+// b_iz+b_hz | b_in | b_hn | b2), W2 planes (W2L), the first w1_lds W1 slices from P / 32 on;
+// sw = the four matrices' scale exponents (packed header)
+template <bool W2L>
+__device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s_h2, int (&sw)[4]) {
     const u32x4v *gru = a.pk + 1 + h2_w1_f4(a.K);  // W_ih, W_hh, W2 are contiguous after W1
     for (int64_t i = threadIdx.x; i < 2 * kH2GruF4; i += blockDim.x) s_h2[i] = gru[i];
     float *bs = reinterpret_cast<float *>(s_h2 + 2 * kH2GruF4);
@@ -1573,9 +1603,23 @@ rnn_agent_h2_kernel(H2Args a) {
         for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) s_h2[off + i] = w1[i];
     }
     const int4 hdr = *reinterpret_cast<const int4 *>(a.pk);
-    const int sw[4] = {hdr.x, hdr.y, hdr.z, hdr.w};
+    sw[0] = hdr.x;
+    sw[1] = hdr.y;
+    sw[2] = hdr.z;
+    sw[3] = hdr.w;
+}
+
+// Persistent: one 512-thread workgroup per CU stages the LDS image (h2_w1_off), then its 8
+// waves walk 256-row tiles.
+template <bool SEL, bool W2L>
+__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
+rnn_agent_h2_kernel(H2Args a) {
+    constexpr int NT = kH2NT;
+    extern __shared__ u32x4v s_h2[];
+    int sw[4];
+    h2_stage<W2L>(a, s_h2, sw);
     __syncthreads();
-    int sx_obs = 11;
+    int sx_obs = kH2SxInit;
     const int64_t ntiles = (a.R + kH2Waves * (16 * NT) - 1) / (kH2Waves * (16 * NT));
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kH2Waves + (threadIdx.x >> 6)) * (16 * NT);
@@ -1927,6 +1971,374 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
     const SelectArgs sa{avail, a0, a1, n, epsilon, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x5bd1e995u, counter,
                         row_base, out, o0, o1, err};
     return launch_rnn_agent_fwd(X, xs, R, K, Hin, hs, packed, b1, bih, bhh, b2, nout, use_rnn, Hout, Q, &sa, s);
+}
+
+// =====================================================================================
+// Fused rollout step (mock env, Philox bumps): the env transition at step k of every env
+// (actions at batch row ts: MockConstellationEnv.step, mock :116-162, with the runner's
+// batch updates -- what step_kernel does), then the RNNAgent forward + epsilon-greedy for
+// row ts + 1 on the observations that transition produces.  Those observation rows are
+// generated in the split-f16 MFMA operand layout (lane (r, q) holds tasks 16 c + 4 q + v of
+// each 32-task chunk), written to the batch, and consumed from registers: the agent never
+// reads them back from HBM (1 KB per agent row at 64 x 64).  One wave per env: agents are
+// lanes for the transition, then the env's n / 32 agent tiles run the h2 path.  Results
+// are bit-identical to step_kernel + rnn_agent_h2_kernel (same bump arithmetic, per-tile fc1
+// scale, slice order and tail).
+// =====================================================================================
+// timing experiments only: skip the observation / one-hot / avail / beta stores (wrong batch)
+#ifndef ASG_ROLLOUT_NOSTORE
+#define ASG_ROLLOUT_NOSTORE 0
+#endif
+struct RolloutArgs {
+    // the time-major batch rows the step touches, each a contiguous [E][..] slab
+    float *obs1;        // obs row ts + 1        [E][n][K]
+    float *beta1;       // beta row ts + 1       [E][n][m]   (may be NULL)
+    uint8_t *avail1;    // avail row ts + 1      [E][n][m]   (may be NULL)
+    int64_t *onehot0;   // actions_onehot row ts [E][n][m]   (may be NULL)
+    const int64_t *act0;  // actions row ts      [E][n]
+    float *rew0;        // rewards row ts        [E][n]      (may be NULL)
+    int64_t *prev1;     // prev_assigns row ts+1 [E][n]      (may be NULL)
+    uint8_t *term0;     // terminated row ts     [E]         (may be NULL)
+    int64_t *filled1;   // filled row ts + 1     [E]         (may be NULL)
+    // env state
+    int *prev;
+    double *returns;
+    const double *T_trans;
+    int *env_err;
+    double lambda_;
+    uint64_t seed;
+    int64_t env_base, E;
+    uint32_t episode, quirks;
+    int n, m, T, L, k, dense;
+    float wmin, wmax;
+    // agent
+    const u32x4v *pk;
+    const float *W1T, *Hin;
+    int64_t hs;
+    float *Hout;
+    int w1_lds;
+    float epsilon;
+    uint32_t k0, k1, counter;
+    int64_t row_base;
+    int64_t *act1;      // actions row ts + 1 [E][n] (the selection's output)
+    int *sel_err;
+    const float *b1, *bih, *bhh, *b2;
+    int64_t scratch_off;  // per-wave transition scratch in LDS (u32x4v units)
+};
+
+__host__ __device__ static inline int64_t rollout_scratch_bytes(int n, int m) {
+    return ((int64_t)4 * m + 4 * m + 4 * n + 8 * n + 15) / 16 * 16 + 16;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// the h2 tail's view of the agent arguments
+__device__ __forceinline__ H2Args rollout_h2args(const RolloutArgs &ra) {
+    H2Args a;
+    a.X = nullptr;
+    a.xs = 0;
+    a.R = ra.E * ra.n;
+    a.K = ra.m * (ra.L + 1);
+    a.P = ra.m;
+    a.Hin = ra.Hin;
+    a.hs = ra.hs;
+    a.pk = ra.pk;
+    a.W1T = ra.W1T;
+    a.b1 = ra.b1;
+    a.bih = ra.bih;
+    a.bhh = ra.bhh;
+    a.b2 = ra.b2;
+    a.nout = ra.m;
+    a.Hout = ra.Hout;
+    a.Q = nullptr;
+    a.sel = SelectArgs{nullptr, 0, 0, ra.n, ra.epsilon, ra.k0, ra.k1, ra.counter, ra.row_base, ra.act1,
+                       (int64_t)ra.n, 1, ra.sel_err};
+    a.w1_lds = ra.w1_lds;
+    return a;
+}
+
+template <bool W2L>
+__device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, int sub, const EnvKey &key,
+                                             const float *s_scale, const int *s_act, const u32x4v *Wl,
+                                             const int (&sw)[4]) {
+    constexpr int NT = kH2NT;
+    const H2Args a = rollout_h2args(ra);
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    const int n = ra.n, m = ra.m, T = ra.T, L = ra.L, k = ra.k;
+    const int K = m * (L + 1);
+    const int U = m >> 5;
+    const int64_t row0 = e * n + 32 * sub;
+    int64_t rows[NT];
+    bool ok[NT];
+    int ia[NT], act[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        ia[nt] = 32 * sub + 16 * nt + r;
+        rows[nt] = e * n + ia[nt];
+        ok[nt] = true;
+        act[nt] = s_act[ia[nt]];
+    }
+    // obs block 0 = onehot(a) (row ts + 1), actions_onehot (row ts), avail = 1 (row ts + 1)
+    for (int u = 0; u < (ASG_ROLLOUT_NOSTORE ? 0 : U); ++u)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int j0 = 32 * u + 16 * c + 4 * q;
+                const int aa = act[nt];
+                *reinterpret_cast<float4 *>(ra.obs1 + rows[nt] * K + j0) =
+                    make_float4(aa == j0, aa == j0 + 1, aa == j0 + 2, aa == j0 + 3);
+                if (ra.onehot0) {
+                    longlong2 *hp = reinterpret_cast<longlong2 *>(ra.onehot0 + rows[nt] * m + j0);
+                    hp[0] = make_longlong2(aa == j0, aa == j0 + 1);
+                    hp[1] = make_longlong2(aa == j0 + 2, aa == j0 + 3);
+                }
+                if (ra.avail1) *reinterpret_cast<uint32_t *>(ra.avail1 + rows[nt] * m + j0) = 0x01010101u;
+            }
+    // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
+    const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);
+    const u32x4v *W1g = a.pk + 1;
+    const int s0 = U, s_l2 = s0 + a.w1_lds;
+    f32x4 acc[4][NT];
+    int sx = kH2SxInit;
+    for (int attempt = 0;; ++attempt) {
+        const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
+                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
+            }
+        float mx = 0.f;
+        for (int u = 0; u < U; ++u) {
+            // bump parameters of the lane's 16 (row, task) pairs of this chunk
+            Bump32 bp[2][4][NT];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int j = 32 * u + 16 * c + 4 * q + v;
+                        bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + j, s_scale[j], T, ra.wmin, ra.wmax,
+                                                     ra.dense != 0);
+                    }
+                }
+            for (int l = 1; l <= L; ++l) {
+                const int t = k + l;
+                float4 xv[2][NT];
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        float vv[4];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) vv[v] = (t < T) ? bump32_at(bp[c][v][nt], t) : 0.0f;
+                        xv[c][nt] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                        if (attempt == 0 && !ASG_ROLLOUT_NOSTORE) {
+                            const int j0 = 32 * u + 16 * c + 4 * q;
+                            *reinterpret_cast<float4 *>(ra.obs1 + rows[nt] * K + m * l + j0) = xv[c][nt];
+                            if (l == 1 && ra.beta1) *reinterpret_cast<float4 *>(ra.beta1 + rows[nt] * m + j0) = xv[c][nt];
+                        }
+                    }
+                // the h2 kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
+                const int sl = l * U + u;
+                u32x4v xp[NT][2];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    mx = absmax4(absmax4(mx, xv[0][nt]), xv[1][nt]);
+                    const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
+                                         xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
+                    split2s(x8, scx, xp[nt][0], xp[nt][1]);
+                }
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    u32x4v w[2];
+                    if (sl < s_l2) {
+                        const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
+#pragma unroll
+                        for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
+                    } else {
+#pragma unroll
+                        for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
+                    }
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
+                }
+            }
+        }
+        const float tmax = wave_max_f32(mx);
+        if (!(tmax * scx >= 32768.f) || attempt > 0) break;
+        sx = h2_scale(tmax, -90, 90 - sw[0]);
+    }
+    // h_t rows (the only agent-side loads of the tile), issued after fc1 like the h2 kernel
+    float4 hB[4][NT];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    f32x4 xB[4][NT];
+    {
+        const float un = pow2f(-(sw[0] + sx));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const f32x4 bb = Bs[4 * mt + q];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
+        }
+    }
+    h2_tail<NT, true, W2L, true>(a, Wl, sw, row0, rows, ok, hB, xB);
+}
+
+template <bool W2L>
+__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
+rollout_h2_kernel(RolloutArgs ra) {
+    extern __shared__ u32x4v s_h2[];
+    int sw[4];
+    h2_stage<W2L>(rollout_h2args(ra), s_h2, sw);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = ra.n, m = ra.m, T = ra.T, k = ra.k;
+    char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
+    float *s_scale = reinterpret_cast<float *>(scr);
+    int *s_cnt = reinterpret_cast<int *>(s_scale + m);
+    int *s_act = s_cnt + m;
+    double *s_rew = reinterpret_cast<double *>(scr + (((int64_t)8 * m + 4 * n + 7) & ~(int64_t)7));
+    const int64_t GW = (int64_t)gridDim.x * kH2Waves;
+    for (int64_t e = (int64_t)blockIdx.x * kH2Waves + wv; e < ra.E; e += GW) {
+        const EnvKey key = env_key(ra.seed, ra.env_base + e);
+        // ---- transition (lane = agent): counts, rewards, returns (step_kernel's arithmetic)
+        for (int j = lane; j < m; j += 64) {
+            s_scale[j] = philox_task_scale(key, ra.episode, j);
+            s_cnt[j] = 0;
+        }
+        wave_lds_fence();
+        int err = 0;
+        for (int i = lane; i < n; i += 64) {
+            const int64_t a64 = ra.act0[e * n + i];
+            int ai = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
+            if (ai < 0) err = ASG_E_ACTION_RANGE;
+            ai = ai < 0 ? 0 : ai;
+            s_act[i] = ai;
+            atomicAdd(&s_cnt[ai], 1);
+        }
+        wave_lds_fence();
+        for (int i = lane; i < n; i += 64) {
+            const int j = s_act[i];
+            const int p = ra.prev[e * n + i];
+            const Bump32 b = philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
+            const double beta = bump64_at(b, k);
+            const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+            const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+            const double bh = beta - ra.lambda_ * pen;
+            const double rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+            s_rew[i] = rr;
+            if (ra.rew0) ra.rew0[e * n + i] = (float)rr;
+            ra.prev[e * n + i] = j;
+            if (ra.prev1) ra.prev1[e * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+        }
+        wave_lds_fence();
+        err = wave_or_i32(err);
+        if (lane == 0) {
+            double sum = 0.0;
+            for (int i = 0; i < n; ++i) sum += s_rew[i];  // Python's sum(rewards), left to right
+            ra.returns[e] += sum;
+            bool term = k + 1 >= T;
+            if (ra.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
+            if (ra.term0) ra.term0[e] = term;
+            if (ra.filled1) ra.filled1[e] = 1;
+            if (err) atomicCAS(ra.env_err, 0, err);
+        }
+        // ---- agent + selection for row ts + 1, tile by tile
+        for (int sub = 0; sub < n / 32; ++sub) rollout_rows<W2L>(ra, e, sub, key, s_scale, s_act, s_h2, sw);
+        wave_lds_fence();  // the next env reuses the scratch
+    }
+}
+
+// shapes the fused rollout takes (the h2 agent shape with the mock env's obs layout)
+bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn) {
+    return h2_shape(K, nout, use_rnn) && use_h2_kernel() && onehot_prefix_enabled() && nout == st.m &&
+           st.m % 32 == 0 && st.n % 32 == 0 && K == st.m * (st.L + 1) && st.L >= 1;
+}
+
+hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
+                                      const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                      const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,
+                                      uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s) {
+    (void)ts;
+    const int K = st.m * (st.L + 1), nout = st.m;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    ncu = stream_cus(s, ncu);
+    RolloutArgs ra{};
+    ra.obs1 = sl.obs1;
+    ra.beta1 = sl.beta1;
+    ra.avail1 = sl.avail1;
+    ra.onehot0 = sl.onehot0;
+    ra.act0 = sl.act0;
+    ra.rew0 = sl.rew0;
+    ra.prev1 = sl.prev1;
+    ra.term0 = sl.term0;
+    ra.filled1 = sl.filled1;
+    ra.act1 = sl.act1;
+    ra.prev = st.prev;
+    ra.returns = st.returns;
+    ra.T_trans = st.T_trans;
+    ra.env_err = st.err;
+    ra.lambda_ = st.lambda_;
+    ra.seed = st.seed;
+    ra.env_base = st.env_base;
+    ra.E = st.E;
+    ra.episode = st.episode;
+    ra.quirks = st.quirks;
+    ra.n = st.n;
+    ra.m = st.m;
+    ra.T = st.T;
+    ra.L = st.L;
+    ra.k = k;
+    ra.dense = st.benefit_mode == ASG_BENEFIT_DENSE;
+    ra.wmin = (float)st.wmin;
+    ra.wmax = (float)st.wmax;
+    ra.pk = reinterpret_cast<const u32x4v *>(packed + rnn_agent_packed_f4(K, nout, 1) - rnn_agent_h2_f4(K, nout, 1));
+    const int64_t w2_f4 = 4 * (int64_t)((nout + 15) / 16) * 64;
+    const float4 *W2p = packed + (int64_t)((K + 15) / 16) * 4 * 64 + 2 * kGruF4;  // as launch_rnn_agent_fwd
+    ra.W1T = reinterpret_cast<const float *>(W2p + w2_f4);
+    ra.Hin = Hin;
+    ra.hs = hs;
+    ra.Hout = Hout;
+    ra.epsilon = epsilon;
+    ra.k0 = (uint32_t)seed;
+    ra.k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
+    ra.counter = counter;
+    ra.row_base = row_base;
+    ra.sel_err = err;
+    ra.b1 = b1;
+    ra.bih = bih;
+    ra.bhh = bhh;
+    ra.b2 = b2;
+    constexpr int64_t kCap = 160 * 1024 / 16;
+    const int64_t scr_f4 = (rollout_scratch_bytes(st.n, st.m) * kH2Waves + 15) / 16;
+    const bool w2l = h2_w2_off(nout) + h2_w2_f4(nout) + scr_f4 <= kCap;
+    const int64_t w1off = h2_w1_off(nout, w2l);
+    const int64_t slices = K / 32 - nout / 32, fit = (kCap - scr_f4 - w1off) / (4 * 2 * 64);
+    ra.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
+    ra.scratch_off = w1off + (int64_t)ra.w1_lds * 4 * 2 * 64;
+    const size_t lds_b = (size_t)(ra.scratch_off + scr_f4) * 16;
+    const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
+    const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
+    if (w2l)
+        hipLaunchKernelGGL((rollout_h2_kernel<true>), dim3(grid), dim3(64 * kH2Waves), lds_b, s, ra);
+    else
+        hipLaunchKernelGGL((rollout_h2_kernel<false>), dim3(grid), dim3(64 * kH2Waves), lds_b, s, ra);
+    return hipGetLastError();
 }
 
 }  // namespace asg

@@ -90,6 +90,25 @@ hipError_t launch_filtered_soft_map(const int64_t *picked, const int64_t *topm, 
                                     hipStream_t s);
 
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
+
+// fused rollout step (asg_agent.hip): the contiguous [E][..] slabs of the time-major batch
+// rows it touches
+struct RolloutSlabs {
+    float *obs1, *beta1;
+    uint8_t *avail1;
+    int64_t *onehot0;
+    const int64_t *act0;
+    float *rew0;
+    int64_t *prev1;
+    uint8_t *term0;
+    int64_t *filled1;
+    int64_t *act1;
+};
+bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn);
+hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
+                                      const float4 *packed, const float *b1, const float *bih, const float *bhh,
+                                      const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,
+                                      uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
                                  int use_rnn, float4 *packed, hipStream_t s);
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,

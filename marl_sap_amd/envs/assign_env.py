@@ -146,6 +146,26 @@ class AssignEnvBatch(MultiAgentEnv):
         self.k += 1
         return self.k >= self.T
 
+    def can_step_select(self):
+        """Whether asg_step_select (the fused env step + next selection) takes this env:
+        Philox bump/dense benefits, integer actions, n and m multiples of 32, m <= 256."""
+        return (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
+                and self.n % 32 == 0 and self.m % 32 == 0 and self.m <= 256 and self.L >= 1)
+
+    def step_select(self, batch, ts, agent, hidden_state, epsilon, seed, counter, status):
+        """asg_step at row ts and the fused agent forward + epsilon-greedy for row ts + 1 in
+        one kernel (asg_step_select): the observations of ts + 1 are written to the batch and
+        consumed on the chip.  `agent` is the RNNFusedAgent; returns the new hidden state
+        [E n, hidden].  Same batch, returns, actions and hidden state as env.step(batch, ts)
+        followed by mac.select_actions(batch, ts + 1)."""
+        args = agent.step_select_args(hidden_state, batch["obs"].shape[-1], self.device, self.num_envs * self.n)
+        h_out = args[-1]
+        self._call("asg_step_select", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
+                   ctypes.c_void_p(h_out.data_ptr()), float(epsilon), seed & 0xFFFFFFFFFFFFFFFF, int(counter),
+                   ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(self.device))
+        self.k += 1
+        return h_out
+
     def random_actions(self, batch, ts):
         self._call("asg_random_actions", ctypes.byref(batch_view(batch)), int(ts))
 

@@ -99,6 +99,26 @@ class RNNFusedAgent(RNNAgent):
                 _lib.stream_ptr(x.device)))
         return h_out
 
+    def step_select_args(self, hidden_state, K, device, R):
+        """The agent half of asg_step_select's arguments: packed weights, biases, K, hidden,
+        h_in (+ row stride), and a fresh h_out tensor (last)."""
+        H = self.args.hidden_dim
+        h = hidden_state
+        if h.dim() == 3 and h.stride(0) == 0 and h.stride(1) == 0 and h.stride(2) == 1:
+            hs = 0  # init_hidden's expanded zero row
+        else:
+            h = h.reshape(-1, H)
+            if h.stride(-1) != 1 or h.stride(0) % 4 != 0 or h.data_ptr() % 16 != 0:
+                h = h.contiguous()
+            hs = h.stride(0)
+        if hs and h.shape[0] != R:
+            raise ValueError(f"hidden state has {h.shape[0]} rows, the batch {R}")
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._h_keep = h  # alive until the kernel has read it (stream order)
+        h_out = torch.empty((R, H), dtype=torch.float32, device=device)
+        return [p(self._packed(K, device)), p(self.fc1.bias), p(self.rnn.bias_ih), p(self.rnn.bias_hh),
+                p(self.fc2.bias), int(K), int(H), p(h), int(hs), h_out]
+
     def _packed(self, K, device):
         """Weights in the kernel's fragment order, re-packed only when a weight changed
         (optimizer steps bump the tensors' version counters; load_state_dict too)."""

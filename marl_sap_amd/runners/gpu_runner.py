@@ -97,9 +97,17 @@ class GpuVecRunner:
         """One episode of every env, fully asynchronous (no host sync)."""
         self.reset()
         self.mac.init_hidden(batch_size=self.batch_size)
+        # env.step(t) + select_actions(t + 1) as one kernel when the MAC and env allow it
+        # (asg_step_select: bit-identical batches, the t + 1 observations never re-read)
+        fused = hasattr(self.mac, "fused_step_ok") and self.mac.fused_step_ok(self.env, self.batch)
+        self.select_into_batch(0, test_mode)
         for t in range(self.T):
-            self.select_into_batch(t, test_mode)
+            if fused and t + 1 < self.T:
+                self.mac.fused_step_select(self.env, self.batch, t, self.t_env, test_mode)
+                continue
             self.env.step(self.batch, ts=t)
+            if t + 1 < self.T:
+                self.select_into_batch(t + 1, test_mode)
         self.t = self.T
         if self.protocol == "parallel":
             actions = self.mac.select_actions(self.batch, t_ep=self.T, t_env=self.t_env, test_mode=test_mode)

@@ -1,0 +1,104 @@
+"""Fused rollout step (asg_step_select: the env transition of step t and the RNNAgent forward
++ epsilon-greedy for step t + 1 in one kernel, the t + 1 observations generated in the
+agent's operand layout and never re-read).  It must be a pure scheduling change: every
+EpisodeBatch field, the returns, the hidden state and t_env bit-identical to the separate
+asg_step + asg_rnn_agent_select calls (reference loop: episode_runner.py:76-95)."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from marl_sap_amd.controllers import REGISTRY as MAC  # noqa: E402
+from marl_sap_amd.runners import REGISTRY as RUN  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+class _Logger:
+    def log_stat(self, *a, **k):
+        pass
+
+
+def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protocol="episode", seed=7):
+    args = SimpleNamespace(
+        batch_size_run=E, env="mock_constellation_env",
+        env_args=dict(n=n, m=m, T=T, L=L, lambda_=0.5, bids_as_actions=False, seed=seed, benefits=benefits),
+        env_rng="philox", env_quirks=tuple(quirks), runner_protocol=protocol, test_nepisode=1,
+        runner_log_interval=10 ** 12, n=n, m=m, T=T, hidden_dim=64, use_rnn=True, obs_last_action=False,
+        obs_agent_id=False, agent_output_type="q", action_selector="epsilon_greedy", agent="rnn_fused",
+        mac="basic_mac", seed=3, epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
+        evaluation_epsilon=0.0, fused_rollout=fused)
+    runner = RUN["gpu"](args, _Logger())
+    env = runner.get_env()
+    torch.manual_seed(1234)
+    mac = MAC["basic_mac"](env.scheme, {"agents": n}, args)
+    mac.to(DEV)
+    runner.setup(env.scheme, {"agents": n}, env.preprocess, mac)
+    with torch.no_grad():
+        assert mac.fused_step_ok(env, runner.new_batch()) == fused
+    out = []
+    for _ in range(episodes):
+        batch = runner.run(test_mode=False)
+        out.append(({k: v.cpu().clone() for k, v in batch.data.transition_data.items()},
+                    runner.last_returns.cpu().clone(), mac.hidden_states.detach().cpu().clone()))
+    res = out, runner.t_env, list(runner.train_returns)
+    env.close()
+    return res
+
+
+@pytest.mark.parametrize("n,m,T,L,E,eps,benefits", [
+    (64, 64, 6, 3, 24, 0.05, "bump"),   # the bench shape (episode length cut short)
+    (32, 96, 5, 2, 10, 0.3, "dense"),   # three 32-task chunks per block, heavy exploration
+    (96, 128, 4, 1, 7, 0.0, "bump"),    # three agent tiles per env, n > 64 lanes, greedy
+    (32, 256, 4, 3, 5, 0.1, "bump"),    # configs[4]-like task count (W1 slices through L2)
+])
+def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits):
+    a, ta, ra = _rollout(n, m, T, L, E, eps, benefits, fused=True)
+    b, tb, rb = _rollout(n, m, T, L, E, eps, benefits, fused=False)
+    assert ta == tb and ra == rb
+    for (fa, reta, ha), (fb, retb, hb) in zip(a, b):
+        assert fa.keys() == fb.keys()
+        for k in fa:
+            assert torch.equal(fa[k], fb[k]), k
+        assert torch.equal(reta, retb)
+        assert torch.equal(ha, hb)
+
+
+def test_fused_rollout_quirks_and_parallel_protocol():
+    kw = dict(n=32, m=32, T=5, L=3, E=6, eps=0.2, benefits="bump", quirks=("prev_assigns_zero", "parallel_terminated"),
+              protocol="parallel")
+    a, ta, ra = _rollout(fused=True, **kw)
+    b, tb, rb = _rollout(fused=False, **kw)
+    assert ta == tb and ra == rb
+    for (fa, reta, ha), (fb, retb, hb) in zip(a, b):
+        for k in fa:
+            assert torch.equal(fa[k], fb[k]), k
+        assert torch.equal(reta, retb)
+
+
+def test_fused_rollout_out_of_range_action_is_reported():
+    """An invalid action read by the fused kernel raises like asg_step (sticky device error)."""
+    from marl_sap_amd.envs import AssignEnvBatch
+    from marl_sap_amd.components import EpisodeBatch
+    from marl_sap_amd.modules.agents import RNNFusedAgent
+    n = m = 32
+    env = AssignEnvBatch(n, m, 4, 3, 0.5, seed=1, num_envs=3, device=DEV)
+    batch = EpisodeBatch(env.scheme, {"agents": n}, 3, 5, preprocess=env.preprocess, device=DEV, time_major=True)
+    args = SimpleNamespace(hidden_dim=64, use_rnn=True, m=m)
+    agent = RNNFusedAgent(m * 4, args).to(DEV)
+    env.reset(batch, 0)
+    batch["actions"][:, 0] = 0
+    batch["actions"][1, 0, 5, 0] = m  # out of range
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    h0 = torch.zeros((3 * n, 64), device=DEV)
+    with torch.no_grad():
+        env.step_select(batch, 0, agent, h0, 0.0, 1, 1, status)
+    with pytest.raises(ValueError):
+        env.sync()
+    env.close()
+    assert np.all(np.isfinite(batch["obs"][:, 1].cpu().numpy()))
