@@ -185,8 +185,9 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--fused-rollout", type=int, default=0,
-                   help="1: env step t + agent/eps-greedy t+1 in one kernel (asg_step_select)")
+    p.add_argument("--fused-rollout", type=int, default=1,
+                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select); "
+                        "0: separate asg_step + agent select launches")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):

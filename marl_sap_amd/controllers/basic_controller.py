@@ -64,7 +64,7 @@ class BasicMAC:
                 and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
                 and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
                 and bool(self.args.use_rnn) and self.selector_agent.n_out == env.m
-                and bool(getattr(self.args, "fused_rollout", False)))
+                and bool(getattr(self.args, "fused_rollout", True)))
 
     def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
         """env.step at row t_ep and select_actions for row t_ep + 1 in one kernel; the

@@ -1280,6 +1280,10 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
         amask[nt][0] = amask[nt][1] = 0;
     }
     const float un3 = pow2f(-S3);
+    int lane2 = lane;
+    // the fused rollout recomputes the lane's W2 address here each tile (hoisted, it was
+    // spilled, and its reload waited for every store of the tile)
+    if (ALLAV) asm volatile("" : "+v"(lane2));
     const lds_u4p W2s = (lds_u4p)(Wl + h2_w2_off(a.nout));
     const u32x4v *W2g = a.pk + 1 + h2_w1_f4(a.K) + 2 * kH2GruF4;
     for (int c0 = 0; c0 < nct; c0 += 4) {
@@ -1304,7 +1308,7 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
                 u32x4v w[2];
 #pragma unroll
                 for (int pl = 0; pl < 2; ++pl)
-                    w[pl] = W2L ? W2s[h2_w2_idx(c, sl, pl, lane)] : W2g[h2_w2_idx(c, sl, pl, lane)];
+                    w[pl] = W2L ? W2s[h2_w2_idx(c, sl, pl, lane2)] : W2g[h2_w2_idx(c, sl, pl, lane2)];
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) a2[nt] = mfma_h2(w, hq[sl][nt], a2[nt]);
             }
@@ -1989,6 +1993,37 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 #ifndef ASG_ROLLOUT_NOSTORE
 #define ASG_ROLLOUT_NOSTORE 0
 #endif
+#ifndef ASG_ROLLOUT_EARLY
+#define ASG_ROLLOUT_EARLY 0
+#endif
+// the batch rows are written once and not re-read by this kernel: streaming (nontemporal) stores
+#ifndef ASG_ROLLOUT_NT
+#define ASG_ROLLOUT_NT 1
+#endif
+typedef long long i64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void ro_st(float *p, float4 v) {
+    const f32x4 x{v.x, v.y, v.z, v.w};
+#if ASG_ROLLOUT_NT
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
+#else
+    *reinterpret_cast<f32x4 *>(p) = x;
+#endif
+}
+__device__ __forceinline__ void ro_st(int64_t *p, long long a, long long b) {
+    const i64x2v x{a, b};
+#if ASG_ROLLOUT_NT
+    __builtin_nontemporal_store(x, reinterpret_cast<i64x2v *>(p));
+#else
+    *reinterpret_cast<i64x2v *>(p) = x;
+#endif
+}
+__device__ __forceinline__ void ro_st(uint8_t *p, uint32_t v) {
+#if ASG_ROLLOUT_NT
+    __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(p));
+#else
+    *reinterpret_cast<uint32_t *>(p) = v;
+#endif
+}
 struct RolloutArgs {
     // the time-major batch rows the step touches, each a contiguous [E][..] slab
     float *obs1;        // obs row ts + 1        [E][n][K]
@@ -2027,7 +2062,7 @@ struct RolloutArgs {
 };
 
 __host__ __device__ static inline int64_t rollout_scratch_bytes(int n, int m) {
-    return ((int64_t)4 * m + 4 * m + 4 * n + 8 * n + 15) / 16 * 16 + 16;
+    return ((int64_t)4 * m + 4 * m + 4 * n + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -2081,6 +2116,26 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
         ok[nt] = true;
         act[nt] = s_act[ia[nt]];
     }
+    // bit 1: the one-hot block's W1 columns, bit 2: the h_t rows, loaded before the tile's
+    // stores (gfx9's vmcnt retires memory ops in order: a load issued behind the observation
+    // stores waits for their write acknowledgements)
+#if ASG_ROLLOUT_EARLY & 1
+    float4 g0[4][NT];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            g0[t][nt] = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * t + 4 * q);
+#endif
+#if ASG_ROLLOUT_EARLY & 2
+    float4 hB[4][NT];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     // obs block 0 = onehot(a) (row ts + 1), actions_onehot (row ts), avail = 1 (row ts + 1)
     for (int u = 0; u < (ASG_ROLLOUT_NOSTORE ? 0 : U); ++u)
 #pragma unroll
@@ -2089,14 +2144,12 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
             for (int nt = 0; nt < NT; ++nt) {
                 const int j0 = 32 * u + 16 * c + 4 * q;
                 const int aa = act[nt];
-                *reinterpret_cast<float4 *>(ra.obs1 + rows[nt] * K + j0) =
-                    make_float4(aa == j0, aa == j0 + 1, aa == j0 + 2, aa == j0 + 3);
+                ro_st(ra.obs1 + rows[nt] * K + j0, make_float4(aa == j0, aa == j0 + 1, aa == j0 + 2, aa == j0 + 3));
                 if (ra.onehot0) {
-                    longlong2 *hp = reinterpret_cast<longlong2 *>(ra.onehot0 + rows[nt] * m + j0);
-                    hp[0] = make_longlong2(aa == j0, aa == j0 + 1);
-                    hp[1] = make_longlong2(aa == j0 + 2, aa == j0 + 3);
+                    ro_st(ra.onehot0 + rows[nt] * m + j0, aa == j0, aa == j0 + 1);
+                    ro_st(ra.onehot0 + rows[nt] * m + j0 + 2, aa == j0 + 2, aa == j0 + 3);
                 }
-                if (ra.avail1) *reinterpret_cast<uint32_t *>(ra.avail1 + rows[nt] * m + j0) = 0x01010101u;
+                if (ra.avail1) ro_st(ra.avail1 + rows[nt] * m + j0, 0x01010101u);
             }
     // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
     const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);
@@ -2110,7 +2163,11 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
+#if ASG_ROLLOUT_EARLY & 1
+                const float4 g = g0[mt][nt];
+#else
                 const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
+#endif
                 acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
             }
         float mx = 0.f;
@@ -2141,8 +2198,8 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                         xv[c][nt] = make_float4(vv[0], vv[1], vv[2], vv[3]);
                         if (attempt == 0 && !ASG_ROLLOUT_NOSTORE) {
                             const int j0 = 32 * u + 16 * c + 4 * q;
-                            *reinterpret_cast<float4 *>(ra.obs1 + rows[nt] * K + m * l + j0) = xv[c][nt];
-                            if (l == 1 && ra.beta1) *reinterpret_cast<float4 *>(ra.beta1 + rows[nt] * m + j0) = xv[c][nt];
+                            ro_st(ra.obs1 + rows[nt] * K + m * l + j0, xv[c][nt]);
+                            if (l == 1 && ra.beta1) ro_st(ra.beta1 + rows[nt] * m + j0, xv[c][nt]);
                         }
                     }
                 // the h2 kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
@@ -2155,27 +2212,36 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                                          xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
                     split2s(x8, scx, xp[nt][0], xp[nt][1]);
                 }
+                // two copies of the MFMA block: merged after an LDS-or-global select, the MFMAs
+                // would wait for vmcnt(0) -- every observation store of the tile -- each slice
+                auto mma = [&](bool lds) {
 #pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
-                    u32x4v w[2];
-                    if (sl < s_l2) {
-                        const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
+                    for (int mt = 0; mt < 4; ++mt) {
+                        u32x4v w[2];
+                        if (lds) {
+                            const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
 #pragma unroll
-                        for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
-                    } else {
+                            for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
+                        } else {
 #pragma unroll
-                        for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
+                            for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
+                        }
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
                     }
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
-                }
+                };
+                if (sl < s_l2)
+                    mma(true);
+                else
+                    mma(false);
             }
         }
         const float tmax = wave_max_f32(mx);
         if (!(tmax * scx >= 32768.f) || attempt > 0) break;
         sx = h2_scale(tmax, -90, 90 - sw[0]);
     }
-    // h_t rows (the only agent-side loads of the tile), issued after fc1 like the h2 kernel
+#if !(ASG_ROLLOUT_EARLY & 2)
+    // h_t rows, issued after fc1 like the h2 kernel
     float4 hB[4][NT];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -2183,6 +2249,7 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
         for (int nt = 0; nt < NT; ++nt)
             hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     f32x4 xB[4][NT];
     {
         const float un = pow2f(-(sw[0] + sx));
@@ -2211,7 +2278,6 @@ rollout_h2_kernel(RolloutArgs ra) {
     float *s_scale = reinterpret_cast<float *>(scr);
     int *s_cnt = reinterpret_cast<int *>(s_scale + m);
     int *s_act = s_cnt + m;
-    double *s_rew = reinterpret_cast<double *>(scr + (((int64_t)8 * m + 4 * n + 7) & ~(int64_t)7));
     const int64_t GW = (int64_t)gridDim.x * kH2Waves;
     for (int64_t e = (int64_t)blockIdx.x * kH2Waves + wv; e < ra.E; e += GW) {
         const EnvKey key = env_key(ra.seed, ra.env_base + e);
@@ -2231,25 +2297,32 @@ rollout_h2_kernel(RolloutArgs ra) {
             atomicAdd(&s_cnt[ai], 1);
         }
         wave_lds_fence();
-        for (int i = lane; i < n; i += 64) {
-            const int j = s_act[i];
-            const int p = ra.prev[e * n + i];
-            const Bump32 b = philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
-            const double beta = bump64_at(b, k);
-            const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
-            const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
-            const double bh = beta - ra.lambda_ * pen;
-            const double rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
-            s_rew[i] = rr;
-            if (ra.rew0) ra.rew0[e * n + i] = (float)rr;
-            ra.prev[e * n + i] = j;
-            if (ra.prev1) ra.prev1[e * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+        double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            double rr = 0.0;
+            if (i < n) {
+                const int j = s_act[i];
+                const int p = ra.prev[e * n + i];
+                const Bump32 b =
+                    philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
+                const double beta = bump64_at(b, k);
+                const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+                const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+                const double bh = beta - ra.lambda_ * pen;
+                rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+                if (ra.rew0) ra.rew0[e * n + i] = (float)rr;
+                ra.prev[e * n + i] = j;
+                if (ra.prev1) ra.prev1[e * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+            }
+            const int lo = __double2loint(rr), hi = __double2hiint(rr);
+            const int cnt = n - i0 < 64 ? n - i0 : 64;
+            for (int l2 = 0; l2 < cnt; ++l2)
+                sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
         }
         wave_lds_fence();
         err = wave_or_i32(err);
         if (lane == 0) {
-            double sum = 0.0;
-            for (int i = 0; i < n; ++i) sum += s_rew[i];  // Python's sum(rewards), left to right
             ra.returns[e] += sum;
             bool term = k + 1 >= T;
             if (ra.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
