@@ -185,9 +185,9 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--fused-rollout", type=int, default=1,
-                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select); "
-                        "0: separate asg_step + agent select launches")
+    p.add_argument("--fused-rollout", type=int, default=1, choices=[0, 1, 2],
+                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select) where the "
+                        "env reports it faster; 2: wherever it applies; 0: separate asg_step + select launches")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -208,7 +208,7 @@ def make_args(a, E, selector=None, agent=None):
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
         agent=agent or a.agent, seed=a.seed,
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac",
-        reuse_batch=True, fused_rollout=bool(a.fused_rollout))
+        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always"}[a.fused_rollout])
 
 
 class NullLogger:

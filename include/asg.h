@@ -320,6 +320,11 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
                     const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
                     int32_t *status, void *hip_stream);
+/* Number of fc1 weight slices (32 inputs x 64 units) the fused rollout kernel reads through
+ * L2 instead of LDS for an (n, m, L) env, or -1 when asg_step_select does not take the shape.
+ * Each such slice waits for the tile's pending batch stores (gfx9 vmcnt retires in order), so
+ * callers prefer the fused kernel when it is 0 or 1 (64 x 64, L = 3: 1; 256 x 256: 20). */
+int asg_step_select_l2_slices(int n, int m, int L);
 
 /* ==== RealConstellationEnv ======================================
  * Batched form of src/envs/real_constellation_env.py with injected benefits

@@ -58,13 +58,16 @@ class BasicMAC:
     def fused_step_ok(self, env, ep_batch):
         """The runner may fuse env.step(t) with select_actions(t + 1) (asg_step_select):
         the fused agent + epsilon-greedy selection on plain observation inputs, a time-major
-        batch and an env that takes it."""
+        batch and an env that takes it.  args.fused_rollout: True (default) where the env
+        reports the fused kernel as the faster schedule, "always" wherever it applies,
+        False never."""
         from ..modules.agents.rnn_agent import RNNFusedAgent
-        return (self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select") and env.can_step_select()
+        mode = getattr(self.args, "fused_rollout", True)
+        return (bool(mode) and self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select")
+                and env.can_step_select(prefer=(mode != "always"))
                 and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
                 and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
-                and bool(self.args.use_rnn) and self.selector_agent.n_out == env.m
-                and bool(getattr(self.args, "fused_rollout", True)))
+                and bool(self.args.use_rnn) and self.selector_agent.n_out == env.m)
 
     def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
         """env.step at row t_ep and select_actions for row t_ep + 1 in one kernel; the

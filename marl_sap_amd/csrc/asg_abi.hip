@@ -524,6 +524,8 @@ static void *tm_slab(const asg_field &f, int t, int64_t E, int64_t d2, int64_t d
     return static_cast<char *>(f.ptr) + (size_t)t * f.stride[1] * esize;
 }
 
+int asg_step_select_l2_slices(int n, int m, int L) { return asg::rollout_l2_slices(n, m, L); }
+
 int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                     const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,

@@ -1993,12 +1993,19 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 #ifndef ASG_ROLLOUT_NOSTORE
 #define ASG_ROLLOUT_NOSTORE 0
 #endif
+// timing experiments only (wrong results): 1 = the L2 fc1 slices read LDS slice 0 instead,
+// 2 = h_t not loaded (constants), 4 = the one-hot W1 columns not gathered (zeros)
+#ifndef ASG_ROLLOUT_SKIP
+#define ASG_ROLLOUT_SKIP 0
+#endif
 #ifndef ASG_ROLLOUT_EARLY
 #define ASG_ROLLOUT_EARLY 0
 #endif
-// the batch rows are written once and not re-read by this kernel: streaming (nontemporal) stores
+// 1: streaming (nontemporal) stores for the batch rows.  Measured on MI355X boxes of this pool:
+// 0.78 ms on some, 0.89-0.93 ms on others, against 0.82-0.84 ms with plain stores everywhere
+// (the write acknowledgements the in-order vmcnt waits on take box-dependent paths), so off
 #ifndef ASG_ROLLOUT_NT
-#define ASG_ROLLOUT_NT 1
+#define ASG_ROLLOUT_NT 0
 #endif
 typedef long long i64x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void ro_st(float *p, float4 v) {
@@ -2165,6 +2172,8 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
             for (int mt = 0; mt < 4; ++mt) {
 #if ASG_ROLLOUT_EARLY & 1
                 const float4 g = g0[mt][nt];
+#elif ASG_ROLLOUT_SKIP & 4
+                const float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
 #else
                 const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
 #endif
@@ -2221,7 +2230,8 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                         if (lds) {
                             const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
 #pragma unroll
-                            for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
+                            for (int pl = 0; pl < 2; ++pl)
+                                w[pl] = W1s[h2_w1_idx((ASG_ROLLOUT_SKIP & 1) && sl >= s_l2 ? 0 : sl - s0, mt, pl, lane)];
                         } else {
 #pragma unroll
                             for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
@@ -2230,7 +2240,7 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
                     }
                 };
-                if (sl < s_l2)
+                if (sl < s_l2 || (ASG_ROLLOUT_SKIP & 1))
                     mma(true);
                 else
                     mma(false);
@@ -2247,8 +2257,9 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-            hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+            hB[t][nt] = (ASG_ROLLOUT_SKIP & 2) ? make_float4(0.5f, 0.25f, -0.5f, 0.125f)
+                        : a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
     f32x4 xB[4][NT];
     {
@@ -2342,6 +2353,39 @@ bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn) {
            st.m % 32 == 0 && st.n % 32 == 0 && K == st.m * (st.L + 1) && st.L >= 1;
 }
 
+// LDS plan of the fused rollout: GRU planes, biases, W2 (when it fits), as many fc1 slices as
+// fit, then the per-wave transition scratch
+struct RolloutLds {
+    bool w2l;
+    int w1_lds, l2_slices;
+    int64_t scratch_off;
+    size_t bytes;
+};
+static RolloutLds rollout_lds_plan(int n, int m, int L) {
+    constexpr int64_t kCap = 160 * 1024 / 16;
+    const int K = m * (L + 1), nout = m;
+    RolloutLds p{};
+    const int64_t scr_f4 = (rollout_scratch_bytes(n, m) * kH2Waves + 15) / 16;
+    p.w2l = h2_w2_off(nout) + h2_w2_f4(nout) + scr_f4 <= kCap;
+    const int64_t w1off = h2_w1_off(nout, p.w2l);
+    const int64_t slices = K / 32 - nout / 32, fit = (kCap - scr_f4 - w1off) / (4 * 2 * 64);
+    p.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
+    p.l2_slices = (int)(slices - p.w1_lds);
+    p.scratch_off = w1off + (int64_t)p.w1_lds * 4 * 2 * 64;
+    p.bytes = (size_t)(p.scratch_off + scr_f4) * 16;
+    return p;
+}
+
+int rollout_l2_slices(int n, int m, int L) {
+    if (n <= 0 || m <= 0 || L < 1 || m > 256 || n % 32 || m % 32) return -1;
+    EnvState st{};
+    st.n = n;
+    st.m = m;
+    st.L = L;
+    if (!rollout_shape_ok(st, m * (L + 1), m, 1)) return -1;
+    return rollout_lds_plan(n, m, L).l2_slices;
+}
+
 hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
                                       const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                       const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,
@@ -2397,14 +2441,11 @@ hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st
     ra.bih = bih;
     ra.bhh = bhh;
     ra.b2 = b2;
-    constexpr int64_t kCap = 160 * 1024 / 16;
-    const int64_t scr_f4 = (rollout_scratch_bytes(st.n, st.m) * kH2Waves + 15) / 16;
-    const bool w2l = h2_w2_off(nout) + h2_w2_f4(nout) + scr_f4 <= kCap;
-    const int64_t w1off = h2_w1_off(nout, w2l);
-    const int64_t slices = K / 32 - nout / 32, fit = (kCap - scr_f4 - w1off) / (4 * 2 * 64);
-    ra.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
-    ra.scratch_off = w1off + (int64_t)ra.w1_lds * 4 * 2 * 64;
-    const size_t lds_b = (size_t)(ra.scratch_off + scr_f4) * 16;
+    const RolloutLds plan = rollout_lds_plan(st.n, st.m, st.L);
+    const bool w2l = plan.w2l;
+    ra.w1_lds = plan.w1_lds;
+    ra.scratch_off = plan.scratch_off;
+    const size_t lds_b = plan.bytes;
     const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
     const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
     if (w2l)

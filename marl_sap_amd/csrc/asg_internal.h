@@ -105,6 +105,7 @@ struct RolloutSlabs {
     int64_t *act1;
 };
 bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn);
+int rollout_l2_slices(int n, int m, int L);
 hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
                                       const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                       const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,

@@ -98,3 +98,15 @@ def test_agent_pack_layout_without_gpu(L):
                                                                     and 16 <= m <= 256) else 0
         assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K) + h2), (K, m, rnn)
     assert L.asg_rnn_agent_packed_size(256, 32, 64, 1) < 0  # hidden must be 64
+
+
+def test_step_select_l2_slices_without_gpu(L):
+    """The fused rollout's LDS plan (asg_step_select_l2_slices): fc1 slices read through L2,
+    -1 for shapes asg_step_select rejects."""
+    assert L.asg_step_select_l2_slices(64, 64, 3) == 1
+    assert L.asg_step_select_l2_slices(64, 64, 1) == 0
+    assert L.asg_step_select_l2_slices(256, 256, 3) > 1
+    assert L.asg_step_select_l2_slices(30, 64, 3) == -1
+    assert L.asg_step_select_l2_slices(64, 48, 3) == -1
+    assert L.asg_step_select_l2_slices(64, 512, 3) == -1
+    assert L.asg_step_select_l2_slices(64, 64, 0) == -1

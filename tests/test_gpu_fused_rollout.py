@@ -32,7 +32,7 @@ def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protoco
         runner_log_interval=10 ** 12, n=n, m=m, T=T, hidden_dim=64, use_rnn=True, obs_last_action=False,
         obs_agent_id=False, agent_output_type="q", action_selector="epsilon_greedy", agent="rnn_fused",
         mac="basic_mac", seed=3, epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
-        evaluation_epsilon=0.0, fused_rollout=fused)
+        evaluation_epsilon=0.0, fused_rollout="always" if fused else False)
     runner = RUN["gpu"](args, _Logger())
     env = runner.get_env()
     torch.manual_seed(1234)
