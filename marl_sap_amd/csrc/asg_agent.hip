@@ -2283,14 +2283,19 @@ rollout_h2_kernel(RolloutArgs ra) {
     int sw[4];
     h2_stage<W2L>(rollout_h2args(ra), s_h2, sw);
     __syncthreads();
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int n = ra.n, m = ra.m, T = ra.T, k = ra.k;
     char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
     float *s_scale = reinterpret_cast<float *>(scr);
     int *s_cnt = reinterpret_cast<int *>(s_scale + m);
     int *s_act = s_cnt + m;
     const int64_t GW = (int64_t)gridDim.x * kH2Waves;
-    for (int64_t e = (int64_t)blockIdx.x * kH2Waves + wv; e < ra.E; e += GW) {
+    for (int64_t e0 = (int64_t)blockIdx.x * kH2Waves + wv; e0 < ra.E; e0 += GW) {
+        // addresses are recomputed from e each env: strength-reduced per-lane pointers carried
+        // across the env loop were spilled around the tile loop, and their reloads waited for
+        // every store of the env
+        int64_t e = e0;
+        asm volatile("" : "+s"(e));
         const EnvKey key = env_key(ra.seed, ra.env_base + e);
         // ---- transition (lane = agent): counts, rewards, returns (step_kernel's arithmetic)
         for (int j = lane; j < m; j += 64) {
