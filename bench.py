@@ -425,6 +425,19 @@ def main():
         pm = pmc_lookup("*pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
     achieved = per_launch / (roof_ms * 1e-3) / 1e9
     traffic = pm.get("hbm_bytes_per_launch") if pm else None
+    issue = None
+    if res.get("fused_ms"):
+        # the fused kernel is issue/latency-bound rather than HBM-bound: its SQ counters
+        # (tools/pmc_agent_summary.py over the round profile's SQ pass), when profiled
+        pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L)
+        if pq:
+            c, d = pq["counters"], pq["derived"]
+            issue = {"valu_insts_per_launch": round(c["SQ_INSTS_VALU"]),
+                     "mfma_insts_per_launch": round(c["SQ_INSTS_MFMA"]),
+                     "valu_issue_frac": round(c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_WAVE_INSTR
+                                              / (SIMDS * CLOCK_HZ * roof_ms * 1e-3), 4),
+                     "mfma_busy_frac": round(d["mfma_busy_frac"], 4), "wait_any_frac": round(d["wait_any_frac"], 4),
+                     "pmc": os.path.basename(pq.get("_path", "")) or None}
 
     secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))
     extra = {}
@@ -473,7 +486,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": roof_kernel, "kernel_ms": round(roof_ms, 4),
-                         "bytes_per_launch": per_launch},
+                         "bytes_per_launch": per_launch, **({"issue": issue} if issue else {})},
             "kernels_ms": {"fused_step_select": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
                            "env_step": round(kern_ms, 4) if kern_ms else None,
                            "select": round(sel_ms, 4) if sel_ms else None,

@@ -23,6 +23,10 @@ def main():
     p.add_argument("--kernel", default="rnn_agent_lds_kernel")
     p.add_argument("--rows", type=int, default=16384 * 64)
     p.add_argument("--note", default="")
+    p.add_argument("--n", type=int, default=None)
+    p.add_argument("--m", type=int, default=None)
+    p.add_argument("--E", type=int, default=None)
+    p.add_argument("--L", type=int, default=None)
     a = p.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     name = None
@@ -37,7 +41,8 @@ def main():
         if a.kernel in r["Name"]:
             kt_ms = float(r["AverageNs"]) / 1e6
     tiles = a.rows / 32
-    out = {
+    out = {k: getattr(a, k) for k in ("n", "m", "E", "L") if getattr(a, k) is not None}
+    out.update({
         "kernel": (name or a.kernel).split("(")[0] + (f" -- {a.note}" if a.note else ""),
         "dispatches_averaged": n,
         "kernel_ms_from_kernel_trace": kt_ms,
@@ -49,7 +54,7 @@ def main():
             "mfma_insts_per_wave_tile": avg["SQ_INSTS_MFMA"] / tiles,
             "valu_insts_per_wave_tile": avg["SQ_INSTS_VALU"] / tiles,
         },
-    }
+    })
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out["derived"]))
 

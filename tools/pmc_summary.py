@@ -34,6 +34,8 @@ def main():
     p.add_argument("--m", type=int, default=64)
     p.add_argument("--L", type=int, default=3)
     p.add_argument("--E", type=int, default=16384)
+    p.add_argument("--fetch-doubled", action="store_true",
+                   help="headline bytes with FETCH_SIZE doubled (kernels whose reads are 16-B/lane streams)")
     a = p.parse_args()
     fetch, write = load(a.fetch_dir, "FETCH_SIZE"), load(a.write_dir, "WRITE_SIZE")
     kernels = {}
@@ -48,9 +50,11 @@ def main():
     sel = [k for k in kernels if a.kernel in k]
     main_k = max(sel, key=lambda k: kernels[k]["write_kib"]) if sel else None
     out = {"n": a.n, "m": a.m, "L": a.L, "E": a.E, "kernel": main_k,
-           "hbm_bytes_per_launch": round(kernels[main_k]["hbm_bytes_raw"]) if main_k else None,
-           "note": "(FETCH_SIZE + WRITE_SIZE) KiB * 1024 per launch, averaged over launches; "
-                   "separate --pmc passes; see kernels[] for the fetch-doubled variant",
+           "hbm_bytes_per_launch": round(kernels[main_k]["hbm_bytes_fetch_doubled" if a.fetch_doubled
+                                                 else "hbm_bytes_raw"]) if main_k else None,
+           "note": ("(2 FETCH_SIZE + WRITE_SIZE)" if a.fetch_doubled else "(FETCH_SIZE + WRITE_SIZE)")
+                   + " KiB * 1024 per launch, averaged over launches; separate --pmc passes; see kernels[] "
+                     "for both variants",
            "kernels": kernels}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "kernels"}))
