@@ -185,9 +185,9 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--fused-rollout", type=int, default=1, choices=[0, 1, 2],
-                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select) where the "
-                        "env reports it faster; 2: wherever it applies; 0: separate asg_step + select launches")
+    p.add_argument("--fused-rollout", type=int, default=0, choices=[0, 1, 2],
+                   help="0 (default): separate asg_step + agent select launches; 1: env step t + agent/eps-greedy "
+                        "t+1 in one kernel (asg_step_select) where the env reports it faster; 2: wherever it applies")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -196,8 +196,9 @@ def parse(argv=None):
     return a
 
 
-def make_args(a, E, selector=None, agent=None):
+def make_args(a, E, selector=None, agent=None, fused=None):
     selector = selector or a.selector
+    fused = a.fused_rollout if fused is None else fused
     sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy"}[selector]
     return SimpleNamespace(
         batch_size_run=E, env="mock_constellation_env",
@@ -208,7 +209,7 @@ def make_args(a, E, selector=None, agent=None):
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
         agent=agent or a.agent, seed=a.seed,
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac",
-        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always"}[a.fused_rollout])
+        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always"}[fused])
 
 
 class NullLogger:
@@ -245,7 +246,7 @@ def cpu_baseline(a):
                                                      f"(oracle/asg_rollout.c), no agent network"}}
 
 
-def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_lsa=False):
+def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_lsa=False, fused=None):
     """Build runner + MAC for one workload and time `steps` transitions after `warmup`.
     Returns elapsed seconds (max over ranks) and mean HIP-event times of the env step, the
     whole selection, and (SAP) the selector kernel alone."""
@@ -254,7 +255,7 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     from marl_sap_amd.runners import REGISTRY as r_REGISTRY
 
     selector = selector or a.selector
-    args = make_args(a, E, selector, agent)
+    args = make_args(a, E, selector, agent, fused)
     runner = r_REGISTRY["gpu"](args, NullLogger())
     env = runner.get_env()
     torch.manual_seed(a.seed)  # identical agent weights on every rank
@@ -451,6 +452,17 @@ def main():
                 "what": "configs[2] read literally: BasicMAC + the PyTorch RNNAgent module (hipBLASLt linears + "
                         "GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
                 "select_ms": round(r2["sel_ms"], 4), "env_step_ms": round(r2["kern_ms"], 4)}
+        if a.selector == "eps" and a.agent == "rnn_fused" and not a.fused_rollout:
+            r4 = run_leg(a, dev, world, E, sk, sw, fused=1)
+            if r4.get("fused_ms"):
+                fb = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
+                extra["fused_rollout"] = {
+                    "value": round(r4["global_envs"] * sk / r4["elapsed"], 1), "unit": "env-steps/s",
+                    "ms_per_step": round(r4["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                    "what": "same workload with --fused-rollout 1: asg_step_select (env step t + agent forward + "
+                            "eps-greedy for t + 1 in one kernel, observations consumed on chip) for T - 1 of T steps",
+                    "fused_step_select_ms": round(r4["fused_ms"], 4),
+                    "hbm_achieved_gbs": round(fb / (r4["fused_ms"] * 1e-3) / 1e9, 1), "bytes_per_launch": fb}
         if a.n <= a.m <= 64 and a.selector != "sap":
             r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn_fused", count_lsa=True)
             agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)
