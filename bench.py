@@ -185,9 +185,9 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--fused-rollout", type=int, default=0, choices=[0, 1, 2],
-                   help="0 (default): separate asg_step + agent select launches; 1: env step t + agent/eps-greedy "
-                        "t+1 in one kernel (asg_step_select) where the env reports it faster; 2: wherever it applies")
+    p.add_argument("--fused-rollout", type=int, default=1, choices=[0, 1, 2],
+                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select) where the env "
+                        "reports it faster; 2: wherever it applies; 0: separate asg_step + agent select launches")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -452,17 +452,26 @@ def main():
                 "what": "configs[2] read literally: BasicMAC + the PyTorch RNNAgent module (hipBLASLt linears + "
                         "GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
                 "select_ms": round(r2["sel_ms"], 4), "env_step_ms": round(r2["kern_ms"], 4)}
-        if a.selector == "eps" and a.agent == "rnn_fused" and not a.fused_rollout:
-            r4 = run_leg(a, dev, world, E, sk, sw, fused=1)
+        if a.selector == "eps" and a.agent == "rnn_fused":
+            # the other schedule of the same workload: split launches when the headline fused them
+            # (or the fused kernel when the headline ran split)
+            other = 0 if res.get("fused_ms") else 1
+            r4 = run_leg(a, dev, world, E, sk, sw, fused=other)
+            leg = {"value": round(r4["global_envs"] * sk / r4["elapsed"], 1), "unit": "env-steps/s",
+                   "ms_per_step": round(r4["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                   "env_step_ms": round(r4["kern_ms"], 4) if r4["kern_ms"] else None,
+                   "select_ms": round(r4["sel_ms"], 4) if r4["sel_ms"] else None}
             if r4.get("fused_ms"):
                 fb = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
-                extra["fused_rollout"] = {
-                    "value": round(r4["global_envs"] * sk / r4["elapsed"], 1), "unit": "env-steps/s",
-                    "ms_per_step": round(r4["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
-                    "what": "same workload with --fused-rollout 1: asg_step_select (env step t + agent forward + "
-                            "eps-greedy for t + 1 in one kernel, observations consumed on chip) for T - 1 of T steps",
-                    "fused_step_select_ms": round(r4["fused_ms"], 4),
-                    "hbm_achieved_gbs": round(fb / (r4["fused_ms"] * 1e-3) / 1e9, 1), "bytes_per_launch": fb}
+                leg.update({"what": "same workload with --fused-rollout 1: asg_step_select (env step t + agent "
+                                    "forward + eps-greedy for t + 1 in one kernel) for T - 1 of T steps",
+                            "fused_step_select_ms": round(r4["fused_ms"], 4),
+                            "hbm_achieved_gbs": round(fb / (r4["fused_ms"] * 1e-3) / 1e9, 1), "bytes_per_launch": fb})
+                extra["fused_rollout"] = leg
+            elif other == 0:
+                leg["what"] = ("same workload with --fused-rollout 0: asg_step then the fused agent forward + "
+                               "eps-greedy kernel (rnn_agent_h2_kernel), one launch each per step")
+                extra["split_rollout"] = leg
         if a.n <= a.m <= 64 and a.selector != "sap":
             r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn_fused", count_lsa=True)
             agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)

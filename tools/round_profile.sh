@@ -3,7 +3,7 @@
 #   rocprofv3 kernel statistics of the default bench (configs[2]: asg_step + fused agent
 #   select) and of configs[4] (256x256 dense), separate PMC passes (FETCH_SIZE, WRITE_SIZE,
 #   SQ counters) for the step and agent kernels at both sizes; the same for the fused
-#   rollout kernel (--fused-rollout 1) at configs[2]; the SAP leg's kernel statistics.
+#   rollout kernel (--fused-rollout 0) at configs[2]; the SAP leg's kernel statistics.
 #   Every GPU step has its own time limit; the chain stops at the first failure.
 #   (GPU tests / smoke / the plain bench line run in their own call.)
 set -o pipefail
@@ -16,11 +16,11 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B --steps 20 --warmup 5 > "$OUT/fetch.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B --steps 20 --warmup 5 > "$OUT/write.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq" -o run -- python3 $B --steps 20 --warmup 5 > "$OUT/sq.log" 2>&1 &&
-timeout -k 10 300 python bench.py --cpu-baseline 0 --secondary 0 --fused-rollout 1 > "$OUT/bench_fused.log" 2>&1 &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_fused" -o run -- python3 $B --fused-rollout 1 > "$OUT/kt_fused.log" 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_fused" -o run -- python3 $B --fused-rollout 1 --steps 20 --warmup 5 > "$OUT/fetch_fused.log" 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_fused" -o run -- python3 $B --fused-rollout 1 --steps 20 --warmup 5 > "$OUT/write_fused.log" 2>&1 &&
-timeout -k 10 400 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq_fused" -o run -- python3 $B --fused-rollout 1 --steps 20 --warmup 5 > "$OUT/sq_fused.log" 2>&1 &&
+timeout -k 10 300 python bench.py --cpu-baseline 0 --secondary 0 --fused-rollout 0 > "$OUT/bench_split.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_split" -o run -- python3 $B --fused-rollout 0 > "$OUT/kt_split.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_split" -o run -- python3 $B --fused-rollout 0 --steps 20 --warmup 5 > "$OUT/fetch_split.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_split" -o run -- python3 $B --fused-rollout 0 --steps 20 --warmup 5 > "$OUT/write_split.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq_split" -o run -- python3 $B --fused-rollout 0 --steps 20 --warmup 5 > "$OUT/sq_split.log" 2>&1 &&
 timeout -k 10 300 python bench.py --config 4 --cpu-baseline 0 > "$OUT/bench_256.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_256" -o run -- python3 $B --config 4 > "$OUT/kt_256.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_256" -o run -- python3 $B --config 4 --steps 20 --warmup 5 > "$OUT/fetch_256.log" 2>&1 &&
