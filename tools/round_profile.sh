@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round-end evidence on one MI355X (run through gpurun from the repo root):
-#   rocprofv3 kernel statistics of the default bench (configs[2]: asg_step + fused agent
-#   select) and of configs[4] (256x256 dense), separate PMC passes (FETCH_SIZE, WRITE_SIZE,
-#   SQ counters) for the step and agent kernels at both sizes; the same for the fused
-#   rollout kernel (--fused-rollout 0) at configs[2]; the SAP leg's kernel statistics.
+#   rocprofv3 kernel statistics of the default bench (configs[2]: the fused rollout kernel
+#   asg_step_select) and of configs[4] (256x256 dense: asg_step + fused agent select),
+#   separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ counters) for the rollout, step and agent
+#   kernels; the same for the split schedule (--fused-rollout 0) at configs[2]; the SAP leg.
 #   Every GPU step has its own time limit; the chain stops at the first failure.
 #   (GPU tests / smoke / the plain bench line run in their own call.)
 set -o pipefail
