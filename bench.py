@@ -486,6 +486,12 @@ def main():
 
     if a.selector == "random":
         ra = None
+    elif res.get("fused_ms"):
+        # the separate agent kernel only runs the episode's first selection here (h = 0, the
+        # W_hh products skipped): its figure comes from the split-schedule leg when it ran
+        sp = extra.get("split_rollout")
+        ra = agent_roofline(a, E, sp["select_ms"], "asg::rnn_agent_h2_kernel (forward + eps-greedy), "
+                            "split-schedule leg") if sp and sp.get("select_ms") else None
     elif a.selector == "sap":
         ra = agent_roofline(a, E, sel_ms - (res["lsa_ms"] or 0.0), f"{a.agent} forward")
     else:
