@@ -17,11 +17,21 @@ struct u32x4 {
     uint32_t x, y, z, w;
 };
 
+#ifndef ASG_PHILOX_MAD64
+#define ASG_PHILOX_MAD64 1
+#endif
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+#if ASG_PHILOX_MAD64
+        // one v_mad_u64_u32 per product instead of v_mul_hi_u32 + v_mul_lo_u32
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
         const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
         const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+#endif
         c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -99,7 +109,7 @@ __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, in
     const int q = 24 - (32 - __builtin_clz((unsigned)(T > 0 ? T : 1)));
     b.center = __builtin_ldexpf((float)(((uint64_t)r.y * (uint64_t)(uint32_t)T) >> (32 - q)), -q);
     const float spread = wmin + (wmax - wmin) * ((float)r.z * k2m32);
-    const float s2 = sqrtf(spread * spread / -8.0f / (float)kLog005);
+    const float s2 = sqrtf(spread * spread * -0.125f / (float)kLog005);  // "/ -8" exactly
     b.a2 = 0.72134752044448170f / s2;  // log2(e) / 2 / sigma_2
     return b;
 }
