@@ -20,6 +20,9 @@ struct u32x4 {
 #ifndef ASG_PHILOX_MAD64
 #define ASG_PHILOX_MAD64 1
 #endif
+#ifndef ASG_PHILOX_BITOP3
+#define ASG_PHILOX_BITOP3 1
+#endif
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -32,7 +35,13 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
         const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
         const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
 #endif
+#if ASG_PHILOX_BITOP3
+        // three-input XOR in one v_bitop3_b32 (truth table 0x96; gfx950)
+        c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+                  (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
+#else
         c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+#endif
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
