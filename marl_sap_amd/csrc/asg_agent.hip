@@ -2159,6 +2159,8 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                 if (ra.avail1) ro_st(ra.avail1 + rows[nt] * m + j0, 0x01010101u);
             }
     // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
+    BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
+    bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
     const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);
     const u32x4v *W1g = a.pk + 1;
     const int s0 = U, s_l2 = s0 + a.w1_lds;
@@ -2190,8 +2192,7 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
                         const int j = 32 * u + 16 * c + 4 * q + v;
-                        bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + j, s_scale[j], T, ra.wmin, ra.wmax,
-                                                     ra.dense != 0);
+                        bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + j, s_scale[j], bsh, ra.dense != 0);
                     }
                 }
             for (int l = 1; l <= L; ++l) {

@@ -107,20 +107,35 @@ __device__ __forceinline__ float philox_task_scale(EnvKey key, uint32_t episode,
     return (sc.x & 3u) == 3u ? 10.0f : 1.0f;
 }
 
-__device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale, int T,
-                                                float wmin, float wmax, bool dense) {
+// the bump-shape constants of one launch (T's center grid exponent q, the width range)
+struct BumpShape {
+    int T, q;
+    float wmin, wspan;
+};
+__host__ __device__ inline BumpShape bump_shape(int T, float wmin, float wmax) {
+    int bits = 0;
+    for (unsigned t = (unsigned)(T > 0 ? T : 1); t; t >>= 1) ++bits;
+    return BumpShape{T, 24 - bits, wmin, wmax - wmin};
+}
+
+__device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale,
+                                                const BumpShape &bs, bool dense) {
     const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair, 0u, kCtrPair, episode}, key.k0, key.k1);
     constexpr float k2m32 = 2.3283064365386963e-10f;  // 2^-32
     const bool active = dense || r.x >= 0xC0000000u;
     Bump32 b;
     b.scale = active ? scale : 0.0f;
     // center = T * u on the 2^-q grid: floor(u * T * 2^q) * 2^-q, u = r.y * 2^-32 (< T * 2^q <= 2^24: exact)
-    const int q = 24 - (32 - __builtin_clz((unsigned)(T > 0 ? T : 1)));
-    b.center = __builtin_ldexpf((float)(((uint64_t)r.y * (uint64_t)(uint32_t)T) >> (32 - q)), -q);
-    const float spread = wmin + (wmax - wmin) * ((float)r.z * k2m32);
+    // (the grid index is < 2^24: a 32-bit convert is exact)
+    b.center = __builtin_ldexpf((float)(uint32_t)(((uint64_t)r.y * (uint64_t)(uint32_t)bs.T) >> (32 - bs.q)), -bs.q);
+    const float spread = bs.wmin + bs.wspan * ((float)r.z * k2m32);
     const float s2 = sqrtf(spread * spread * -0.125f / (float)kLog005);  // "/ -8" exactly
     b.a2 = 0.72134752044448170f / s2;  // log2(e) / 2 / sigma_2
     return b;
+}
+__device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale, int T,
+                                                float wmin, float wmax, bool dense) {
+    return philox_bump32(key, episode, pair, scale, bump_shape(T, wmin, wmax), dense);
 }
 
 // float32 evaluation with an error that does not grow with the exponent: x = t - center is
