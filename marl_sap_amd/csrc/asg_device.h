@@ -23,6 +23,9 @@ struct u32x4 {
 #ifndef ASG_PHILOX_BITOP3
 #define ASG_PHILOX_BITOP3 1
 #endif
+#ifndef ASG_BUMP_RCP
+#define ASG_BUMP_RCP 1
+#endif
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -129,8 +132,17 @@ __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, in
     // (the grid index is < 2^24: a 32-bit convert is exact)
     b.center = __builtin_ldexpf((float)(uint32_t)(((uint64_t)r.y * (uint64_t)(uint32_t)bs.T) >> (32 - bs.q)), -bs.q);
     const float spread = bs.wmin + bs.wspan * ((float)r.z * k2m32);
+#if ASG_BUMP_RCP
+    // log2(e) / (2 sigma_2) with sigma_2 = sqrt(spread^2 / -8 / ln 0.05) is, for spread > 0,
+    // log2(e) sqrt(-2 ln 0.05) / spread: one v_rcp_f32 (<= 1 ulp) and a multiply instead of a
+    // correctly rounded sqrt and two divisions (~30 instructions per pair).  Within 3e-7
+    // relative of the float64 formula; every kernel derives the parameters through this one
+    // function and the parity checks use the exported values (asg_export_bump_params).
+    b.a2 = 0x1.c4035ap+1f * __builtin_amdgcn_rcpf(spread);
+#else
     const float s2 = sqrtf(spread * spread * -0.125f / (float)kLog005);  // "/ -8" exactly
     b.a2 = 0.72134752044448170f / s2;  // log2(e) / 2 / sigma_2
+#endif
     return b;
 }
 __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale, int T,
