@@ -2189,11 +2189,20 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
             for (int c = 0; c < 2; ++c)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
+#if ASG_BUMP_PAIR2
+#pragma unroll
+                    for (int v = 0; v < 4; v += 2) {  // pairs (j, j + 1) share one Philox call (m even)
+                        const int j = 32 * u + 16 * c + 4 * q + v;
+                        philox_bump32x2(key, ra.episode, ia[nt] * m + j, s_scale[j], s_scale[j + 1], bsh, ra.dense != 0,
+                                        bp[c][v][nt], bp[c][v + 1][nt]);
+                    }
+#else
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
                         const int j = 32 * u + 16 * c + 4 * q + v;
                         bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + j, s_scale[j], bsh, ra.dense != 0);
                     }
+#endif
                 }
             for (int l = 1; l <= L; ++l) {
                 const int t = k + l;
