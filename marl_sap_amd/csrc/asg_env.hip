@@ -43,6 +43,18 @@ struct BumpSrc {  // Philox, float32 bumps regenerated on the fly (no table in H
         __device__ Pair pair(int i, int j) const {
             return Pair{philox_bump32(key, episode, i * m + j, scale[j], T, wmin, wmax, dense)};
         }
+        // pairs (i, j) and (i, j + 1): one Philox call when they share one (even pair index)
+        __device__ void pair2(int i, int j, Pair &p0, Pair &p1) const {
+#if ASG_BUMP_PAIR2
+            const int p = i * m + j;
+            if ((p & 1) == 0) {
+                philox_bump32x2(key, episode, p, scale[j], scale[j + 1], bump_shape(T, wmin, wmax), dense, p0.b, p1.b);
+                return;
+            }
+#endif
+            p0 = pair(i, j);
+            p1 = pair(i, j + 1);
+        }
     };
     // fills scale[0..m) cooperatively (caller syncs)
     __device__ void fill_scale(int64_t e, float *scale) const {
@@ -70,6 +82,10 @@ struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
             __device__ double at64(int t) const { return p[t * tstride]; }
         };
         __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, nm}; }
+        __device__ void pair2(int i, int j, Pair &p0, Pair &p1) const {
+            p0 = pair(i, j);
+            p1 = pair(i, j + 1);
+        }
     };
     __device__ void fill_scale(int64_t, float *) const {}
     __device__ Env bind(int64_t e, const float *) const {
@@ -96,9 +112,13 @@ __device__ void write_pre_row(const EnvB &src, const asg_batch_view &bv, int64_t
         float oh[VEC];
         typename EnvB::Pair P[VEC];
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) {
-            oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
-            P[q] = src.pair(i, j0 + q);
+        for (int q = 0; q < VEC; ++q) oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
+        if constexpr (VEC % 2 == 0) {
+#pragma unroll
+            for (int q = 0; q < VEC; q += 2) src.pair2(i, j0 + q, P[q], P[q + 1]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) P[q] = src.pair(i, j0 + q);
         }
         float *ob = fptr<float>(bv.obs, e, ts, i, j0);
         if (VEC == 4) {
