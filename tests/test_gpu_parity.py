@@ -557,3 +557,31 @@ def test_epsilon_greedy_writes_batch_row_in_place():
     assert out is row
     assert torch.equal(b["actions"][:, 1, :, 0], q.max(2)[1])
     assert (b["actions"][:, 0] == 0).all() and (b["actions"][:, 2:] == 0).all()
+
+
+def test_philox_bump_parameter_distribution():
+    """The Philox bump draws (one Philox call per two pairs, asg_device.h:philox_bump32x2)
+    follow generate_benefits_over_time's distribution (mock_constellation_env.py:281-293):
+    active with probability 1/4, center ~ U(0, T), width ~ U(wmin, wmax) -- and the two
+    pairs of one call are independent."""
+    n = m = 64
+    T, E = 20, 64
+    env = AssignEnvBatch(n, m, T, 3, 0.5, seed=11, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    env.reset(b, 0)
+    p = env.export_bump_params().cpu().numpy().reshape(E, n * m, 3)
+    scale, center, a = p[..., 0], p[..., 1], p[..., 2]
+    act = scale > 0
+    assert abs(act.mean() - 0.25) < 0.005
+    assert set(np.unique(scale[act])) <= {1.0, 10.0}
+    even, odd = act[:, 0::2], act[:, 1::2]
+    assert abs((even & odd).mean() - 0.0625) < 0.004
+    assert abs(np.corrcoef(even.ravel(), odd.ravel())[0, 1]) < 0.01
+    assert center.min() >= 0.0 and center.max() < T and abs(center.mean() - T / 2) < 0.05
+    spread = float.fromhex("0x1.c4035ap+1") / a.astype(np.float64)  # a = log2(e) sqrt(-2 ln 0.05) / spread
+    lo, hi = spread.min(), spread.max()
+    assert 2.99 < lo and hi < 8.01 and hi - lo > 2.9
+    u = (spread - lo) / (hi - lo)
+    assert abs(u.mean() - 0.5) < 0.01
+    assert abs(np.corrcoef(u[:, 0::2].ravel(), u[:, 1::2].ravel())[0, 1]) < 0.01
+    env.close()
