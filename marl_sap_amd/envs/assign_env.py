@@ -150,7 +150,7 @@ class AssignEnvBatch(MultiAgentEnv):
         """Whether asg_step_select (the fused env step + next selection) takes this env:
         Philox bump/dense benefits, integer actions, n and m multiples of 32, m <= 256.
         With `prefer`, also whether it is the faster schedule: at most one fc1 weight slice
-        read through L2 (measured on MI355X: 64 x 64 +4 %, 256 x 256 -3 % against
+        read through L2 (measured on MI355X: 64 x 64 +15 %, 256 x 256 -3 % against
         asg_step + asg_rnn_agent_select)."""
         ok = (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
               and self.n % 32 == 0 and self.m % 32 == 0 and self.m <= 256 and self.L >= 1)
