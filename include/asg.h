@@ -321,9 +321,11 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
                     int32_t *status, void *hip_stream);
 /* Number of fc1 weight slices (32 inputs x 64 units) the fused rollout kernel reads through
- * L2 instead of LDS for an (n, m, L) env, or -1 when asg_step_select does not take the shape.
- * Each such slice waits for the tile's pending batch stores (gfx9 vmcnt retires in order), so
- * callers prefer the fused kernel when it is 0 or 1 (64 x 64, L = 3: 1; 256 x 256: 20). */
+ * L2 instead of LDS for an (n, m, L) env, or -1 when asg_step_select does not take the shape
+ * (64 x 64, L = 3: 1; 256 x 256: 20).  Each such slice waits for the tile's pending batch
+ * stores (gfx9 vmcnt retires in order); measured, the fused kernel still beats asg_step +
+ * asg_rnn_agent_select at 20 (256 x 256 dense: +8-13 %), so the runner uses it wherever
+ * this is >= 0. */
 int asg_step_select_l2_slices(int n, int m, int L);
 
 /* ==== RealConstellationEnv ======================================

@@ -58,10 +58,9 @@ class BasicMAC:
     def fused_step_ok(self, env, ep_batch):
         """The runner may fuse env.step(t) with select_actions(t + 1) (asg_step_select):
         the fused agent + epsilon-greedy selection on plain observation inputs, a time-major
-        batch and an env that takes it.  args.fused_rollout: True (default) where the env
-        reports the fused kernel as the faster schedule (64 x 64: +15 % over asg_step +
-        asg_rnn_agent_select across MI355X boxes), "always" wherever it applies,
-        False never."""
+        batch and an env that takes it.  args.fused_rollout: True (default) / "always" wherever
+        it applies (64 x 64: +15 %, 256 x 256 dense: +8-13 % over asg_step +
+        asg_rnn_agent_select on MI355X), False never."""
         from ..modules.agents.rnn_agent import RNNFusedAgent
         mode = getattr(self.args, "fused_rollout", True)
         return (bool(mode) and self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select")

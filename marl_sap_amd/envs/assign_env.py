@@ -149,14 +149,13 @@ class AssignEnvBatch(MultiAgentEnv):
     def can_step_select(self, prefer=True):
         """Whether asg_step_select (the fused env step + next selection) takes this env:
         Philox bump/dense benefits, integer actions, n and m multiples of 32, m <= 256.
-        With `prefer`, also whether it is the faster schedule: at most one fc1 weight slice
-        read through L2 (measured on MI355X: 64 x 64 +15 %, 256 x 256 -3 % against
-        asg_step + asg_rnn_agent_select)."""
-        ok = (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
-              and self.n % 32 == 0 and self.m % 32 == 0 and self.m <= 256 and self.L >= 1)
-        if not ok or not prefer:
-            return ok
-        return 0 <= _lib.lib().asg_step_select_l2_slices(self.n, self.m, self.L) <= 1
+        `prefer` (kept for callers that ask whether it is also the faster schedule): measured
+        on MI355X it is wherever it applies -- 64 x 64 +15 %, 256 x 256 dense +8-13 % against
+        asg_step + asg_rnn_agent_select (asg_step_select_l2_slices reports the fc1 weight
+        slices it streams through L2: 1 and 20 there)."""
+        return (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
+                and self.n % 32 == 0 and self.m % 32 == 0 and self.m <= 256 and self.L >= 1
+                and _lib.lib().asg_step_select_l2_slices(self.n, self.m, self.L) >= 0)
 
     def step_select(self, batch, ts, agent, hidden_state, epsilon, seed, counter, status):
         """asg_step at row ts and the fused agent forward + epsilon-greedy for row ts + 1 in
