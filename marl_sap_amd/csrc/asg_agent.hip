@@ -1994,7 +1994,8 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 #define ASG_ROLLOUT_NOSTORE 0
 #endif
 // timing experiments only (wrong results): 1 = the L2 fc1 slices read LDS slice 0 instead,
-// 2 = h_t not loaded (constants), 4 = the one-hot W1 columns not gathered (zeros)
+// 2 = h_t not loaded (constants), 4 = the one-hot W1 columns not gathered (zeros),
+// 8 = the transition's actions / previous tasks not loaded (synthetic)
 #ifndef ASG_ROLLOUT_SKIP
 #define ASG_ROLLOUT_SKIP 0
 #endif
@@ -2315,7 +2316,7 @@ rollout_h2_kernel(RolloutArgs ra) {
         wave_lds_fence();
         int err = 0;
         for (int i = lane; i < n; i += 64) {
-            const int64_t a64 = ra.act0[e * n + i];
+            const int64_t a64 = (ASG_ROLLOUT_SKIP & 8) ? (int64_t)((i * 7 + (int)e) % m) : ra.act0[e * n + i];
             int ai = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
             if (ai < 0) err = ASG_E_ACTION_RANGE;
             ai = ai < 0 ? 0 : ai;
@@ -2329,7 +2330,7 @@ rollout_h2_kernel(RolloutArgs ra) {
             double rr = 0.0;
             if (i < n) {
                 const int j = s_act[i];
-                const int p = ra.prev[e * n + i];
+                const int p = (ASG_ROLLOUT_SKIP & 8) ? (i % m) : ra.prev[e * n + i];
                 const Bump32 b =
                     philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
                 const double beta = bump64_at(b, k);
