@@ -2025,13 +2025,6 @@ __device__ __forceinline__ void ro_st(int64_t *p, long long a, long long b) {
     *reinterpret_cast<i64x2v *>(p) = x;
 #endif
 }
-__device__ __forceinline__ void ro_st(uint8_t *p, uint32_t v) {
-#if ASG_ROLLOUT_NT
-    __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(p));
-#else
-    *reinterpret_cast<uint32_t *>(p) = v;
-#endif
-}
 struct RolloutArgs {
     // the time-major batch rows the step touches, each a contiguous [E][..] slab
     float *obs1;        // obs row ts + 1        [E][n][K]
@@ -2157,8 +2150,13 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                     ro_st(ra.onehot0 + rows[nt] * m + j0, aa == j0, aa == j0 + 1);
                     ro_st(ra.onehot0 + rows[nt] * m + j0 + 2, aa == j0 + 2, aa == j0 + 3);
                 }
-                if (ra.avail1) ro_st(ra.avail1 + rows[nt] * m + j0, 0x01010101u);
             }
+    // avail rows of the tile: 32 contiguous rows of m bytes, all 1 -- full 16-B lanes
+    if (ra.avail1 && !ASG_ROLLOUT_NOSTORE) {
+        uint8_t *ab = ra.avail1 + (e * n + 32 * sub) * m;
+        for (int off = 16 * lane; off < 32 * m; off += 64 * 16)
+            *reinterpret_cast<uint4 *>(ab + off) = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+    }
     // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
     BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
     bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
