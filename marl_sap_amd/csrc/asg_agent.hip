@@ -2106,13 +2106,14 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
     const int n = ra.n, m = ra.m, T = ra.T, L = ra.L, k = ra.k;
     const int K = m * (L + 1);
     const int U = m >> 5;
-    const int64_t row0 = e * n + 32 * sub;
+    constexpr int RT = 16 * NT;  // rows per tile
+    const int64_t row0 = e * n + RT * sub;
     int64_t rows[NT];
     bool ok[NT];
     int ia[NT], act[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        ia[nt] = 32 * sub + 16 * nt + r;
+        ia[nt] = RT * sub + 16 * nt + r;
         rows[nt] = e * n + ia[nt];
         ok[nt] = true;
         act[nt] = s_act[ia[nt]];
@@ -2151,10 +2152,12 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
                     ro_st(ra.onehot0 + rows[nt] * m + j0 + 2, aa == j0 + 2, aa == j0 + 3);
                 }
             }
-    // avail rows of the tile: 32 contiguous rows of m bytes, all 1 -- full 16-B lanes
+    // avail rows of the tile: RT contiguous rows of m bytes, all 1 -- full 16-B lanes
     if (ra.avail1 && !ASG_ROLLOUT_NOSTORE) {
-        uint8_t *ab = ra.avail1 + (e * n + 32 * sub) * m;
-        for (int off = 16 * lane; off < 32 * m; off += 64 * 16)
+        uint8_t *ab = ra.avail1 + (e * n + RT * sub) * m;
+        int off0 = 16 * lane;
+        asm volatile("" : "+v"(off0));  // not hoisted: a per-lane 64-bit address kept across loops spilled
+        for (int off = off0; off < RT * m; off += 64 * 16)
             *reinterpret_cast<uint4 *>(ab + off) = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
     }
     // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
@@ -2356,7 +2359,7 @@ rollout_h2_kernel(RolloutArgs ra) {
             if (err) atomicCAS(ra.env_err, 0, err);
         }
         // ---- agent + selection for row ts + 1, tile by tile
-        for (int sub = 0; sub < n / 32; ++sub) rollout_rows<W2L>(ra, e, sub, key, s_scale, s_act, s_h2, sw);
+        for (int sub = 0; sub < n / (16 * kH2NT); ++sub) rollout_rows<W2L>(ra, e, sub, key, s_scale, s_act, s_h2, sw);
         wave_lds_fence();  // the next env reuses the scratch
     }
 }
