@@ -2008,6 +2008,43 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 #ifndef ASG_ROLLOUT_NT
 #define ASG_ROLLOUT_NT 0
 #endif
+// 1: the transition's actions / previous tasks come through the scalar path (s_load, counted
+// by lgkmcnt): a vector load there sits behind the previous env's ~130 KB of row stores in the
+// in-order vmcnt queue and waits for all their write acknowledgements
+#ifndef ASG_ROLLOUT_SLOAD
+#define ASG_ROLLOUT_SLOAD 1
+#endif
+typedef const int __attribute__((address_space(4))) *cint_sp;
+// lane l < cnt receives the W dwords of element l of the wave-uniform array at base (read-only
+// in this launch: written by the previous launch on the stream, so the scalar cache, which
+// each dispatch starts invalidated, holds no stale line)
+// W dwords per lane (1: int32, 2: int64 as lo / hi), contiguous blocks of 16 lanes so the loads
+// merge into s_load_dwordx16
+template <int W, int CNT>
+__device__ __forceinline__ void sload_spread_n(const void *base, int (&x)[W]) {
+    const cint_sp p = (cint_sp)(uintptr_t)base;
+#pragma unroll
+    for (int w = 0; w < W; ++w) x[w] = 0;
+#pragma unroll
+    for (int l0 = 0; l0 < CNT; l0 += 16) {
+        int v[16 * W];
+#pragma unroll
+        for (int d = 0; d < 16 * W; ++d) v[d] = p[W * l0 + d];
+#pragma unroll
+        for (int l = 0; l < 16; ++l)
+#pragma unroll
+            for (int w = 0; w < W; ++w)
+                asm("v_writelane_b32 %0, %1, %2" : "+v"(x[w]) : "s"(v[W * l + w]), "n"(l0 + l));
+    }
+}
+// cnt is 64 or 32 (the fused rollout takes n % 32 == 0)
+template <int W>
+__device__ __forceinline__ void sload_spread(const void *base, int cnt, int (&x)[W]) {
+    if (cnt >= 64)
+        sload_spread_n<W, 64>(base, x);
+    else
+        sload_spread_n<W, 32>(base, x);
+}
 typedef long long i64x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void ro_st(float *p, float4 v) {
     const f32x4 x{v.x, v.y, v.z, v.w};
@@ -2316,8 +2353,19 @@ rollout_h2_kernel(RolloutArgs ra) {
         }
         wave_lds_fence();
         int err = 0;
-        for (int i = lane; i < n; i += 64) {
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+#if ASG_ROLLOUT_SLOAD
+            int av[2];
+            sload_spread<2>(ra.act0 + e * n + i0, n - i0 < 64 ? n - i0 : 64, av);
+            if (i >= n) continue;
+            const int64_t a64 = (ASG_ROLLOUT_SKIP & 8)
+                                    ? (int64_t)((i * 7 + (int)e) % m)
+                                    : (int64_t)(((uint64_t)(uint32_t)av[1] << 32) | (uint32_t)av[0]);
+#else
+            if (i >= n) continue;
             const int64_t a64 = (ASG_ROLLOUT_SKIP & 8) ? (int64_t)((i * 7 + (int)e) % m) : ra.act0[e * n + i];
+#endif
             int ai = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
             if (ai < 0) err = ASG_E_ACTION_RANGE;
             ai = ai < 0 ? 0 : ai;
@@ -2329,9 +2377,20 @@ rollout_h2_kernel(RolloutArgs ra) {
         for (int i0 = 0; i0 < n; i0 += 64) {
             const int i = i0 + lane;
             double rr = 0.0;
+#if ASG_ROLLOUT_SLOAD
+            int pv[1];
+            sload_spread<1>(ra.prev + e * n + i0, n - i0 < 64 ? n - i0 : 64, pv);
+            // the invariant scalar loads carry no memory ordering: this barrier (fed by their
+            // values) keeps the stores of the same prev row below behind them
+            asm volatile("" : "+v"(pv[0])::"memory");
+#endif
             if (i < n) {
                 const int j = s_act[i];
+#if ASG_ROLLOUT_SLOAD
+                const int p = (ASG_ROLLOUT_SKIP & 8) ? (i % m) : pv[0];
+#else
                 const int p = (ASG_ROLLOUT_SKIP & 8) ? (i % m) : ra.prev[e * n + i];
+#endif
                 const Bump32 b =
                     philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
                 const double beta = bump64_at(b, k);
