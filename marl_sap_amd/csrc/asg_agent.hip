@@ -2000,7 +2000,7 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 #define ASG_ROLLOUT_SKIP 0
 #endif
 #ifndef ASG_ROLLOUT_EARLY
-#define ASG_ROLLOUT_EARLY 0
+#define ASG_ROLLOUT_EARLY 4
 #endif
 // 1: streaming (nontemporal) stores for the batch rows.  Measured on MI355X boxes of this pool:
 // 0.78 ms on some, 0.89-0.93 ms on others, against 0.82-0.84 ms with plain stores everywhere
@@ -2175,6 +2175,22 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
             hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
                               : make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
+#if ASG_ROLLOUT_EARLY & 4
+    // bit 4: fc1's accumulators start from the one-hot block's W1 columns, gathered (and
+    // consumed) before the tile's prefix stores; a rescaled retry gathers them again
+    f32x4 acc[4][NT];
+    int sx = kH2SxInit;
+    {
+        const float scS = pow2f(sw[0] + sx);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
+                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
+            }
+    }
+#endif
     // obs block 0 = onehot(a) (row ts + 1), actions_onehot (row ts), avail = 1 (row ts + 1)
     for (int u = 0; u < (ASG_ROLLOUT_NOSTORE ? 0 : U); ++u)
 #pragma unroll
@@ -2203,10 +2219,15 @@ __device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, i
     const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);
     const u32x4v *W1g = a.pk + 1;
     const int s0 = U, s_l2 = s0 + a.w1_lds;
+#if !(ASG_ROLLOUT_EARLY & 4)
     f32x4 acc[4][NT];
     int sx = kH2SxInit;
+#endif
     for (int attempt = 0;; ++attempt) {
         const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
+#if ASG_ROLLOUT_EARLY & 4
+        if (attempt > 0)
+#endif
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
