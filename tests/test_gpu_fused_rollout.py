@@ -56,6 +56,7 @@ def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protoco
     (32, 96, 5, 2, 10, 0.3, "dense"),   # three 32-task chunks per block, heavy exploration
     (96, 128, 4, 1, 7, 0.0, "bump"),    # three agent tiles per env, n > 64 lanes, greedy
     (32, 256, 4, 3, 5, 0.1, "bump"),    # configs[4]-like task count (W1 slices through L2)
+    (160, 192, 4, 1, 4, 0.1, "bump"),   # scalar-loaded transition rows in 64 + 64 + 32-agent blocks
 ])
 def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits):
     a, ta, ra = _rollout(n, m, T, L, E, eps, benefits, fused=True)
