@@ -163,6 +163,42 @@ def pmc_lookup(pattern, **match):
     return None
 
 
+def fused_roofline(a, E, fused_ms):
+    """Roofline of the fused rollout kernel (asg_step_select -> rollout_h2_kernel): the env
+    step's bytes plus the agent's h in / h out and the action written -- the observations it
+    generates are consumed on chip, never read back -- per env, times E, over its mean
+    HIP-event time.  `frac` is against HBM; `bound` names what binds, from the kernel's SQ
+    counters when profiled (tools/round_profile.sh): "latency/store-ack" when neither VALU
+    issue nor the MFMA pipe is at half its capacity and HBM is not near its roof (the waves
+    wait on the in-order vmcnt queue behind their own row stores)."""
+    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
+    achieved = per_launch / (fused_ms * 1e-3) / 1e9
+    frac = achieved / HBM_PEAK_GBS
+    pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    issue = None
+    pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L)
+    if pq:
+        c, d = pq["counters"], pq["derived"]
+        issue = {"valu_insts_per_launch": round(c["SQ_INSTS_VALU"]),
+                 "mfma_insts_per_launch": round(c["SQ_INSTS_MFMA"]),
+                 "valu_issue_frac": round(c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_WAVE_INSTR
+                                          / (SIMDS * CLOCK_HZ * fused_ms * 1e-3), 4),
+                 "mfma_busy_frac": round(d["mfma_busy_frac"], 4), "wait_any_frac": round(d["wait_any_frac"], 4),
+                 "pmc": os.path.basename(pq.get("_path", "")) or None}
+    bound = "hbm"
+    if issue and issue["valu_issue_frac"] < 0.5 and issue["mfma_busy_frac"] < 0.5 and frac < 0.6:
+        bound = "latency/store-ack"
+    out = {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(frac, 4), "traffic": pm.get("hbm_bytes_per_launch") if pm else None,
+           "kernel": "asg::rollout_h2_kernel (env step t + agent/eps-greedy t+1)", "kernel_ms": round(fused_ms, 4),
+           "bytes_per_launch": per_launch, "frac_note": "frac is against the 8 TB/s HBM peak"}
+    if pm:
+        out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
+    if issue:
+        out["issue"] = issue
+    return out
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -415,30 +451,14 @@ def main():
     value = G * a.steps / res["elapsed"]
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     if res.get("fused_ms"):
-        # the dominant kernel is the fused rollout step: the env step's bytes plus the agent's
-        # h in / h out and the action written -- its observations are never read back
-        roof_kernel, roof_ms = "asg::rollout_h2_kernel (env step t + agent/eps-greedy t+1)", res["fused_ms"]
-        per_launch = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
-        pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+        roof = fused_roofline(a, E, res["fused_ms"])
     else:
-        roof_kernel, roof_ms = "asg::step_kernel", kern_ms
         per_launch = step_bytes(a.n, a.m, a.L) * E
+        achieved = per_launch / (kern_ms * 1e-3) / 1e9
         pm = pmc_lookup("*pmc_step_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
-    achieved = per_launch / (roof_ms * 1e-3) / 1e9
-    traffic = pm.get("hbm_bytes_per_launch") if pm else None
-    issue = None
-    if res.get("fused_ms"):
-        # the fused kernel is issue/latency-bound rather than HBM-bound: its SQ counters
-        # (tools/pmc_agent_summary.py over the round profile's SQ pass), when profiled
-        pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L)
-        if pq:
-            c, d = pq["counters"], pq["derived"]
-            issue = {"valu_insts_per_launch": round(c["SQ_INSTS_VALU"]),
-                     "mfma_insts_per_launch": round(c["SQ_INSTS_MFMA"]),
-                     "valu_issue_frac": round(c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_WAVE_INSTR
-                                              / (SIMDS * CLOCK_HZ * roof_ms * 1e-3), 4),
-                     "mfma_busy_frac": round(d["mfma_busy_frac"], 4), "wait_any_frac": round(d["wait_any_frac"], 4),
-                     "pmc": os.path.basename(pq.get("_path", "")) or None}
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pm.get("hbm_bytes_per_launch") if pm else None,
+                "kernel": "asg::step_kernel", "kernel_ms": round(kern_ms, 4), "bytes_per_launch": per_launch}
 
     secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))
     extra = {}
@@ -483,6 +503,25 @@ def main():
                 "env_step_ms": round(r3["kern_ms"], 4), "agent_ms": round(agent_ms, 4),
                 "roofline_lsa": lsa_roofline(a, E, r3),
                 "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_h2_kernel (forward only)")}
+        if a.config == 2 and world == 1:
+            # BASELINE configs[4] on this GPU: 256 x 256 dense benefits, 2,048 envs, the same
+            # BasicMAC + RNNAgent + eps-greedy on the fused rollout schedule
+            c4 = argparse.Namespace(**vars(a))
+            for k in ("n", "m", "envs", "benefits"):
+                setattr(c4, k, CONFIGS[4][k])
+            c4.config = 4
+            r5 = run_leg(c4, dev, world, c4.envs, sk, sw)
+            leg = {"value": round(r5["global_envs"] * sk / r5["elapsed"], 1), "unit": "env-steps/s",
+                   "ms_per_step": round(r5["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                   "workload": CONFIGS[4]["label"] + f"; T={a.T}, L={a.L}, BasicMAC+rnn_fused(GRU 64, fp32) + "
+                                                     "epsilon-greedy 0.05, dense benefits",
+                   "envs_per_gpu": c4.envs, "n": c4.n, "m": c4.m,
+                   "kernels_ms": {"fused_step_select": round(r5["fused_ms"], 4) if r5.get("fused_ms") else None,
+                                  "env_step": round(r5["kern_ms"], 4) if r5["kern_ms"] else None,
+                                  "select": round(r5["sel_ms"], 4) if r5["sel_ms"] else None}}
+            if r5.get("fused_ms"):
+                leg["roofline"] = fused_roofline(c4, c4.envs, r5["fused_ms"])
+            extra["config4"] = leg
 
     if a.selector == "random":
         ra = None
@@ -510,10 +549,7 @@ def main():
                        "baseline_config_index": 3 if (a.config == 2 and world > 1) else a.config,
                        "envs_per_gpu": E, "global_envs": G, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
                        "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": roof_kernel, "kernel_ms": round(roof_ms, 4),
-                         "bytes_per_launch": per_launch, **({"issue": issue} if issue else {})},
+            "roofline": roof,
             "kernels_ms": {"fused_step_select": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
                            "env_step": round(kern_ms, 4) if kern_ms else None,
                            "select": round(sel_ms, 4) if sel_ms else None,

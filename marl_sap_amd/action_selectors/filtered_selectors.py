@@ -101,13 +101,16 @@ class _FilteredBase:
                 _p(self.status), _lib.stream_ptr(mat.device)))
         return out
 
+    # the message of this selector's device status word (ASG_E_INVALID_ARG)
+    status_message = "epsilon-greedy exploration over a row with no available action"
+
     def flush(self):
         """Raise (once per episode, from the runner) on a deferred device error."""
         if isinstance(getattr(self, "lsa_status", None), DeferredStatus):
             self.lsa_status.flush()
         if self.status is not None and int(self.status.item()) != 0:
             self.status.zero_()
-            raise ValueError("epsilon-greedy exploration over a row with no available action")
+            raise ValueError(self.status_message)
 
 
 class FilteredSAPActionSelector(_FilteredBase):
@@ -174,6 +177,8 @@ class FilteredSoftPoliciesSelector(_FilteredBase):
     """filtered_classic_selectors.py:69-103: sample an index from the M + 1 policy values
     (Categorical), then map it to a task: the index-th top task, or for index M a uniformly
     random task outside the top M (int64)."""
+
+    status_message = "soft-policies selection picked an index outside [0, M] (policy over M + 1 outputs expected)"
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None):
         assert beta is not None, "Need beta to figure out which are the top M tasks for each agent."

@@ -470,19 +470,13 @@ int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int6
     if (B == 0) return ASG_OK;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     const bool gauss = gauss_noise != nullptr || gauss_epsilon > 0.0;
-    double *rowabs = nullptr;
-    hipError_t e = hipSuccess;
-    if (gauss && !gauss_noise) e = hipMallocAsync(reinterpret_cast<void **>(&rowabs), sizeof(double) * B * n, s);
-    if (e == hipSuccess)
-        e = asg::launch_filtered_matrix(q, q_strides, topm, B, n, m, M, tie_noise, seed, (uint32_t)counter,
-                                        env_index_base, mat_out, rowabs, s);
+    if (gauss && !gauss_noise && (size_t)n * sizeof(double) > 64 * 1024)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: n > 8192 agents with Gaussian noise");
+    hipError_t e = asg::launch_filtered_matrix(q, q_strides, topm, B, n, m, M, tie_noise, seed, (uint32_t)counter,
+                                               env_index_base, mat_out, nullptr, s);
     if (e == hipSuccess && gauss)
-        e = asg::launch_filtered_gauss(mat_out, rowabs, B, n, m, (float)gauss_epsilon, gauss_noise, seed,
-                                       (uint32_t)counter, env_index_base, s);
-    if (rowabs) {
-        const hipError_t e2 = hipFreeAsync(rowabs, s);
-        if (e == hipSuccess) e = e2;
-    }
+        e = asg::launch_filtered_gauss(mat_out, B, n, m, (float)gauss_epsilon, gauss_noise, seed, (uint32_t)counter,
+                                       env_index_base, s);
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_benefits");
 }
 

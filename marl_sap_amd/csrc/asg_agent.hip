@@ -1989,6 +1989,13 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
 // are bit-identical to step_kernel + rnn_agent_h2_kernel (same bump arithmetic, per-tile fc1
 // scale, slice order and tail).
 // =====================================================================================
+// The A/B switches below (NOSTORE / SKIP: timing-only builds with WRONG results; EARLY 1|2 and
+// NT: slower variants kept for the record) are refused unless the build says
+// it is a timing experiment: the product library never carries them.
+#if !defined(ASG_TIMING_EXPERIMENTS) && (defined(ASG_ROLLOUT_NOSTORE) || defined(ASG_ROLLOUT_SKIP) || \
+                                         defined(ASG_ROLLOUT_EARLY) || defined(ASG_ROLLOUT_NT))
+#error "rollout A/B switches (some give wrong results) need -DASG_TIMING_EXPERIMENTS"
+#endif
 // timing experiments only: skip the observation / one-hot / avail / beta stores (wrong batch)
 #ifndef ASG_ROLLOUT_NOSTORE
 #define ASG_ROLLOUT_NOSTORE 0

@@ -161,10 +161,14 @@ __global__ void __launch_bounds__(256) filtered_matrix_kernel(const float *q, in
 // FilteredSAPActionSelector exploration: per env, std = float32(float32(mean|mat| * eps) * 2)
 // and mat += N(0, std^2) (Philox Box-Muller), or mat += the given noise.  One workgroup per
 // env.
-__global__ void __launch_bounds__(256) filtered_gauss_kernel(float *mat, const double *rowabs, int n, int m,
-                                                             float epsilon, const float *gauss, uint64_t seed,
-                                                             uint32_t counter, int64_t env_base) {
+// The per-row float64 sums of |mat| are formed here (a wave per row, lane j-strided then a
+// wave sum: the association filtered_matrix_kernel uses) into LDS, so the selection needs no
+// scratch buffer in HBM.
+__global__ void __launch_bounds__(256) filtered_gauss_kernel(float *mat, int n, int m, float epsilon,
+                                                             const float *gauss, uint64_t seed, uint32_t counter,
+                                                             int64_t env_base) {
     __shared__ double s_part[4];
+    extern __shared__ double s_rowabs[];  // [n]
     const int64_t b = blockIdx.x;
     const int64_t nm = (int64_t)n * m;
     float *mb = mat + b * nm;
@@ -173,8 +177,18 @@ __global__ void __launch_bounds__(256) filtered_gauss_kernel(float *mat, const d
         for (int64_t x = threadIdx.x; x < nm; x += blockDim.x) mb[x] = mb[x] + g[x];
         return;
     }
+    {
+        const int lane = threadIdx.x & 63;
+        for (int i = threadIdx.x >> 6; i < n; i += (int)(blockDim.x >> 6)) {
+            double ra = 0.0;
+            for (int j = lane; j < m; j += 64) ra += (double)__builtin_fabsf(mb[(int64_t)i * m + j]);
+            ra = wave_allreduce(ra, [](double a, double c) { return a + c; });
+            if (lane == 0) s_rowabs[i] = ra;
+        }
+    }
+    __syncthreads();
     double acc = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += rowabs[b * n + i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += s_rowabs[i];
     acc = wave_allreduce(acc, [](double a, double c) { return a + c; });
     if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -272,10 +286,10 @@ hipError_t launch_filtered_matrix(const float *q, const int64_t qs[3], const int
     return hipGetLastError();
 }
 
-hipError_t launch_filtered_gauss(float *mat, const double *rowabs, int64_t B, int n, int m, float epsilon,
-                                 const float *gauss, uint64_t seed, uint32_t counter, int64_t env_base, hipStream_t s) {
-    hipLaunchKernelGGL(filtered_gauss_kernel, dim3((unsigned)B), dim3(256), 0, s, mat, rowabs, n, m, epsilon, gauss,
-                       seed, counter, env_base);
+hipError_t launch_filtered_gauss(float *mat, int64_t B, int n, int m, float epsilon, const float *gauss,
+                                 uint64_t seed, uint32_t counter, int64_t env_base, hipStream_t s) {
+    hipLaunchKernelGGL(filtered_gauss_kernel, dim3((unsigned)B), dim3(256), sizeof(double) * n, s, mat, n, m, epsilon,
+                       gauss, seed, counter, env_base);
     return hipGetLastError();
 }
 

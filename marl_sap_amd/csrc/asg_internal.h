@@ -83,8 +83,8 @@ hipError_t launch_filtered_topm(const void *beta, int dtype, const int64_t bs[4]
 hipError_t launch_filtered_matrix(const float *q, const int64_t qs[3], const int64_t *topm, int64_t B, int n, int m,
                                   int M, const float *tie, uint64_t seed, uint32_t counter, int64_t env_base,
                                   float *mat, double *rowabs, hipStream_t s);
-hipError_t launch_filtered_gauss(float *mat, const double *rowabs, int64_t B, int n, int m, float epsilon,
-                                 const float *gauss, uint64_t seed, uint32_t counter, int64_t env_base, hipStream_t s);
+hipError_t launch_filtered_gauss(float *mat, int64_t B, int n, int m, float epsilon, const float *gauss,
+                                 uint64_t seed, uint32_t counter, int64_t env_base, hipStream_t s);
 hipError_t launch_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B, int n, int m, int M,
                                     uint64_t seed, uint32_t counter, int64_t env_base, int64_t *out, int *err,
                                     hipStream_t s);

@@ -619,6 +619,12 @@ __global__ void __launch_bounds__(256) haal_matrix_kernel(RealState st, int k, H
     const int prev = par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i];
     const double *tab = st.table + e * st.table_env_stride;
     double *row = mats + gr * m;
+    if (prev < 0 || prev >= m) {
+        // the parent node's LSA failed (its assignment is -1 rows): poison this row so the
+        // node's LSA reports invalid entries too, never index T_trans with it
+        for (int j = lane; j < m; j += 64) row[j] = __builtin_nan("");
+        return;
+    }
     for (int j = lane; j < m; j += 64) {
         double s = real_beta(st, tab, k + t, i, j, 0);
         const double b0 = s;
@@ -652,13 +658,22 @@ __global__ void __launch_bounds__(256) haal_values_kernel(RealState st, int k, H
         for (int t = t0; t <= t1; ++t) {
             for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
             __syncthreads();
-            for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[(int)A[i]], 1);
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int c = (int)A[i];
+                if (c >= 0 && c < m) atomicAdd(&scnt[c], 1);
+            }
             __syncthreads();
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
                 // the previous assignment: the parent's on the interval's first step, then A
                 const int p = t > t0 ? (int)A[i]
                                      : (par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i]);
                 const int c = (int)A[i];
+                if (c < 0 || c >= m || p < 0 || p >= m) {
+                    // a failed LSA upstream (-1 assignment rows): the sequence's value is NaN
+                    // and the env's status carries the LSA error
+                    s_rew[i] = __builtin_nan("");
+                    continue;
+                }
                 double sum = real_beta(st, tab, k + t, i, c, 0);
                 const double b0 = sum;
                 for (int l = 1; l < st.L; ++l) sum = sum + real_beta(st, tab, k + t, i, c, l);

@@ -1,7 +1,13 @@
 """Multi-GPU plumbing: one process per GPU under torch.distributed (backend "nccl" is
 RCCL on ROCm; "gloo" for CPU tests).  Envs are independent, so nothing is exchanged per
-step; once per episode the float64 returns are all-gathered (env order = global env
-index) and the env-step counter is all-reduced."""
+step.  The per-rank env counts are all-gathered once, at runner construction (the
+env-step counter of an episode is then T * sum_r E_r on every rank with no per-episode
+collective), and once per episode the float64 returns are all-gathered in global env
+order (reference runners/parallel_runner.py:173-179, :220-221).
+
+Every collective here runs whenever a process group is initialised, world size 1
+included, so a one-rank RCCL job (`init_from_env(force=True)`) executes the same
+device-tensor all-gathers and barrier as an 8-GPU one."""
 import os
 
 import torch
@@ -14,9 +20,14 @@ def rank_world():
     return 0, 1
 
 
-def init_from_env(backend=None):
-    """Initialise the default process group from torchrun's env vars (no-op for 1 rank)."""
-    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or (dist.is_available() and dist.is_initialized()):
+def _initialized():
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_from_env(backend=None, force=False):
+    """Initialise the default process group from torchrun's env vars (no-op for 1 rank
+    unless `force`: a one-rank group runs the real collectives, e.g. an RCCL rehearsal)."""
+    if (int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not force) or _initialized():
         return rank_world()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend is None:
@@ -40,9 +51,9 @@ def all_gather_returns(local, counts=None):
     """[E_r] per-rank returns -> [sum_r E_r] in global env order.  counts: every rank's
     E_r (from envs_per_rank); equal counts (the sharded rollout) take one
     all_gather_into_tensor, ragged ones are padded to the largest shard and stripped."""
-    rank, world = rank_world()
-    if world == 1:
+    if not _initialized():
         return local
+    rank, world = rank_world()
     if dist.get_backend() == "gloo" and local.is_cuda:
         local = local.cpu()
     local = local.contiguous()
@@ -62,9 +73,9 @@ def envs_per_rank(local_envs):
     """Every rank's env count (one all-gather at runner construction): the env-step
     counter of an episode is T * sum(E_r), the reference's per-env accounting
     (parallel_runner.py:178-179, :220-221) summed over ranks."""
-    rank, world = rank_world()
-    if world == 1:
+    if not _initialized():
         return [int(local_envs)]
+    rank, world = rank_world()
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([int(local_envs)], dtype=torch.int64, device=dev)
     out = torch.empty(world, dtype=torch.int64, device=dev)
@@ -78,8 +89,7 @@ def env_index_base(counts, rank):
 
 
 def all_reduce_sum(value):
-    rank, world = rank_world()
-    if world == 1:
+    if not _initialized():
         return int(value)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
@@ -88,7 +98,7 @@ def all_reduce_sum(value):
 
 
 def barrier():
-    if rank_world()[1] > 1:
+    if _initialized():
         if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:

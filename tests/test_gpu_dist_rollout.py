@@ -30,7 +30,7 @@ def _free_port():
     return p
 
 
-def _launch(tmp, counts, eps, selector, episodes=2, tag="run"):
+def _launch(tmp, counts, eps, selector, episodes=2, tag="run", extra=(), timeout=100):
     world = len(counts)
     port = _free_port()
     procs, outs = [], []
@@ -40,12 +40,12 @@ def _launch(tmp, counts, eps, selector, episodes=2, tag="run"):
         out = os.path.join(tmp, f"{tag}_w{world}_r{r}.pt")
         outs.append(out)
         procs.append(subprocess.Popen(
-            [sys.executable, WORKER, out, ",".join(map(str, counts)), str(eps), selector, str(episodes)],
+            [sys.executable, WORKER, out, ",".join(map(str, counts)), str(eps), selector, str(episodes), *extra],
             env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=100)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -97,3 +97,36 @@ def test_bench_multi_rank_branch(tmp_path):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 512 and line["value"] > 0
     assert line["scaling"] == "weak" and line["cpu_baseline"] is None
+
+
+def test_configs3_per_rank_size_and_rccl_rehearsal(tmp_path):
+    """BASELINE configs[3] at its real per-rank size: 64 x 64 envs, 16,384 per rank, two ranks
+    (gloo; two processes on the one GPU of the test box, 2 x 41 GB of batch shards) against a
+    one-rank run over the same 32,768 global envs on an RCCL group (backend "nccl", world 1:
+    init_process_group(device_id=...), device-tensor all_gather_into_tensor of the env counts
+    and the returns, barrier(device_ids=...) -- the code path an 8-GPU node runs).  The
+    gathered float64 returns are bitwise equal, every (env, field) checksum of the shards
+    equals the one-rank batch's, and sampled env rows are equal.  Both schedules run the fused
+    rollout kernel.  Reference: runners/parallel_runner.py:173-179, :220-221."""
+    E = 16384
+    sample = [0, E - 1, E, E + 4097, 2 * E - 1]
+    common = ["--n", "64", "--m", "64", "--T", "20", "--checksums", "--sample", ",".join(map(str, sample))]
+    (one,) = _launch(str(tmp_path), [2 * E], 0.05, "epsilon_greedy", episodes=1, tag="one",
+                     extra=["--backend", "nccl", *common], timeout=300)
+    assert one["backend"] == "nccl" and one["world"] == 1 and one["fused"]
+    shards = _launch(str(tmp_path), [E, E], 0.05, "epsilon_greedy", episodes=1, tag="two",
+                     extra=["--backend", "gloo", *common], timeout=300)
+    assert one["t_env"] == [2 * E * 20]
+    for r, sh in enumerate(shards):
+        assert sh["backend"] == "gloo" and sh["world"] == 2 and sh["fused"]
+        assert sh["env_index_base"] == r * E and sh["rank_envs"] == [E, E]
+        assert sh["t_env"] == one["t_env"]
+        assert torch.equal(sh["returns"][0], one["returns"][0])  # gathered returns, bitwise
+        for k, c in one["checksums"].items():
+            assert torch.equal(sh["checksums"][k], c[r * E:(r + 1) * E]), k
+        for g, rows in sh["sample"].items():
+            for k, v in rows.items():
+                assert torch.equal(v, one["sample"][g][k]), (g, k)
+    assert sum(len(sh["sample"]) for sh in shards) == len(sample)
+    # the rollout really explored and the envs differ (global keying)
+    assert not torch.equal(one["checksums"]["actions"][:E], one["checksums"]["actions"][E:])

@@ -221,6 +221,46 @@ def test_haal_vs_oracle_through_an_episode(oracle, n, m, T, L):
     env.close()
 
 
+def test_haal_nan_benefits_report_status_without_fault():
+    """A NaN benefit makes the root LSA of that env fail (scipy: "matrix contains invalid
+    numeric entries"); its -1 assignment rows must not be used as indices by the tree's
+    child matrices or the sequence values (they are poisoned with NaN instead).  The failing
+    env reports its status, the selector raises scipy's ValueError on flush, and the other
+    envs' actions equal a NaN-free run."""
+    E, n, m, T, L = 3, 6, 9, 5, 4
+    rng = np.random.RandomState(5)
+    tables = rng.uniform(0.0, 1.0, size=(E, n, m, T))
+    bad = tables.copy()
+    bad[1, 2, 4, 1] = np.nan    # seen by the root node's L-summed benefit
+    bad[2, 0, :, 4] = -np.inf   # outside the root's window (times 0-3): a child node's LSA fails
+    #                             (agent 0 has no finite task: infeasible) and its -1 rows feed
+    #                             the grandchildren's matrices and the sequence values
+
+    def run(tab):
+        env = RealAssignEnvBatch(1, n, m, T, 2, 2, L, 0.4, sat_prox_mat=tab, num_envs=E, device=DEV)
+        b = EpisodeBatch(env.scheme, {"agents": n}, E, T + 1, preprocess=env.preprocess, device=DEV,
+                         time_major=True)
+        env.reset(b, 0)
+        out, values, best, status = env.haal_select(return_values=True)
+        env.sync()
+        res = out.cpu(), status.cpu(), values.cpu()
+        env.close()
+        return res
+
+    out_ok, st_ok, _ = run(tables)
+    out_bad, st_bad, val_bad = run(bad)
+    assert int(st_ok.abs().max()) == 0
+    assert int(st_bad[0]) == 0 and int(st_bad[1]) != 0 and int(st_bad[2]) != 0
+    assert torch.equal(out_bad[0], out_ok[0])
+    assert bool((out_bad[1] == -1).all())
+    from marl_sap_amd.action_selectors.lsa import DeferredStatus
+    ds = DeferredStatus()
+    ds.add(st_bad[:2].to(DEV))
+    with pytest.raises(ValueError, match="invalid numeric entries"):
+        ds.flush()
+    assert int(st_bad[2]) == -5  # ASG_E_LSA_INFEASIBLE
+
+
 # ---------------------------------------------------------------------------------------
 @pytest.mark.parametrize("selector,agent", [("filtered_const_epsgr_sap_test", "flat_const_agent_fused"),
                                             ("filtered_const_sap", "flat_const_agent"),

@@ -57,6 +57,7 @@ def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protoco
     (96, 128, 4, 1, 7, 0.0, "bump"),    # three agent tiles per env, n > 64 lanes, greedy
     (32, 256, 4, 3, 5, 0.1, "bump"),    # configs[4]-like task count (W1 slices through L2)
     (160, 192, 4, 1, 4, 0.1, "bump"),   # scalar-loaded transition rows in 64 + 64 + 32-agent blocks
+    (256, 256, 4, 3, 6, 0.05, "dense"),  # the configs[4] shape (256 x 256 dense, L = 3)
 ])
 def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits):
     a, ta, ra = _rollout(n, m, T, L, E, eps, benefits, fused=True)
