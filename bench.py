@@ -163,25 +163,27 @@ def pmc_lookup(pattern, **match):
     return None
 
 
-def fused_roofline(a, E, fused_ms):
-    """Roofline of the fused rollout kernel (asg_step_select -> rollout_h2_kernel): the env
-    step's bytes plus the agent's h in / h out and the action written -- the observations it
-    generates are consumed on chip, never read back -- per env, times E, over its mean
-    HIP-event time.  `frac` is against HBM; `bound` names what binds, from the kernel's SQ
-    counters when profiled (tools/round_profile.sh): "latency/store-ack" when neither VALU
-    issue nor the MFMA pipe is at half its capacity and HBM is not near its roof (the waves
-    wait on the in-order vmcnt queue behind their own row stores)."""
-    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
+def fused_roofline(a, E, fused_ms, use_rnn=True):
+    """Roofline of the fused rollout kernel (asg_rollout -> rollout_kernel), per env step: the
+    env step's bytes plus the agent's h in / h out and the action written -- the observations
+    it generates are consumed on chip, never read back -- per env, times E, over its HIP-event
+    time per step (a launch of s steps counts s).  Linear agent (use_rnn False): no h read.
+    `frac` is against HBM; `bound` names what binds, from the kernel's SQ counters when
+    profiled (tools/round_profile.sh): "latency/store-ack" when neither VALU issue nor the
+    MFMA pipe is at half its capacity and HBM is not near its roof (the waves wait on the
+    in-order vmcnt queue behind their own row stores)."""
+    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)) * E
     achieved = per_launch / (fused_ms * 1e-3) / 1e9
     frac = achieved / HBM_PEAK_GBS
-    pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L)
+    pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     issue = None
-    pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L)
+    pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     if pq:
         c, d = pq["counters"], pq["derived"]
-        issue = {"valu_insts_per_launch": round(c["SQ_INSTS_VALU"]),
-                 "mfma_insts_per_launch": round(c["SQ_INSTS_MFMA"]),
-                 "valu_issue_frac": round(c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_WAVE_INSTR
+        spl = pq.get("steps_per_launch", 1)  # the profiled launches ran spl steps each
+        issue = {"valu_insts_per_step": round(c["SQ_INSTS_VALU"] / spl),
+                 "mfma_insts_per_step": round(c["SQ_INSTS_MFMA"] / spl),
+                 "valu_issue_frac": round(c["SQ_INSTS_VALU"] / spl * VALU_CYCLES_PER_WAVE_INSTR
                                           / (SIMDS * CLOCK_HZ * fused_ms * 1e-3), 4),
                  "mfma_busy_frac": round(d["mfma_busy_frac"], 4), "wait_any_frac": round(d["wait_any_frac"], 4),
                  "pmc": os.path.basename(pq.get("_path", "")) or None}
@@ -189,9 +191,12 @@ def fused_roofline(a, E, fused_ms):
     if issue and issue["valu_issue_frac"] < 0.5 and issue["mfma_busy_frac"] < 0.5 and frac < 0.6:
         bound = "latency/store-ack"
     out = {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(frac, 4), "traffic": pm.get("hbm_bytes_per_launch") if pm else None,
-           "kernel": "asg::rollout_h2_kernel (env step t + agent/eps-greedy t+1)", "kernel_ms": round(fused_ms, 4),
-           "bytes_per_launch": per_launch, "frac_note": "frac is against the 8 TB/s HBM peak"}
+           "frac": round(frac, 4),
+           "traffic": round(pm["hbm_bytes_per_launch"] / pm.get("steps_per_launch", 1)) if pm else None,
+           "kernel": "asg::rollout_kernel (env steps + agent/eps-greedy selections, per step)",
+           "kernel_ms": round(fused_ms, 4), "bytes_per_launch": per_launch,
+           "per_launch_note": "per env step of the launch (bytes_per_launch, kernel_ms: one step's share)",
+           "frac_note": "frac is against the 8 TB/s HBM peak"}
     if pm:
         out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
     if issue:
@@ -221,9 +226,11 @@ def parse(argv=None):
                    help=f"CPU-baseline env workers (default min(os.cpu_count(), {CPU_WORKER_CAP}))")
     p.add_argument("--secondary", type=int, default=-1, help="secondary legs (-1: on at N = 1 for configs 2/3)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--fused-rollout", type=int, default=1, choices=[0, 1, 2],
-                   help="1 (default): env step t + agent/eps-greedy t+1 in one kernel (asg_step_select) where the env "
-                        "reports it faster; 2: wherever it applies; 0: separate asg_step + agent select launches")
+    p.add_argument("--fused-rollout", type=int, default=1, choices=[0, 1, 2, 3],
+                   help="1 (default): the whole episode -- env steps + agent/eps-greedy selections -- in one kernel "
+                        "(asg_rollout); 3: one asg_rollout launch per step (env step t + selection t + 1); 0: separate "
+                        "asg_step + agent select launches; 2: as 1")
+    p.add_argument("--use-rnn", type=int, default=1, help="0: the Linear + ReLU RNNAgent (use_rnn: False)")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -232,20 +239,24 @@ def parse(argv=None):
     return a
 
 
-def make_args(a, E, selector=None, agent=None, fused=None):
+def make_args(a, E, selector=None, agent=None, fused=None, mac="basic_mac", use_rnn=None, **extra):
     selector = selector or a.selector
     fused = a.fused_rollout if fused is None else fused
     sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy"}[selector]
-    return SimpleNamespace(
+    args = SimpleNamespace(
         batch_size_run=E, env="mock_constellation_env",
         env_args=dict(n=a.n, m=a.m, T=a.T, L=a.L, lambda_=0.5, bids_as_actions=False, seed=a.seed,
                       benefits=a.benefits),
         env_rng="philox", env_quirks=(), runner_protocol="episode", test_nepisode=1,
-        runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, hidden_dim=64, use_rnn=True,
+        runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, hidden_dim=64,
+        use_rnn=bool(a.use_rnn if use_rnn is None else use_rnn),
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
         agent=agent or a.agent, seed=a.seed,
-        epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac="basic_mac",
-        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always"}[fused])
+        epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac=mac,
+        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always", 3: "step"}[fused])
+    for k, v in extra.items():
+        setattr(args, k, v)
+    return args
 
 
 class NullLogger:
@@ -282,7 +293,8 @@ def cpu_baseline(a):
                                                      f"(oracle/asg_rollout.c), no agent network"}}
 
 
-def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_lsa=False, fused=None):
+def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_lsa=False, fused=None, mac="basic_mac",
+            use_rnn=None, **extra):
     """Build runner + MAC for one workload and time `steps` transitions after `warmup`.
     Returns elapsed seconds (max over ranks) and mean HIP-event times of the env step, the
     whole selection, and (SAP) the selector kernel alone."""
@@ -291,11 +303,11 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     from marl_sap_amd.runners import REGISTRY as r_REGISTRY
 
     selector = selector or a.selector
-    args = make_args(a, E, selector, agent, fused)
+    args = make_args(a, E, selector, agent, fused, mac=mac, use_rnn=use_rnn, **extra)
     runner = r_REGISTRY["gpu"](args, NullLogger())
     env = runner.get_env()
     torch.manual_seed(a.seed)  # identical agent weights on every rank
-    mac = mac_REGISTRY["basic_mac"](env.scheme, {"agents": a.n}, args)
+    mac = mac_REGISTRY[mac](env.scheme, {"agents": a.n}, args)
     mac.to(dev)
     runner.setup(env.scheme, {"agents": a.n}, env.preprocess, mac)
 
@@ -311,43 +323,61 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         e0.record()
         out = inner(*args_, **kw)
         e1.record()
-        lsa_pairs.append((e0, e1))
+        lsa_pairs.append((e0, e1, 1))
         return out
 
     if selector == "sap":
         sel_obj.select_action = timed_select
 
-    # the runner's schedule (GpuVecRunner.rollout): with the fused agent + epsilon-greedy, env.step(t)
-    # and the selection for t + 1 are one kernel (asg_step_select) for t < T - 1; the first selection
-    # of an episode and its last step are the separate kernels.  Either way one "step" = one env
-    # transition plus one selection (over an episode: T of each).
+    # the runner's schedule (GpuVecRunner.rollout).  mode "episode" (the default with the fused
+    # agent + epsilon-greedy): asg_rollout -- select(0); for t: env.step(t), select(t + 1) -- as one
+    # kernel; here it is launched per chunk of steps so that exactly `steps` transitions fall in
+    # the timed region (a chunk that stops inside an episode also selects the row after it; the
+    # runner itself launches whole episodes).  mode "step": env.step(t) + select(t + 1) fused per
+    # step (asg_step_select), the episode's first selection and last step separate.  None:
+    # separate env-step and selection launches.  Either way one "step" = one env transition plus
+    # one selection (over an episode: T of each).
     fused_pairs = []
     state["selected"] = False
 
+    def timed(pairs, fn, w=1):
+        if not state["timing"]:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        pairs.append((e0, e1, w))
+
+    def new_episode():
+        if runner.batch is not None and runner.env.k == a.T:
+            runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
+        runner.reset()
+        mac.init_hidden(E)
+        state["t"] = 0
+        state["selected"] = False
+        # planned per episode, as GpuVecRunner.rollout does (JumpstartMAC draws its flips here)
+        with torch.no_grad():
+            state["mode"] = None if selector == "random" else mac.fused_mode(env, runner.batch, runner.t_env)
+
+    def advance(s_):
+        """s_ transitions (+ their selections) of the current episode in one asg_rollout launch"""
+        t = state["t"]
+        sf, sl = t == 0, t + s_ < a.T
+        with torch.no_grad():
+            eps, seed, counter, status, _ = mac.action_selector.fused_params(runner.t_env, False, dev,
+                                                                             calls=s_ + sf + sl - 1)
+
+            def launch():
+                mac.hidden_states = env.rollout(runner.batch, t, s_, mac.selector_agent, mac.hidden_states, eps, seed,
+                                                counter, status, select_first=sf, select_last=sl)
+            timed(fused_pairs, launch, s_)
+        state["t"] = t + s_
+
     def one_step():
-        if state["t"] >= a.T:
-            if runner.batch is not None and runner.env.k == a.T:
-                runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
-            runner.reset()
-            mac.init_hidden(E)
-            state["t"] = 0
-            state["selected"] = False
         t = state["t"]
         with torch.no_grad():
-            timing = state["timing"]
-            if "fused" not in state:
-                state["fused"] = selector != "random" and mac.fused_step_ok(env, runner.batch)
-            fused = state["fused"]
-
-            def timed(pairs, fn):
-                if not timing:
-                    return fn()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                fn()
-                e1.record()
-                pairs.append((e0, e1))
-
+            fused = state["mode"] == "step"
             if selector == "random":
                 timed(sel_pairs, lambda: env.random_actions(runner.batch, ts=t))
             elif not state["selected"]:
@@ -360,14 +390,26 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
                 state["selected"] = False
         state["t"] = t + 1
 
-    for _ in range(warmup):
-        one_step()
+    def run_steps(k):
+        while k > 0:
+            if state["t"] >= a.T:
+                new_episode()
+            if state["mode"] == "episode":
+                s_ = min(k, a.T - state["t"])
+                advance(s_)
+                k -= s_
+            else:
+                one_step()
+                k -= 1
+
+    tw = time.perf_counter()
+    run_steps(warmup)
     asg_dist.barrier()
     torch.cuda.synchronize()
+    warm_elapsed = time.perf_counter() - tw
     state["timing"] = True
     t0 = time.perf_counter()
-    for _ in range(steps):
-        one_step()
+    run_steps(steps)
     torch.cuda.synchronize()
     asg_dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -375,10 +417,12 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     if runner.env.k == a.T:
         runner.finish_episode(sync=False)
     runner.flush_pending()  # surfaces any sticky device error of the timed steps
-    mean = lambda prs: sum(s.elapsed_time(e) for s, e in prs) / len(prs) if prs else 0.0  # noqa: E731
-    res = {"elapsed": elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
+    # mean HIP-event time per step (a launch of w steps counts w)
+    mean = lambda prs: sum(p[0].elapsed_time(p[1]) for p in prs) / sum(p[2] for p in prs) if prs else 0.0  # noqa
+    res = {"elapsed": elapsed, "warmup_elapsed": warm_elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
            "lsa_ms": mean(lsa_pairs) if lsa_pairs else None,
-           "fused_ms": mean(fused_pairs) if fused_pairs else None, "fused": bool(state.get("fused"))}
+           "fused_ms": mean(fused_pairs) if fused_pairs else None, "mode": state.get("mode"),
+           "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs)}
     if count_lsa and selector == "sap" and a.n <= a.m <= 64:
         # one more selection on the current state, with the step-counting kernel instance
         sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
@@ -462,47 +506,72 @@ def main():
 
     secondary = a.secondary if a.secondary >= 0 else int(world == 1 and a.config in (2, 3))
     extra = {}
+
+    def leg_base(r, sk, sw):
+        return {"value": round(r["global_envs"] * sk / r["elapsed"], 1), "unit": "env-steps/s",
+                "ms_per_step": round(r["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                "schedule": r.get("mode") or "split"}
+
     if secondary:
         sk, sw = max(10, a.steps // 2), max(5, a.warmup // 2)
         if a.selector != "random":
             r2 = run_leg(a, dev, world, E, sk, sw, selector="eps", agent="rnn")
             extra["pytorch_agent"] = {
-                "value": round(r2["global_envs"] * sk / r2["elapsed"], 1), "unit": "env-steps/s",
-                "ms_per_step": round(r2["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                **leg_base(r2, sk, sw),
                 "what": "configs[2] read literally: BasicMAC + the PyTorch RNNAgent module (hipBLASLt linears + "
                         "GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
                 "select_ms": round(r2["sel_ms"], 4), "env_step_ms": round(r2["kern_ms"], 4)}
         if a.selector == "eps" and a.agent == "rnn_fused":
-            # the other schedule of the same workload: split launches when the headline fused them
-            # (or the fused kernel when the headline ran split)
-            other = 0 if res.get("fused_ms") else 1
-            r4 = run_leg(a, dev, world, E, sk, sw, fused=other)
-            leg = {"value": round(r4["global_envs"] * sk / r4["elapsed"], 1), "unit": "env-steps/s",
-                   "ms_per_step": round(r4["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
-                   "env_step_ms": round(r4["kern_ms"], 4) if r4["kern_ms"] else None,
-                   "select_ms": round(r4["sel_ms"], 4) if r4["sel_ms"] else None}
-            if r4.get("fused_ms"):
-                fb = (step_bytes(a.n, a.m, a.L) + a.n * (2 * 4 * 64 + 8)) * E
-                leg.update({"what": "same workload with --fused-rollout 1: asg_step_select (env step t + agent "
-                                    "forward + eps-greedy for t + 1 in one kernel) for T - 1 of T steps",
-                            "fused_step_select_ms": round(r4["fused_ms"], 4),
-                            "hbm_achieved_gbs": round(fb / (r4["fused_ms"] * 1e-3) / 1e9, 1), "bytes_per_launch": fb})
-                extra["fused_rollout"] = leg
-            elif other == 0:
-                leg["what"] = ("same workload with --fused-rollout 0: asg_step then the fused agent forward + "
-                               "eps-greedy kernel (rnn_agent_h2_kernel), one launch each per step")
-                extra["split_rollout"] = leg
+            # the other schedules of the same workload: one fused launch per step, and separate
+            # env-step + agent launches
+            r4 = run_leg(a, dev, world, E, sk, sw, fused=3)
+            extra["step_rollout"] = {
+                **leg_base(r4, sk, sw), "fused_step_select_ms": round(r4["fused_ms"], 4) if r4["fused_ms"] else None,
+                "env_step_ms": round(r4["kern_ms"], 4) if r4["kern_ms"] else None,
+                "select_ms": round(r4["sel_ms"], 4) if r4["sel_ms"] else None,
+                "what": "same workload, asg_rollout launched per step (env step t + agent forward + eps-greedy for "
+                        "t + 1) for T - 1 of T steps, the episode's first selection and last step separate"}
+            r6 = run_leg(a, dev, world, E, sk, sw, fused=0)
+            extra["split_rollout"] = {
+                **leg_base(r6, sk, sw), "env_step_ms": round(r6["kern_ms"], 4), "select_ms": round(r6["sel_ms"], 4),
+                "what": "same workload with --fused-rollout 0: asg_step then the fused agent forward + eps-greedy "
+                        "kernel (rnn_agent_h2_kernel), one launch each per step"}
         if a.n <= a.m <= 64 and a.selector != "sap":
             r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn_fused", count_lsa=True)
             agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)
             extra["sap"] = {
-                "value": round(r3["global_envs"] * sk / r3["elapsed"], 1), "unit": "env-steps/s",
-                "ms_per_step": round(r3["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+                **leg_base(r3, sk, sw),
                 "what": "SequentialAssignmentProblemSelector (eps 0.05): fused RNNAgent forward kernel, then "
                         "asg_sap_select (per-env Gaussian noise + scipy-exact LSA, one wave64 per env)",
                 "env_step_ms": round(r3["kern_ms"], 4), "agent_ms": round(agent_ms, 4),
                 "roofline_lsa": lsa_roofline(a, E, r3),
                 "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_h2_kernel (forward only)")}
+        if a.config == 2 and world == 1 and a.selector == "eps":
+            # the reference's own algorithms for this env (config/algs/mock_constellation_*.yaml):
+            # jumpstart_mac with the HAA jumpstart selector, use_rnn: False (Linear + ReLU agent),
+            # jumpstart epsilon 1 -> 0 over 20,000 env steps -- one 16,384-env episode is 327,680
+            # env steps, so the warmup episode is the jumpstart (HAA) phase and the timed steps run
+            # the RL selector
+            js = dict(mac="jumpstart_mac", use_rnn=False, jumpstart_action_selector="haa_selector",
+                      jumpstart_epsilon_start=1.0, jumpstart_epsilon_finish=0.0, jumpstart_epsilon_anneal_time=20000,
+                      jumpstart_evaluation_epsilon=0.0)
+            for name, sel_, yaml in (("iql", "eps", "mock_constellation_iql.yaml"),
+                                     ("reda", "sap", "mock_constellation_reda.yaml")):
+                eps_over = dict(epsilon_start=1.0, epsilon_finish=0.0, epsilon_anneal_time=20000)
+                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn_fused", **js, **eps_over)
+                extra[name] = {
+                    **leg_base(rj, sk, a.T),
+                    "what": f"{yaml}: jumpstart_mac (haa_selector jumpstart) + "
+                            f"{'epsilon_greedy' if sel_ == 'eps' else 'sap'} selector, RNNAgent use_rnn False "
+                            f"(Linear + ReLU, fused split-f16 kernel), both epsilons 1 -> 0 over 20,000 env steps; "
+                            f"timed after one warmup episode (the jumpstart/HAA phase, t_env = 0)",
+                    "jumpstart_phase_value": round(rj["global_envs"] * a.T / rj["warmup_elapsed"], 1),
+                    "kernels_ms": {"fused_rollout_per_step": round(rj["fused_ms"], 4) if rj["fused_ms"] else None,
+                                   "env_step": round(rj["kern_ms"], 4) if rj["kern_ms"] else None,
+                                   "select": round(rj["sel_ms"], 4) if rj["sel_ms"] else None,
+                                   "sap_select": round(rj["lsa_ms"], 4) if rj.get("lsa_ms") else None}}
+                if rj.get("fused_ms"):
+                    extra[name]["roofline"] = fused_roofline(a, E, rj["fused_ms"], use_rnn=False)
         if a.config == 2 and world == 1:
             # BASELINE configs[4] on this GPU: 256 x 256 dense benefits, 2,048 envs, the same
             # BasicMAC + RNNAgent + eps-greedy on the fused rollout schedule
@@ -511,12 +580,11 @@ def main():
                 setattr(c4, k, CONFIGS[4][k])
             c4.config = 4
             r5 = run_leg(c4, dev, world, c4.envs, sk, sw)
-            leg = {"value": round(r5["global_envs"] * sk / r5["elapsed"], 1), "unit": "env-steps/s",
-                   "ms_per_step": round(r5["elapsed"] / sk * 1e3, 4), "steps": sk, "warmup": sw,
+            leg = {**leg_base(r5, sk, sw),
                    "workload": CONFIGS[4]["label"] + f"; T={a.T}, L={a.L}, BasicMAC+rnn_fused(GRU 64, fp32) + "
                                                      "epsilon-greedy 0.05, dense benefits",
                    "envs_per_gpu": c4.envs, "n": c4.n, "m": c4.m,
-                   "kernels_ms": {"fused_step_select": round(r5["fused_ms"], 4) if r5.get("fused_ms") else None,
+                   "kernels_ms": {"fused_rollout_per_step": round(r5["fused_ms"], 4) if r5.get("fused_ms") else None,
                                   "env_step": round(r5["kern_ms"], 4) if r5["kern_ms"] else None,
                                   "select": round(r5["sel_ms"], 4) if r5["sel_ms"] else None}}
             if r5.get("fused_ms"):
@@ -544,17 +612,22 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(res["elapsed"] / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": f"synthetic (Philox {a.benefits} benefits, random-init RNN agent)",
-            "config": {"workload": CONFIGS[a.config]["label"] + f"; T={a.T}, L={a.L}, "
-                                   f"BasicMAC+{a.agent}(GRU 64, fp32) + {sel_name} selector, {a.benefits} benefits",
+            "config": {"workload": CONFIGS[a.config]["label"] + f"; T={a.T}, L={a.L}, BasicMAC+{a.agent}"
+                                   f"({'GRU' if a.use_rnn else 'Linear'} 64, fp32) + {sel_name} selector, "
+                                   f"{a.benefits} benefits",
                        "baseline_config_index": 3 if (a.config == 2 and world > 1) else a.config,
                        "envs_per_gpu": E, "global_envs": G, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
                        "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
             "roofline": roof,
-            "kernels_ms": {"fused_step_select": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
+            "kernels_ms": {"fused_rollout_per_step": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
                            "env_step": round(kern_ms, 4) if kern_ms else None,
                            "select": round(sel_ms, 4) if sel_ms else None,
-                           "note": "fused: T-1 fused launches + 1 select + 1 step per episode"
-                                   if res.get("fused_ms") else "one select + one step per step"},
+                           "schedule": res.get("mode") or "split",
+                           "fused_launches": res.get("fused_launches"), "fused_steps": res.get("fused_steps"),
+                           "note": {"episode": "asg_rollout: each launch runs a chunk of an episode's steps (the "
+                                               "runner launches whole episodes); kernel time per step",
+                                    "step": "T-1 fused launches + 1 select + 1 step per episode"}.get(
+                                        res.get("mode"), "one select + one step per step")},
             "roofline_agent": ra,
             "cpu_baseline": cpu,
         }

@@ -43,8 +43,10 @@
  *                              FilteredEpsilonGreedyActionSelector / FilteredSoftPoliciesSelector
  *                              (action_selectors/filtered_classic_selectors.py:6-103)
  *   asg_real_haal_select       HAALSelector.select_action (action_selectors/non_rl_selectors.py:54-118)
- *   asg_step_select            the runner's env.step(t) + mac.select_actions(t + 1) fused
- *                              (episode_runner.py:76-95 / parallel_runner.py:113-200)
+ *   asg_rollout                the runner loop select(0); for t: env.step(t) +
+ *                              mac.select_actions(t + 1), fused for a range of steps up to a whole
+ *                              episode (episode_runner.py:60-127 / parallel_runner.py:113-200);
+ *                              asg_step_select = one step of it
  */
 #ifndef ASG_H
 #define ASG_H
@@ -304,28 +306,41 @@ int asg_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B,
                           uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *out,
                           int32_t *status, void *hip_stream);
 
-/* Fused rollout step: asg_step at row ts (actions_t) and then asg_rnn_agent_select for row
- * ts + 1 (the actions of step t + 1) in ONE kernel -- the runner's env.step(t) followed by
- * mac.select_actions(t + 1) (episode_runner.py:80-95 then :76-79).  The observation rows of
- * t + 1 are generated in the agent's operand layout, written to the batch and consumed
- * without being read back; batch contents, returns, hidden state and actions are
- * bit-identical to the two separate calls with the same arguments.  Requirements: Philox
- * bump/dense benefits, integer actions, n % 32 == 0, m % 32 == 0, m <= 256, the GRU agent
- * (hidden 64, K = m (L + 1), weights packed by asg_rnn_agent_pack for n_out = m), a
- * contiguous time-major EpisodeBatch, and k + 1 < T (the episode's last step is a plain
- * asg_step).  h_in [E n][64] (row stride h_stride, 0 = one broadcast row, NULL = zeros),
- * h_out [E n][64]; selection: epsilon / seed / counter / status as asg_rnn_agent_select
- * (global rows keyed by env_index_base).  hip_stream NULL = the handle's stream. */
+/* Fused rollout: `steps` transitions of every env (asg_step semantics, k = the handle's
+ * step .. k + steps - 1, batch rows ts ..) with the agent forward + epsilon-greedy selection
+ * (asg_rnn_agent_select semantics) of the rows in between, in ONE kernel -- the runner loop
+ * select(0); for t: env.step(t), mac.select_actions(t + 1) (episode_runner.py:60-127,
+ * parallel_runner.py:113-200).  select_first: also select on row ts (the reset row; k == 0
+ * only) before the first transition; select_last: also select on the row after the last
+ * transition (needs k + steps < T).  Row k + 1 is selected when k + 1 < T and it is not the
+ * last row without select_last.  A whole episode is asg_reset then
+ * asg_rollout(ts = 0, steps = T, select_first = 1, select_last = 0).  The observation rows
+ * are generated in the agent's operand layout, written to the batch and consumed without
+ * being read back; each env's selected / previous tasks stay in the kernel's LDS between
+ * steps.  Batch contents, returns, hidden state and actions equal the separate
+ * asg_step / asg_rnn_agent_select calls with the same arguments (counter, counter + 1, ...
+ * for the selections in row order).  Requirements: Philox bump/dense benefits, integer
+ * actions, 16 <= m <= 256, n <= 256, L >= 1, the RNNAgent with hidden 64 (use_rnn: GRUCell,
+ * b_r0 / b_r1 = b_ih / b_hh; else Linear + ReLU, b_r0 = its bias, b_r1 unused) on K = m (L + 1)
+ * inputs, weights packed by asg_rnn_agent_pack for n_out = m, and a contiguous time-major
+ * EpisodeBatch.  h_in [E n][64] (row stride h_stride, 0 = one broadcast row, NULL = zeros)
+ * feeds the first selection; h_out [E n][64] receives every later one's state and finally
+ * the last selection's.  hip_stream NULL = the handle's stream. */
+int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_first, int select_last,
+                const void *packed, const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K,
+                int hidden, int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon,
+                uint64_t seed, uint64_t counter, int32_t *status, void *hip_stream);
+/* asg_rollout with steps = 1, select_first = 0, select_last = 1 and the GRU agent: asg_step
+ * at row ts then asg_rnn_agent_select for row ts + 1 (the round-2 per-step entry point). */
 int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                     const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
                     int32_t *status, void *hip_stream);
-/* Number of fc1 weight slices (32 inputs x 64 units) the fused rollout kernel reads through
- * L2 instead of LDS for an (n, m, L) env, or -1 when asg_step_select does not take the shape
- * (64 x 64, L = 3: 1; 256 x 256: 20).  Each such slice waits for the tile's pending batch
- * stores (gfx9 vmcnt retires in order); measured, the fused kernel still beats asg_step +
- * asg_rnn_agent_select at 20 (256 x 256 dense: +8-13 %), so the runner uses it wherever
- * this is >= 0. */
+/* Number of fc1 weight slices (32 inputs x 64 units) the rollout kernel reads through L2
+ * instead of LDS for an (n, m, L) env and agent kind, or -1 when asg_rollout does not take
+ * the shape (GRU: 64 x 64, L = 3: 1; 256 x 256: 19).  asg_step_select_l2_slices = the GRU
+ * agent's. */
+int asg_rollout_l2_slices(int n, int m, int L, int use_rnn);
 int asg_step_select_l2_slices(int n, int m, int L);
 
 /* ==== RealConstellationEnv ======================================

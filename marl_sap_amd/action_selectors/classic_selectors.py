@@ -59,17 +59,19 @@ class EpsilonGreedyActionSelector:
     def env_index_base(self):
         return env_index_base(self)
 
-    def fused_params(self, t_env, test_mode, device):
+    def fused_params(self, t_env, test_mode, device, calls=1):
         """Epsilon / seed / call counter / status word / global env base for a kernel that
-        fuses this selector into the agent forward (asg_rnn_agent_select); same state
-        updates as select_action."""
+        fuses this selector into the agent forward (asg_rnn_agent_select, asg_rollout); same
+        state updates as `calls` select_action calls (their counters are the returned one,
+        + 1, ...)."""
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:
             self.epsilon = self.args.evaluation_epsilon
         if self.status is None or self.status.device != device:
             self.status = torch.zeros(1, dtype=torch.int32, device=device)
-        self.calls += 1
-        return self.epsilon, self.seed, self.calls, self.status, self.env_index_base()
+        first = self.calls + 1
+        self.calls += int(calls)
+        return self.epsilon, self.seed, first, self.status, self.env_index_base()
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None, out=None):
         self.epsilon = self.schedule.eval(t_env)

@@ -56,18 +56,25 @@ class BasicMAC:
                 and not getattr(self.args, "unfused_selection", False))
 
     def fused_step_ok(self, env, ep_batch):
-        """The runner may fuse env.step(t) with select_actions(t + 1) (asg_step_select):
-        the fused agent + epsilon-greedy selection on plain observation inputs, a time-major
-        batch and an env that takes it.  args.fused_rollout: True (default) / "always" wherever
-        it applies (64 x 64: +15 %, 256 x 256 dense: +8-13 % over asg_step +
-        asg_rnn_agent_select on MI355X), False never."""
+        """The runner may fuse env.step(t) with select_actions(t + 1) (asg_rollout): the fused
+        agent (GRU or Linear RNNAgent) + epsilon-greedy selection on plain observation inputs, a
+        time-major batch and an env that takes it.  args.fused_rollout: True / "episode" /
+        "always" (default: a whole episode per launch), "step" (one launch per step), False
+        (separate env-step and agent launches)."""
         from ..modules.agents.rnn_agent import RNNFusedAgent
         mode = getattr(self.args, "fused_rollout", True)
         return (bool(mode) and self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select")
-                and env.can_step_select(prefer=(mode != "always"))
+                and env.can_step_select(prefer=(mode != "always"), use_rnn=bool(self.args.use_rnn))
                 and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
                 and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
-                and bool(self.args.use_rnn) and self.selector_agent.n_out == env.m)
+                and self.selector_agent.n_out == env.m)
+
+    def fused_mode(self, env, ep_batch, t_env=0, test_mode=False):
+        """How the runner schedules this episode: "episode" (asg_rollout over all T steps),
+        "step" (asg_rollout per step) or None (separate launches)."""
+        if not self.fused_step_ok(env, ep_batch):
+            return None
+        return "step" if getattr(self.args, "fused_rollout", True) == "step" else "episode"
 
     def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
         """env.step at row t_ep and select_actions for row t_ep + 1 in one kernel; the
@@ -75,6 +82,15 @@ class BasicMAC:
         eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device)
         self.hidden_states = env.step_select(ep_batch, t_ep, self.selector_agent, self.hidden_states, eps, seed,
                                              counter, status)
+
+    def fused_episode(self, env, ep_batch, t_env, test_mode=False):
+        """select_actions(0), then env.step(t) + select_actions(t + 1) for the whole episode
+        (the last step without a selection after it) in ONE kernel launch; selector counters
+        and the hidden state advance as T select_actions calls would advance them."""
+        T = env.T
+        eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device, calls=T)
+        self.hidden_states = env.rollout(ep_batch, 0, T, self.selector_agent, self.hidden_states, eps, seed, counter,
+                                         status, select_first=True, select_last=False)
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

@@ -1,6 +1,14 @@
 """Jumpstart controller (reference: controllers/jumpstart_controller.py:10-121): with
-probability jumpstart_epsilon (one numpy coin flip per step for the whole batch, drawn
-from numpy's global stream like the reference) the non-RL selector (HAA) acts."""
+probability jumpstart_epsilon (one numpy coin flip per selection for the whole batch, drawn
+from numpy's global stream like the reference) the non-RL selector (HAA) acts.
+
+The GPU runner draws an episode's coin flips when it plans the episode (fused_mode), in the
+reference's order (one per select_actions call, t = 0, 1, ...): nothing else draws from
+numpy's global stream inside the loop, so the stream is consumed exactly as the reference's
+per-step draws consume it.  When every flip picks the RL branch and the RL MAC fuses (the
+RNNAgent + epsilon-greedy: mock_constellation_iql.yaml), the episode is one asg_rollout
+kernel; otherwise the RL steps still fuse env.step(t) with select_actions(t + 1) where they
+can, and the HAA steps run env.step + the HAA selector."""
 import numpy as np
 
 from ..action_selectors.non_rl_selectors import REGISTRY as non_rl_REGISTRY
@@ -16,14 +24,48 @@ class JumpstartMAC(BasicMAC):
                                                             args.jumpstart_epsilon_finish,
                                                             args.jumpstart_epsilon_anneal_time, decay="linear")
         self.jumpstart_epsilon = self.jumpstart_eps_schedule.eval(0)
+        self._flips = []  # pre-drawn coin flips of the planned episode (True: the jumpstart selector acts)
 
-    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False, out=None):
+    def _eps(self, t_env, test_mode):
         self.jumpstart_epsilon = self.jumpstart_eps_schedule.eval(t_env)
         if test_mode:
             self.jumpstart_epsilon = self.args.jumpstart_evaluation_epsilon
-        if np.random.rand() < self.jumpstart_epsilon:
+        return self.jumpstart_epsilon
+
+    def _coin(self, t_env, test_mode):
+        eps = self._eps(t_env, test_mode)
+        if self._flips:
+            return self._flips.pop(0)
+        return np.random.rand() < eps
+
+    def select_actions(self, ep_batch, t_ep, t_env, bs=slice(None), test_mode=False, out=None):
+        if self._coin(t_env, test_mode):
             return self.jumpstart_action_selector.select_action(ep_batch[bs, t_ep])
         return super().select_actions(ep_batch, t_ep, t_env, bs=bs, test_mode=test_mode, out=out)
+
+    def fused_mode(self, env, ep_batch, t_env=0, test_mode=False):
+        """Draw the episode's T coin flips now (the reference's order); "episode" when every
+        one picks the RL branch and the RL MAC fuses, else the base class's per-step choice
+        ("step" fuses the RL steps' env.step + selection) or None."""
+        eps = self._eps(t_env, test_mode)
+        self._flips = list(np.random.rand(env.T) < eps)
+        base = super().fused_mode(env, ep_batch, t_env, test_mode)
+        if base is None:
+            return None
+        return "episode" if base == "episode" and not any(self._flips) else "step"
+
+    def fused_episode(self, env, ep_batch, t_env, test_mode=False):
+        self._flips = []  # all RL: consumed by the one kernel
+        super().fused_episode(env, ep_batch, t_env, test_mode)
+
+    def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
+        """env.step(t) and select_actions(t + 1): one kernel when the flip for t + 1 picks the
+        RL branch, else env.step then the jumpstart selector on row t + 1."""
+        if not self._coin(t_env, test_mode):
+            return super().fused_step_select(env, ep_batch, t_ep, t_env, test_mode)
+        env.step(ep_batch, ts=t_ep)
+        acts = self.jumpstart_action_selector.select_action(ep_batch[:, t_ep + 1])
+        ep_batch.update({"actions": acts}, ts=t_ep + 1, mark_filled=False, preprocess=False)
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

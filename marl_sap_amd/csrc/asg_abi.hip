@@ -507,63 +507,79 @@ int asg_filtered_soft_map(const int64_t *picked, const int64_t *topm, int64_t B,
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_soft_map");
 }
 
-// ---- fused rollout step (asg_agent.hip:rollout_h2_kernel) ----------------------------------
+// ---- fused rollout (asg_h2.hip:rollout_kernel) ------------------------------------------
 // field f of a time-major batch ([T+1][E][d2][d3] storage seen as [E][T+1][d2][d3]): the
-// contiguous [E][d2][d3] slab of row t, or nullptr when absent / laid out otherwise
-static void *tm_slab(const asg_field &f, int t, int64_t E, int64_t d2, int64_t d3, size_t esize, bool *ok) {
+// row-0 pointer and the row stride (elements), or nullptr when absent / laid out otherwise
+static void *tm_base(const asg_field &f, int64_t E, int64_t d2, int64_t d3, int64_t *row, bool *ok) {
+    *row = 0;
     if (!f.ptr) return nullptr;
     const bool good = f.stride[0] == d2 * d3 && f.stride[1] == E * d2 * d3 && (d2 == 1 || f.stride[2] == d3) &&
                       (d3 == 1 || f.stride[3] == 1);
     if (!good) *ok = false;
-    return static_cast<char *>(f.ptr) + (size_t)t * f.stride[1] * esize;
+    *row = f.stride[1];
+    return f.ptr;
 }
 
-int asg_step_select_l2_slices(int n, int m, int L) { return asg::rollout_l2_slices(n, m, L); }
+int asg_step_select_l2_slices(int n, int m, int L) { return asg::rollout_l2_slices(n, m, L, 1); }
+int asg_rollout_l2_slices(int n, int m, int L, int use_rnn) { return asg::rollout_l2_slices(n, m, L, use_rnn); }
+
+int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_first, int select_last,
+                const void *packed, const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K,
+                int hidden, int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon,
+                uint64_t seed, uint64_t counter, int32_t *status, void *hip_stream) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (int rc = check_view(h, b, ts, true)) return rc;
+    if (!packed || !b1 || !b_r0 || (use_rnn && !b_r1) || !b2 || !h_out || !status)
+        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: NULL agent argument");
+    const asg::EnvState &st = h->st;
+    if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
+    if (steps < 1 || h->k + steps > st.T)
+        return fail(h, ASG_E_STATE, "asg_rollout: steps must be >= 1 and stay within the episode (k + steps <= T)");
+    if (select_first && h->k != 0)
+        return fail(h, ASG_E_STATE, "asg_rollout: select_first selects on the reset row (k == 0 only)");
+    if (select_last && h->k + steps >= st.T)
+        return fail(h, ASG_E_STATE, "asg_rollout: select_last needs a next step to select for (k + steps < T)");
+    if (st.bids || st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED)
+        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: Philox bump/dense benefits with integer actions only");
+    if (hidden != 64 || !asg::rollout_shape_ok(st.n, st.m, st.L, K))
+        return fail(h, ASG_E_INVALID_ARG,
+                    "asg_rollout: needs the RNNAgent (hidden 64) on the env's obs (K = m (L + 1), L >= 1), "
+                    "16 <= m <= 256, n <= 256");
+    if (!(epsilon >= 0.0 && epsilon <= 1.0)) return fail(h, ASG_E_INVALID_ARG, "asg_rollout: epsilon in [0, 1]");
+    if (h_stride % 4 != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0) ||
+        (reinterpret_cast<uintptr_t>(h_out) % 16) != 0)
+        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: hidden-state rows must be 16-B aligned");
+    const int64_t E = st.E, n = st.n, m = st.m, Kk = K;
+    bool ok = true;
+    asg::RolloutSlabs sl{};
+    sl.obs = static_cast<float *>(tm_base(b->obs, E, n, Kk, &sl.obs_row, &ok));
+    sl.beta = static_cast<float *>(tm_base(b->beta, E, n, m, &sl.beta_row, &ok));
+    sl.avail = static_cast<uint8_t *>(tm_base(b->avail_actions, E, n, m, &sl.avail_row, &ok));
+    sl.onehot = static_cast<int64_t *>(tm_base(b->actions_onehot, E, n, m, &sl.onehot_row, &ok));
+    sl.act = static_cast<int64_t *>(tm_base(b->actions, E, n, 1, &sl.act_row, &ok));
+    sl.rew = static_cast<float *>(tm_base(b->rewards, E, n, 1, &sl.rew_row, &ok));
+    sl.prevb = static_cast<int64_t *>(tm_base(b->prev_assigns, E, n, 1, &sl.prevb_row, &ok));
+    sl.term = static_cast<uint8_t *>(tm_base(b->terminated, E, 1, 1, &sl.term_row, &ok));
+    sl.filled = static_cast<int64_t *>(tm_base(b->filled, E, 1, 1, &sl.filled_row, &ok));
+    auto al = [](const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
+    if (!ok || !al(sl.obs, 16) || !al(sl.beta, 16) || !al(sl.avail, 16) || !al(sl.onehot, 16))
+        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: needs a contiguous time-major batch (EpisodeBatch(time_major=True))");
+    DeviceGuard g(h->device);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
+    hipError_t e = asg::launch_rollout(sl, st, ts, h->k, steps, select_first, select_last,
+                                       static_cast<const float4 *>(packed), b1, b_r0, b_r1, b2, use_rnn, h_in, h_stride,
+                                       h_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_rollout");
+    h->k += steps;
+    return ASG_OK;
+}
 
 int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                     const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
                     int32_t *status, void *hip_stream) {
-    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
-    if (int rc = check_view(h, b, ts, true)) return rc;
-    if (!packed || !b1 || !b_ih || !b_hh || !b2 || !h_out || !status)
-        return fail(h, ASG_E_INVALID_ARG, "asg_step_select: NULL agent argument");
-    const asg::EnvState &st = h->st;
-    if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
-    if (h->k + 1 >= st.T)
-        return fail(h, ASG_E_STATE, "asg_step_select needs a next step to select for (k + 1 < T): use asg_step");
-    if (st.bids || st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED)
-        return fail(h, ASG_E_INVALID_ARG, "asg_step_select: Philox bump/dense benefits with integer actions only");
-    if (hidden != 64 || !asg::rollout_shape_ok(st, K, st.m, 1))
-        return fail(h, ASG_E_INVALID_ARG,
-                    "asg_step_select: needs the GRU agent (hidden 64, K = m (L + 1)), n % 32 == 0, m % 32 == 0, m <= 256");
-    if (!(epsilon >= 0.0 && epsilon <= 1.0)) return fail(h, ASG_E_INVALID_ARG, "asg_step_select: epsilon in [0, 1]");
-    if (h_stride % 4 != 0 || (h_in && (reinterpret_cast<uintptr_t>(h_in) % 16) != 0))
-        return fail(h, ASG_E_INVALID_ARG, "asg_step_select: h_in rows must be 16-B aligned");
-    const int64_t E = st.E, n = st.n, m = st.m, Kk = K;
-    bool ok = true;
-    asg::RolloutSlabs sl{};
-    sl.obs1 = static_cast<float *>(tm_slab(b->obs, ts + 1, E, n, Kk, 4, &ok));
-    sl.beta1 = static_cast<float *>(tm_slab(b->beta, ts + 1, E, n, m, 4, &ok));
-    sl.avail1 = static_cast<uint8_t *>(tm_slab(b->avail_actions, ts + 1, E, n, m, 1, &ok));
-    sl.onehot0 = static_cast<int64_t *>(tm_slab(b->actions_onehot, ts, E, n, m, 8, &ok));
-    sl.act0 = static_cast<const int64_t *>(tm_slab(b->actions, ts, E, n, 1, 8, &ok));
-    sl.act1 = static_cast<int64_t *>(tm_slab(b->actions, ts + 1, E, n, 1, 8, &ok));
-    sl.rew0 = static_cast<float *>(tm_slab(b->rewards, ts, E, n, 1, 4, &ok));
-    sl.prev1 = static_cast<int64_t *>(tm_slab(b->prev_assigns, ts + 1, E, n, 1, 8, &ok));
-    sl.term0 = static_cast<uint8_t *>(tm_slab(b->terminated, ts, E, 1, 1, 1, &ok));
-    sl.filled1 = static_cast<int64_t *>(tm_slab(b->filled, ts + 1, E, 1, 1, 8, &ok));
-    auto al = [](const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; };
-    if (!ok || !al(sl.obs1, 16) || !al(sl.beta1, 16) || !al(sl.avail1, 4) || !al(sl.onehot0, 16))
-        return fail(h, ASG_E_INVALID_ARG, "asg_step_select: needs a contiguous time-major batch (EpisodeBatch(time_major=True))");
-    DeviceGuard g(h->device);
-    hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
-    hipError_t e = asg::launch_rollout_step_select(sl, st, ts, h->k, static_cast<const float4 *>(packed), b1, b_ih,
-                                                   b_hh, b2, h_in, h_stride, h_out, (float)epsilon, seed,
-                                                   (uint32_t)counter, st.env_base * n, status, s);
-    if (e != hipSuccess) return hip_fail(h, e, "asg_step_select");
-    h->k += 1;
-    return ASG_OK;
+    return asg_rollout(h, b, ts, 1, 0, 1, packed, b1, b_ih, b_hh, b2, K, hidden, 1, h_in, h_stride, h_out, epsilon,
+                       seed, counter, status, hip_stream);
 }
 
 }  // extern "C"

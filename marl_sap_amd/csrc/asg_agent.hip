@@ -21,8 +21,7 @@
 #include <cstring>
 #include <type_traits>
 
-#include "asg_device.h"
-#include "asg_internal.h"
+#include "asg_agent_common.h"
 
 // The library builds with -ffp-contract=off so the env and LSA kernels round every float64
 // add/mul as numpy does.  The agent's results are fp32-accurate, not bit-matched to a
@@ -37,7 +36,6 @@
 
 namespace asg {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // row tiles of 16 per wave (ASG_AGENT_NT = 2: 32 rows per wave at 2 waves per SIMD;
 // 1: 16 rows per wave, fewer registers, more waves per SIMD)
@@ -49,7 +47,6 @@ constexpr int kRowsPerWave = 16 * kNT;
 #ifndef ASG_AGENT_WAVES
 #define ASG_AGENT_WAVES 2  // waves per SIMD the register budget is fitted to
 #endif
-constexpr int kHid = 64;          // hidden_dim
 
 // ASG_AGENT_STAMPS (profiling builds only): s_memtime at the phase boundaries of the
 // first tiles of workgroup 0's waves, read back with asg_debug_agent_stamps()
@@ -96,7 +93,6 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 #define ASG_AGENT_FC2_X3 0
 #endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // packed W_ih / W_hh: [gate 3][slab hb 4][k-slice 2][plane 3][lane 64] x 8 bf16
 constexpr int kGruX3F4 = 3 * 4 * 2 * 3 * 64;
 // float4 count of one packed GRU matrix (W_ih or W_hh)
@@ -147,9 +143,6 @@ __device__ __forceinline__ f32x4 mfma_x3(const u32x4v (&w)[3], const u32x4v (&x)
 
 __device__ __forceinline__ float4 ldg4(const float *p, bool ok) {
     return ok ? *reinterpret_cast<const float4 *>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-__device__ __forceinline__ float comp(const float4 &v, int e) {
-    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
 
 // GRU nonlinearities on the hardware transcendental units (v_exp_f32, v_rcp_f32): a few
@@ -207,98 +200,7 @@ __global__ void pack_weights_kernel(const float *W, int C, int K, float4 *out) {
 // (tiles 0-15, 16-31; the second only with GEN).  The general path costs ~3 % at the
 // bench shape, hence the two instantiations.
 
-// Epilogue of the fused epsilon-greedy selection (asg_select.hip semantics): reduce each
-// row's running argmax over its 4 lanes, then lane q == nt finishes row nt -- the greedy
-// action, or with probability epsilon the target-th available task in index order.
-// best / bj / amask: per-lane partial argmax and availability bits of the row's tasks.
-template <bool GEN, int NT = kNT>
-__device__ __forceinline__ void select_finish(float (&best)[NT], int (&bj)[NT], const uint64_t (&amask)[NT][2],
-                                              const int64_t (&rows)[NT], const bool (&ok)[NT],
-                                              const int64_t (&oidx)[NT], int nct, const SelectArgs &sel, int q) {
-    // reduce each row over its 4 lanes (q = 0..3: lane ^ 16, lane ^ 32) -------------
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        auto red = [&](auto swp) {
-            const SwapPair pb = swp(__builtin_bit_cast(uint32_t, best[nt]));
-            const SwapPair pj = swp((uint32_t)bj[nt]);
-            float vb = __builtin_bit_cast(float, pb.a);
-            int jb = (int)pj.a;
-            if (better(__builtin_bit_cast(float, pb.b), (int)pj.b, vb, jb)) {
-                vb = __builtin_bit_cast(float, pb.b);
-                jb = (int)pj.b;
-            }
-            best[nt] = vb;
-            bj[nt] = jb;
-        };
-        red(swap16);
-        red(swap32);
-    }
-    // lane q == nt finishes row nt: greedy action, or with probability epsilon the
-    // target-th available task in index order (Categorical over avail, as asg_select.hip)
-    const int nt = NT == 1 ? 0 : (q & 1);
-    const int64_t row = rows[nt];
-    int action = bj[nt] == 0x7fffffff ? 0 : bj[nt];
-    bool explore = false;
-    u32x4 rr = u32x4{0u, 0u, 0u, 0u};
-    if (sel.epsilon > 0.0f) {
-        const int64_t grow = row + sel.row_base;  // global (env, agent) row: shard-invariant draws
-        rr = philox4x32_10(u32x4{(uint32_t)grow, (uint32_t)(grow >> 32), kCtrSelect, sel.counter}, sel.k0, sel.k1);
-        constexpr float k2m24 = 5.9604644775390625e-08f;
-        explore = ok[nt] && q < NT && (float)(rr.x >> 8) * k2m24 < sel.epsilon;
-    }
-    if (__ballot(explore)) {  // some row of the wave explores (about epsilon of the rows)
-        // Per 64-task window: the row's availability in task order, assembled from its 4
-        // lanes (task 16 c + 4 q + v is bit 4 c + v of lane q's slice) with two swaps;
-        // the exploring lane then takes the target-th set bit by a popcount bisection.
-        const int nwin = (nct + 3) / 4;
-        int target = -1, found = -1;
-        for (int ntt = 0; ntt < NT; ++ntt) {
-            const bool mine_row = explore && nt == ntt;
-            int cnt = __popcll(amask[ntt][0]) + (GEN ? __popcll(amask[ntt][1]) : 0);
-            {
-                const SwapPair c16 = swap16((uint32_t)cnt);
-                const SwapPair c32 = swap32(c16.a + c16.b);
-                cnt = (int)(c32.a + c32.b);
-            }
-            if (mine_row) {
-                if (cnt == 0) atomicCAS(sel.err, 0, ASG_E_INVALID_ARG);
-                else target = (int)(((uint64_t)rr.y * (uint64_t)cnt) >> 32);
-            }
-            for (int w = 0; w < nwin; ++w) {
-                const uint32_t mine = (uint32_t)(((GEN && w >= 4) ? amask[ntt][1] : amask[ntt][0]) >> (16 * (w & 3))) & 0xFFFFu;
-                uint32_t lo = 0, hi = 0;  // this lane's tasks of the window, in task order
-#pragma unroll
-                for (int c = 0; c < 2; ++c) lo |= ((mine >> (4 * c)) & 0xFu) << (16 * c + 4 * q);
-#pragma unroll
-                for (int c = 2; c < 4; ++c) hi |= ((mine >> (4 * c)) & 0xFu) << (16 * (c - 2) + 4 * q);
-                const SwapPair l16 = swap16(lo), h16 = swap16(hi);
-                const SwapPair l32 = swap32(l16.a | l16.b), h32 = swap32(h16.a | h16.b);
-                uint64_t row_mask = (uint64_t)(l32.a | l32.b) | ((uint64_t)(h32.a | h32.b) << 32);
-                if (mine_row && target >= 0) {
-                    const int pc = __popcll(row_mask);
-                    if (target < pc) {
-                        int k = target, pos = 0;
-#pragma unroll
-                        for (int half = 32; half >= 1; half >>= 1) {
-                            const uint64_t low = row_mask & ((1ull << half) - 1ull);
-                            const int lc = __popcll(low);
-                            const bool up = k >= lc;
-                            k -= up ? lc : 0;
-                            pos += up ? half : 0;
-                            row_mask = up ? (row_mask >> half) : low;
-                        }
-                        found = 64 * w + pos;
-                        target = -1;
-                    } else {
-                        target -= pc;
-                    }
-                }
-            }
-        }
-        if (found >= 0) action = found;
-    }
-    if (q < NT && ok[nt]) sel.out[oidx[nt]] = action;
-}
+// (the fused epsilon-greedy epilogue, select_finish, is in asg_agent_common.h)
 
 template <bool RNN, bool SEL, bool GEN>
 __device__ __forceinline__ void agent_rows(
@@ -899,783 +801,12 @@ rnn_agent_lds_kernel(
     }
 }
 
-// =====================================================================================
-// Two-way-split f16 path ("h2"): every layer's f32 products on v_mfma_f32_16x16x32_f16.
-//
-// An f32 operand x (pre-scaled by a power of two so |x| < 2^15) is split x ~ h + l with
-// h = RNE_f16(x), l = RNE_f16(x - h) (x - h is exact in f32): |x - h - l| <= 2^-22 |x| for
-// every operand whose residual is a normal f16 (the power-of-two scaling keeps them
-// there), and a product sums w.x ~ wh.xh + wh.xl + wl.xh (the dropped wl.xl is below
-// 2^-22 relative).  Products are exact in the MFMA's f32 accumulator; summation stays
-// f32.  So each product carries ~3 x 2^-22 relative error, which over the dot products of
-// this network is the size of fp32 GEMM accumulation error itself
-// (tests/test_gpu_agent.py::test_split_bf16_gru_is_fp32_accurate measures both against
-// float64).  Against the three-way bf16 split (6 MFMAs per 32-deep slice) this is 3
-// MFMAs, and against the f32 MFMA (8 x 32 cycles per slice) 3 x 16 cycles.
-//
-// Scaling: weights by 2^sw per matrix (pack time, from max|W|); activations by 2^sx per
-// wave tile (from the tile's max|x|, a wave reduction); the accumulators start from
-// bias * 2^(sw + sx) and are unscaled by 2^-(sw + sx) (powers of two: exact).  The fc1
-// input scale is chosen before its values are seen: the wave keeps the last tile's
-// scale, tracks the tile's max while it streams the observations, and re-runs fc1 for
-// the tile at a smaller scale in the (never seen in the mock env) case it would have
-// exceeded 2^15.  The r / z gates add the x and h products in one accumulator, so
-// their scales are matched (sw_ih + sx = sw_hh + sh).
-// =====================================================================================
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x4 mfma_h(const u32x4v &a, const u32x4v &b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
-                                                  0);
-}
-// (wh, wl) . (xh, xl) = wh.xh + wh.xl + wl.xh; the correction terms first
-__device__ __forceinline__ f32x4 mfma_h2(const u32x4v (&w)[2], const u32x4v (&x)[2], f32x4 c) {
-    c = mfma_h(w[1], x[0], c);
-    c = mfma_h(w[0], x[1], c);
-    c = mfma_h(w[0], x[0], c);
-    return c;
-}
-// 8 (scaled) f32 -> f16 planes h, l (element j in half j & 1 of dword j >> 1)
-__device__ __forceinline__ void split2(const float (&x)[8], u32x4v &h, u32x4v &l) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const f16x2v hh = {(_Float16)x[2 * p], (_Float16)x[2 * p + 1]};
-        const float ra = x[2 * p] - (float)hh[0], rb = x[2 * p + 1] - (float)hh[1];
-        const f16x2v ll = {(_Float16)ra, (_Float16)rb};
-        h[p] = __builtin_bit_cast(uint32_t, hh);
-        l[p] = __builtin_bit_cast(uint32_t, ll);
-    }
-}
-// The split of 8 UNSCALED values at scale sc (a power of two): h = RNE_f16(x * sc) and
-// l = RNE_f16(x * sc - h), the same planes as split2 of the scaled values.  ASG_H2_MIX: the
-// residual is one v_fma_mix{lo,hi}_f16 per value (fma(x, sc, -h) is exact in f32, rounded
-// once to f16) instead of convert-back + subtract + convert.
-#ifndef ASG_H2_MIX
-#define ASG_H2_MIX 1
-#endif
-__device__ __forceinline__ void split2s(const float (&x)[8], float sc, u32x4v &h, u32x4v &l) {
-#if ASG_H2_MIX
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const f16x2v hh = {(_Float16)(x[2 * p] * sc), (_Float16)(x[2 * p + 1] * sc)};
-        const uint32_t hv = __builtin_bit_cast(uint32_t, hh);
-        uint32_t lv = 0;
-        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "+v"(lv) : "v"(x[2 * p]), "v"(sc), "v"(hv));
-        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "+v"(lv)
-            : "v"(x[2 * p + 1]), "v"(sc), "v"(hv));
-        h[p] = hv;
-        l[p] = lv;
-    }
-#else
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = x[j] * sc;
-    split2(v, h, l);
-#endif
-}
-// max(m, |a|, |b|) in one v_max3_f32 (fmaxf on |x| otherwise canonicalises every input)
-__device__ __forceinline__ float max3_abs(float m, float a, float b) {
-#if ASG_H2_MIX
-    float r;
-    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
-#else
-    return fmaxf(m, fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)));
-#endif
-}
-// 2^s as a float (s clamped to the normal range [-126, 127])
-__device__ __forceinline__ float pow2f(int s) {
-    s = s < -126 ? -126 : (s > 127 ? 127 : s);
-    return __builtin_bit_cast(float, (uint32_t)(s + 127) << 23);
-}
-// the scale exponent s with m * 2^s < 2^15 (m = max |x| >= 0), clamped to [lo, hi]
-__device__ __forceinline__ int h2_scale(float m, int lo, int hi) {
-    const int e = m > 0.f ? (int)((__builtin_bit_cast(uint32_t, m) >> 23) & 0xff) - 126 : -200;  // m < 2^e
-    const int s = 15 - e;
-    return s < lo ? lo : (s > hi ? hi : s);
-}
-__device__ __forceinline__ float wave_max_f32(float v) {
-    return wave_allreduce(v, [](float a, float b) { return fmaxf(a, b); });
-}
-__device__ __forceinline__ float absmax4(float m, const float4 &v) {
-    return max3_abs(max3_abs(m, v.x, v.y), v.z, v.w);
-}
-__device__ __forceinline__ float absmax4(float m, const f32x4 &v) {
-    return max3_abs(max3_abs(m, v[0], v[1]), v[2], v[3]);
-}
-
-// packed h2 section (u32x4v units): [header 1: int sw1, sw_ih, sw_hh, sw2]
-//   [W1 planes: slice K/32][mt 4][plane 2][lane 64]
-//   [W_ih planes: gate 3][hb 4][slice 2][plane 2][lane 64] [W_hh planes: same]
-//   [W2 planes: tile nct][slice 2][plane 2][lane 64]
-constexpr int kH2GruF4 = 3 * 4 * 2 * 2 * 64;
-__device__ __forceinline__ int h2_gru_idx(int g, int hb, int sl, int pl, int lane) {
-    return (((g * 4 + hb) * 2 + sl) * 2 + pl) * 64 + lane;
-}
-__device__ __forceinline__ int64_t h2_w1_idx(int sl, int mt, int pl, int lane) {
-    return (((int64_t)sl * 4 + mt) * 2 + pl) * 64 + lane;
-}
-__device__ __forceinline__ int h2_w2_idx(int c, int sl, int pl, int lane) { return ((c * 2 + sl) * 2 + pl) * 64 + lane; }
-__host__ __device__ static inline int64_t h2_w1_f4(int K) { return (int64_t)(K / 32) * 4 * 2 * 64; }
-__host__ __device__ static inline int64_t h2_w2_f4(int nout) { return (int64_t)((nout + 15) / 16) * 2 * 2 * 64; }
-static int64_t h2_section_f4(int K, int nout) { return 1 + h2_w1_f4(K) + 2 * kH2GruF4 + h2_w2_f4(nout); }
-// shapes the h2 kernel takes: GRU, hidden 64, K % 32 == 0, 16 <= n_out <= 256, n_out % 16 == 0
-static bool h2_shape(int K, int nout, int use_rnn) {
-    return use_rnn && K % 32 == 0 && nout % 16 == 0 && nout >= 16 && nout <= 256;
-}
-static int64_t rnn_agent_h2_f4(int K, int nout, int use_rnn) {
-    return h2_shape(K, nout, use_rnn) ? h2_section_f4(K, nout) : 0;
-}
-
-// observation slices (32 inputs x 32 rows, 4 KiB) in flight per wave in fc1
-#ifndef ASG_H2_XBUF
-#define ASG_H2_XBUF 2
-#endif
-constexpr int kH2XBuf = ASG_H2_XBUF;
-// rows per wave tile = 16 * ASG_H2_NT; waves per SIMD ASG_H2_WAVES (register budget 512 / it)
-#ifndef ASG_H2_NT
-#define ASG_H2_NT 2
-#endif
-#ifndef ASG_H2_WAVES
-#define ASG_H2_WAVES 2
-#endif
-constexpr int kH2NT = ASG_H2_NT, kH2WavesPerSimd = ASG_H2_WAVES, kH2Waves = 4 * ASG_H2_WAVES;
-#ifndef ASG_H2_LATE_H
-#define ASG_H2_LATE_H 1
-#endif
-// fc1 input scale: every tile starts from the launch's guess 2^11 (|x| < 16 needs no retry),
-// so a tile's result depends on its own rows only (the fused rollout kernel reproduces it
-// bit for bit); ASG_H2_CARRY_SX=1 carries the previous tile's scale instead
-#ifndef ASG_H2_CARRY_SX
-#define ASG_H2_CARRY_SX 0
-#endif
-constexpr int kH2SxInit = 11;
-// one-hot columns gathered at the tile start into the fc1 accumulators (0) or added at the
-// fc1 tail (1)
-#ifndef ASG_H2_GATHER_TAIL
-#define ASG_H2_GATHER_TAIL 0
-#endif
-// keep h_in as f32 through the GRU for its update (1) or rebuild it from its f16 planes (0)
-#ifndef ASG_H2_KEEP_H
-#define ASG_H2_KEEP_H 0
-#endif
-
-struct H2Args {
-    const float *X;
-    int64_t xs, R;
-    int K, P;  // P: one-hot prefix inputs (multiple of 32), 0 = none
-    const float *Hin;
-    int64_t hs;
-    const u32x4v *pk;  // h2 section
-    const float *W1T;  // [P][64] f32: W1 columns of the one-hot prefix
-    const float *b1, *bih, *bhh, *b2;
-    int nout;
-    float *Hout, *Q;
-    SelectArgs sel;
-    int w1_lds;        // W1 slices [P/32, P/32 + w1_lds) staged in LDS, the rest read through L2
-};
-
-// LDS stage (float4 units): [W_ih planes][W_hh planes][biases][W2 planes (W2L)][W1 slices]
-// biases (floats): b1 [64] | b_ir + b_hr [64] | b_iz + b_hz [64] | b_in [64] | b_hn [64] | b2 [n_out]
-__host__ __device__ static inline int64_t h2_bias_f4(int nout) { return (5 * 64 + nout + 3) / 4; }
-__host__ __device__ static inline int64_t h2_w2_off(int nout) { return 2 * kH2GruF4 + h2_bias_f4(nout); }
-__host__ __device__ static inline int64_t h2_w1_off(int nout, bool w2l) {
-    return h2_w2_off(nout) + (w2l ? h2_w2_f4(nout) : 0);
-}
-
-typedef const u32x4v __attribute__((address_space(3))) * lds_u4p;
-typedef const f32x4 __attribute__((address_space(3))) * lds_f4v;
-
-// The GRU, fc2 and selection of one 32-row wave tile on split-f16 MFMAs (shared by the
-// agent kernel and the fused rollout kernel): xB = relu(fc1) fragments, hB = h_in rows.
-// ALLAV: every task is available (the fused rollout wrote avail = 1 itself).
-template <int NT, bool SEL, bool W2L, bool ALLAV>
-__device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
-                                        const int64_t (&rows)[NT], const bool (&ok)[NT], const float4 (&hB)[4][NT],
-                                        const f32x4 (&xB)[4][NT]) {
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    (void)r;
-    const lds_u4p Wih = (lds_u4p)Wl, Whh = (lds_u4p)(Wl + kH2GruF4);
-    const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);  // biases
-    // availability words of fc2's first four output tiles: issued now, used after the GRU
-    const SelectArgs &sel = a.sel;
-    const int nct = a.nout >> 4;
-    const uint8_t *arow[NT];
-    int64_t oidx[NT];
-    bool av4 = false;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        arow[nt] = nullptr;
-        oidx[nt] = 0;
-    }
-    if (SEL) {
-        const int64_t b0 = row0 / sel.n;
-        const int i0 = (int)(row0 - b0 * sel.n);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            int64_t b = b0;
-            int i = i0 + 16 * nt + r;
-            while (i >= sel.n) {
-                i -= sel.n;
-                ++b;
-            }
-            arow[nt] = sel.avail + (ok[nt] ? b * sel.a0 + (int64_t)i * sel.a1 : 0);
-            oidx[nt] = b * sel.o0 + (int64_t)i * sel.o1;
-        }
-        av4 = ((reinterpret_cast<uintptr_t>(sel.avail) | (uintptr_t)sel.a0 | (uintptr_t)sel.a1) & 3u) == 0;
-    }
-    auto load_av = [&](int c, int nt) -> uint32_t {
-        if (!SEL || !ok[nt]) return 0u;
-        if (ALLAV) return 0x01010101u;
-        const uint8_t *ap = arow[nt] + 16 * c + 4 * q;
-        return av4 ? *reinterpret_cast<const uint32_t *>(ap)
-                   : ((uint32_t)ap[0] | ((uint32_t)ap[1] << 8) | ((uint32_t)ap[2] << 16) | ((uint32_t)ap[3] << 24));
-    };
-    uint32_t avw[4][NT];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) avw[c][nt] = c < nct ? load_av(c, nt) : 0u;
-
-    // ---- GRU: scales, operand planes, gates per 16-unit block hb ------------------------
-    float mx = 0.f, mh = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            mx = absmax4(mx, xB[t][nt]);
-            mh = absmax4(mh, hB[t][nt]);
-        }
-    mx = wave_max_f32(mx);
-    mh = wave_max_f32(mh);
-    const bool h_zero = !(mh > 0.f);  // zeros (init_hidden): the W_hh products are skipped
-    int Sg = min(sw[1] + h2_scale(mx, -90, 90), h_zero ? 1000 : sw[2] + h2_scale(mh, -90, 90));
-    Sg = Sg > 100 ? 100 : (Sg < -100 ? -100 : Sg);
-    u32x4v xP[2][NT][2], hP[2][NT][2];
-    {
-        const float cx = pow2f(Sg - sw[1]), ch = pow2f(Sg - sw[2]);
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                float v8[8], h8[8];
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        v8[4 * c + v] = xB[2 * sl + c][nt][v];
-                        h8[4 * c + v] = comp(hB[2 * sl + c][nt], v);
-                    }
-                split2s(v8, cx, xP[sl][nt][0], xP[sl][nt][1]);
-                split2s(h8, ch, hP[sl][nt][0], hP[sl][nt][1]);
-            }
-    }
-    // sigmoid(g * 2^-Sg) = 1 / (1 + 2^(g * c1)), tanh(y * 2^-Sg) = 2 / (1 + 2^(y * c2)) - 1
-    const float c1 = -1.4426950408889634f * pow2f(-Sg), c2 = 2.0f * c1;
-    const float hun = pow2f(sw[2] - Sg);  // unscale of the h planes
-    const float scS = pow2f(Sg);
-    f32x4 hp[4][NT];
-#pragma unroll
-    for (int hb = 0; hb < 4; ++hb) {
-#ifndef ASG_STAMP_FC1
-        if (hb > 0) ASG_STAMP(3 + hb);
-#endif
-        // r and z sum the input and hidden products in one accumulator, from b_i + b_h;
-        // n keeps them apart (n = tanh(i_n + r * h_n))
-        const f32x4 br = Bs[16 + 4 * hb + q], bz = Bs[32 + 4 * hb + q], bn = Bs[48 + 4 * hb + q],
-                    bhn = Bs[64 + 4 * hb + q];
-        f32x4 gr[NT], gz[NT], gni[NT], gnh[NT];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            gr[nt] = br * scS;
-            gz[nt] = bz * scS;
-            gni[nt] = bn * scS;
-            gnh[nt] = bhn * scS;
-        }
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-            for (int g = 0; g < 3; ++g) {
-                const u32x4v w[2] = {Wih[h2_gru_idx(g, hb, sl, 0, lane)], Wih[h2_gru_idx(g, hb, sl, 1, lane)]};
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-                    f32x4 &acc_ = g == 0 ? gr[nt] : (g == 1 ? gz[nt] : gni[nt]);
-                    acc_ = mfma_h2(w, xP[sl][nt], acc_);
-                }
-            }
-        if (!h_zero) {
-#pragma unroll
-            for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    const u32x4v w[2] = {Whh[h2_gru_idx(g, hb, sl, 0, lane)], Whh[h2_gru_idx(g, hb, sl, 1, lane)]};
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        f32x4 &acc_ = g == 0 ? gr[nt] : (g == 1 ? gz[nt] : gnh[nt]);
-                        acc_ = mfma_h2(w, hP[sl][nt], acc_);
-                    }
-                }
-        }
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const float rg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gr[nt][v] * c1));
-                const float zg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gz[nt][v] * c1));
-                const float ng =
-                    2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((gni[nt][v] + rg * gnh[nt][v]) * c2)) - 1.0f;
-#if ASG_H2_KEEP_H
-                const float hv = comp(hB[hb][nt], v);
-#else
-                // h from its planes (h_hi + h_lo = h * 2^sh to 2^-22 relative): the f32 copy
-                // is not kept through the gates (registers)
-                const int j = 4 * (hb & 1) + v;
-                const uint32_t dh = hP[hb >> 1][nt][0][j >> 1], dl = hP[hb >> 1][nt][1][j >> 1];
-                const f16x2v ph = __builtin_bit_cast(f16x2v, dh), pl = __builtin_bit_cast(f16x2v, dl);
-                const float hv = ((float)ph[j & 1] + (float)pl[j & 1]) * hun;
-#endif
-                hp[hb][nt][v] = ng + zg * (hv - ng);
-            }
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            if (ok[nt])
-                *reinterpret_cast<float4 *>(a.Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
-                    make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
-    }
-    ASG_STAMP(2);
-
-    // ---- fc2 (+ selection state) ---------------------------------------------------------
-    float m3 = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) m3 = absmax4(m3, hp[t][nt]);
-    m3 = wave_max_f32(m3);
-    const int s3 = h2_scale(m3, -90, 90 - sw[3]);
-    const int S3 = sw[3] + s3;
-    u32x4v hq[2][NT][2];
-    {
-        const float c3 = pow2f(s3);
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                float v8[8];
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) v8[4 * c + v] = hp[2 * sl + c][nt][v];
-                split2s(v8, c3, hq[sl][nt][0], hq[sl][nt][1]);
-            }
-    }
-    float best[NT];
-    int bj[NT];
-    uint64_t amask[NT][2];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        best[nt] = -__builtin_inff();
-        bj[nt] = 0x7fffffff;
-        amask[nt][0] = amask[nt][1] = 0;
-    }
-    const float un3 = pow2f(-S3);
-    int lane2 = lane;
-    // the fused rollout recomputes the lane's W2 address here each tile (hoisted, it was
-    // spilled, and its reload waited for every store of the tile)
-    if (ALLAV) asm volatile("" : "+v"(lane2));
-    const lds_u4p W2s = (lds_u4p)(Wl + h2_w2_off(a.nout));
-    const u32x4v *W2g = a.pk + 1 + h2_w1_f4(a.K) + 2 * kH2GruF4;
-    for (int c0 = 0; c0 < nct; c0 += 4) {
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = c0 + cc;
-            if (c >= nct) break;
-            const int j0 = 16 * c + 4 * q;
-            uint32_t av[NT];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const uint32_t w = avw[cc][nt];
-                av[nt] = ((w & 0xffu) != 0) | (((w >> 8) & 0xffu) != 0) << 1 | (((w >> 16) & 0xffu) != 0) << 2 |
-                         ((w >> 24) != 0) << 3;
-                if (c + 4 < nct) avw[cc][nt] = load_av(c + 4, nt);  // the ring: 4 tiles ahead
-            }
-            f32x4 a2[NT];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) a2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int sl = 0; sl < 2; ++sl) {
-                u32x4v w[2];
-#pragma unroll
-                for (int pl = 0; pl < 2; ++pl)
-                    w[pl] = W2L ? W2s[h2_w2_idx(c, sl, pl, lane2)] : W2g[h2_w2_idx(c, sl, pl, lane2)];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) a2[nt] = mfma_h2(w, hq[sl][nt], a2[nt]);
-            }
-            const f32x4 bq = Bs[80 + 4 * c + q];  // b2[16 c + 4 q ..]
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const f32x4 qv = a2[nt] * un3 + bq;
-                if (a.Q && ok[nt])
-                    *reinterpret_cast<float4 *>(a.Q + rows[nt] * a.nout + j0) = make_float4(qv[0], qv[1], qv[2], qv[3]);
-                if (SEL) {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        // a lane meets its tasks in increasing j, so torch.max order reduces
-                        // to: the first candidate, then strictly greater, or the first NaN
-                        const int j = j0 + v;
-                        const float x = ((av[nt] >> v) & 1u) ? qv[v] : -__builtin_inff();
-                        const bool b = (bj[nt] == 0x7fffffff) | ((best[nt] == best[nt]) & !(x <= best[nt]));
-                        best[nt] = b ? x : best[nt];
-                        bj[nt] = b ? j : bj[nt];
-                    }
-                    amask[nt][0] |= (uint64_t)av[nt] << (4 * (c & 15));
-                }
-            }
-        }
-    }
-    ASG_STAMP(3);
-    if (SEL) select_finish<false, NT>(best, bj, amask, rows, ok, oidx, nct, sel, q);
-    ASG_STAMP(7);
-}
-
-// One wave, 32 agent rows (NT = 2 row tiles of 16): fc1 -> GRU -> fc2 (+ selection).
-// Wl: the LDS stage; W2L: W2 planes staged (else read through L2).  sx_obs: the wave's
-// running fc1 input scale.
-template <int NT, bool SEL, bool W2L>
-__device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, const u32x4v *Wl, int &sx_obs,
-                                              const int (&sw)[4]) {
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    if (row0 >= a.R) return;
-    ASG_STAMP(0);
-    int64_t rows[NT];
-    bool ok[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        rows[nt] = row0 + 16 * nt + r;
-        ok[nt] = rows[nt] < a.R;
-    }
-    const lds_u4p Wih = (lds_u4p)Wl, Whh = (lds_u4p)(Wl + kH2GruF4);
-    const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);  // biases
-    const u32x4v *W1g = a.pk + 1;
-    const float *xr[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) xr[nt] = a.X + (ok[nt] ? rows[nt] : 0) * a.xs;
-    const int nsl = a.K >> 5;
-
-    // observation slices of the main fc1 loop (k >= P): a ring of ASG_H2_XBUF slices in
-    // flight per wave, the first ones issued right behind the one-hot prefix loads
-    auto load_x = [&](int sl, float4 (&xv)[2][NT]) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                xv[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + 32 * sl + 16 * c + 4 * q);
-    };
-    auto load_pa = [&](int t4, float4 (&pa)[4][NT]) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                pa[c][nt] = (t4 + c < a.P / 16) ? *reinterpret_cast<const float4 *>(xr[nt] + 16 * (t4 + c) + 4 * q)
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-    const int s0 = a.P >> 5;
-    float4 xbuf[kH2XBuf][2][NT];
-    float4 pa[4][NT];
-    if (a.P > 0) load_pa(0, pa);
-    // main-loop slice order: with the mock env's obs layout [onehot | B(k+1) | .. | B(k+L)]
-    // (K = P (L + 1)), task chunk u outer and lookahead block l inner -- the order in which
-    // the fused rollout kernel generates them (one set of bump parameters per chunk)
-    const int nmain = nsl - s0;
-    const bool perm = s0 > 0 && nmain % s0 == 0;
-    const int nblk = perm ? nmain / s0 : 1;
-    auto sl_of = [&](int idx) { return perm ? (idx % nblk + 1) * s0 + idx / nblk : s0 + idx; };
-#pragma unroll
-    for (int b = 0; b < kH2XBuf; ++b)
-        if (b < nmain) load_x(sl_of(b), xbuf[b]);
-    // h_in fragments: needed from the GRU on, so issued behind the observations (or, with
-    // ASG_H2_LATE_H, after the fc1 main loop: 32 fewer VGPRs live through fc1)
-    float4 hB[4][NT];
-    auto load_h = [&]() {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs + 16 * t + 4 * q)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-#if !ASG_H2_LATE_H
-    load_h();
-#endif
-
-    // ---- one-hot prefix (see agent_rows): rows whose first P inputs are onehot(a) or zero
-    // add W1[:, a] (W1T, f32) instead of running those slices' MFMAs
-    int pos[NT];
-    bool onehot = false;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) pos[nt] = -1;
-    if (a.P > 0) {
-        bool bad = false;
-        for (int t4 = 0; t4 < a.P / 16; t4 += 4) {  // P % 64 == 0, or P / 16 < 4 guarded
-            if (t4 > 0) load_pa(t4, pa);
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float v = comp(pa[c][nt], e);
-                        const bool one = v == 1.0f;
-                        bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
-                        pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
-                    }
-        }
-        bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const uint64_t mk = __ballot(pos[nt] >= 0);
-            const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull, g3 = mk >> 48;
-            rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
-            int p = pos[nt];
-            p = max(p, __shfl_xor(p, 16));
-            p = max(p, __shfl_xor(p, 32));
-            pos[nt] = p;
-        }
-        onehot = rows_ok && __ballot(bad) == 0;
-    }
-    // ---- fc1 on split f16 MFMAs (accumulators from the one-hot column W1[:, a] scaled like
-    // the products; the bias is added unscaled at the end) -------------------------------
-    f32x4 acc[4][NT];
-    int sx = sx_obs;
-    float tmax = 0.f;
-#if ASG_H2_GATHER_TAIL
-    // the one-hot columns W1[:, a] are gathered now and added after the main loop: their
-    // L2 latency hides under the observation MFMAs instead of delaying the first one
-    float4 g1[4][NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-            g1[mt][nt] = (onehot && pos[nt] >= 0)
-                             ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-    for (int attempt = 0;; ++attempt) {
-        if (attempt > 0) {
-#pragma unroll
-            for (int b = 0; b < kH2XBuf; ++b)
-                if (b < nmain) load_x(sl_of(b), xbuf[b]);
-        }
-        const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
-#if ASG_H2_GATHER_TAIL
-        (void)scS;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#else
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const float4 g = (onehot && pos[nt] >= 0)
-                                     ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
-            }
-#endif
-#ifdef ASG_STAMP_FC1
-        if (attempt == 0) {
-            // wait for the gathered W1 columns here so the stamp measures their latency
-            float z = 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) z += acc[mt][0][0];
-            if (z == 12345.f) acc[0][0][1] += 1.f;
-            ASG_STAMP(5);
-        }
-#endif
-        float m = 0.f;
-        auto slice = [&](int sl, const float4 (&xv)[2][NT], bool lds) {
-            u32x4v xp[NT][2];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                m = absmax4(absmax4(m, xv[0][nt]), xv[1][nt]);
-                const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
-                                     xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
-                split2s(x8, scx, xp[nt][0], xp[nt][1]);
-            }
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                u32x4v w[2];
-                if (lds) {
-                    const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
-#pragma unroll
-                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[h2_w1_idx(sl - s0, mt, pl, lane)];
-                } else {
-#pragma unroll
-                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
-                }
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
-            }
-        };
-        // slices below P / 32 (a tile whose prefix is not one-hot): W1 planes through L2
-        for (int sl = 0; sl < (onehot ? 0 : s0); ++sl) {
-            float4 xv[2][NT];
-            load_x(sl, xv);
-            slice(sl, xv, false);
-        }
-        const int s_l2 = s0 + a.w1_lds;  // first slice read through L2
-        for (int i0 = 0; i0 < nmain; i0 += kH2XBuf) {
-#pragma unroll
-            for (int b = 0; b < kH2XBuf; ++b) {
-                if (i0 + b < nmain) {
-                    const int sl = sl_of(i0 + b);
-                    if (sl < s_l2) slice(sl, xbuf[b], true);
-                    else slice(sl, xbuf[b], false);
-                    if (i0 + b + kH2XBuf < nmain) load_x(sl_of(i0 + b + kH2XBuf), xbuf[b]);
-                }
-            }
-        }
-#if ASG_H2_LATE_H
-        if (attempt == 0) load_h();
-#endif
-        tmax = wave_max_f32(m);
-#ifdef ASG_STAMP_FC1
-        if (attempt == 0) ASG_STAMP(6);
-#endif
-        // the split needs |x| * 2^sx < 2^15 (|h| <= 65504): otherwise redo at a smaller scale
-        if (!(tmax * scx >= 32768.f) || attempt > 0) break;
-        sx = h2_scale(tmax, -90, 90 - sw[0]);
-    }
-#if ASG_H2_CARRY_SX
-    // next tile's guess: this tile's own scale (grows back when values shrink)
-    sx_obs = h2_scale(tmax, -90, 90 - sw[0]);
-#endif
-    f32x4 xB[4][NT];
-    {
-        const float un = pow2f(-(sw[0] + sx));
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const f32x4 bb = Bs[4 * mt + q];  // b1[16 mt + 4 q ..]
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-#if ASG_H2_GATHER_TAIL
-                // unscaled products + the gathered one-hot column + bias
-                const f32x4 gv = f32x4{g1[mt][nt].x, g1[mt][nt].y, g1[mt][nt].z, g1[mt][nt].w};
-#pragma unroll
-                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + gv[v] + bb[v], 0.f);
-#else
-#pragma unroll
-                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
-#endif
-            }
-        }
-    }
-    ASG_STAMP(1);
-
-    h2_tail<NT, SEL, W2L, false>(a, Wl, sw, row0, rows, ok, hB, xB);
-}
-
-// LDS image of the persistent h2 kernels (h2_w1_off): GRU planes, biases (b1 | b_ir+b_hr |
-// b_iz+b_hz | b_in | b_hn | b2), W2 planes (W2L), the first w1_lds W1 slices from P / 32 on;
-// sw = the four matrices' scale exponents (packed header)
-template <bool W2L>
-__device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s_h2, int (&sw)[4]) {
-    const u32x4v *gru = a.pk + 1 + h2_w1_f4(a.K);  // W_ih, W_hh, W2 are contiguous after W1
-    for (int64_t i = threadIdx.x; i < 2 * kH2GruF4; i += blockDim.x) s_h2[i] = gru[i];
-    float *bs = reinterpret_cast<float *>(s_h2 + 2 * kH2GruF4);
-    for (int i = threadIdx.x; i < 5 * kHid + a.nout; i += blockDim.x) {
-        const int blk = i >> 6, u = i & 63;
-        float v;
-        if (blk == 0) v = a.b1[u];
-        else if (blk == 1) v = a.bih[u] + a.bhh[u];
-        else if (blk == 2) v = a.bih[kHid + u] + a.bhh[kHid + u];
-        else if (blk == 3) v = a.bih[2 * kHid + u];
-        else if (blk == 4) v = a.bhh[2 * kHid + u];
-        else v = a.b2[i - 5 * kHid];
-        bs[i] = v;
-    }
-    if (W2L) {
-        const int64_t n2 = h2_w2_f4(a.nout);
-        for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) s_h2[h2_w2_off(a.nout) + i] = gru[2 * kH2GruF4 + i];
-    }
-    {
-        const u32x4v *w1 = a.pk + 1 + h2_w1_idx(a.P >> 5, 0, 0, 0);
-        const int64_t n1 = (int64_t)a.w1_lds * 4 * 2 * 64, off = h2_w1_off(a.nout, W2L);
-        for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) s_h2[off + i] = w1[i];
-    }
-    const int4 hdr = *reinterpret_cast<const int4 *>(a.pk);
-    sw[0] = hdr.x;
-    sw[1] = hdr.y;
-    sw[2] = hdr.z;
-    sw[3] = hdr.w;
-}
-
-// Persistent: one 512-thread workgroup per CU stages the LDS image (h2_w1_off), then its 8
-// waves walk 256-row tiles.
-template <bool SEL, bool W2L>
-__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
-rnn_agent_h2_kernel(H2Args a) {
-    constexpr int NT = kH2NT;
-    extern __shared__ u32x4v s_h2[];
-    int sw[4];
-    h2_stage<W2L>(a, s_h2, sw);
-    __syncthreads();
-    int sx_obs = kH2SxInit;
-    const int64_t ntiles = (a.R + kH2Waves * (16 * NT) - 1) / (kH2Waves * (16 * NT));
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t row0 = (tile * kH2Waves + (threadIdx.x >> 6)) * (16 * NT);
-        agent_rows_h2<NT, SEL, W2L>(row0, a, s_h2, sx_obs, sw);
-    }
-}
-
-// ---- h2 packing: max|W| -> scale exponent, then the scaled f16 planes ------------------
-__global__ void h2_exp_kernel(const float *W, int64_t n, int *out) {
-    __shared__ float s_m[16];
-    float m = 0.f;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, __builtin_fabsf(W[i]));
-    m = wave_max_f32(m);
-    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, s_m[w]);
-        *out = h2_scale(m, -60, 60);
-    }
-}
-// W [C][Kin] row-major -> planes of tiles (ct, sl): lane l = (r, q) holds the 8 values
-// W[16 ct + r][32 sl + gru_x3_k(0, q, j)] * 2^s split into (h, l); order: slice-major
-// (W1: [sl][ct]) or unit-major (GRU [ct = 4 g + hb][sl], W2 [c][sl]).
-__global__ void h2_pack_kernel(const float *W, int C, int Kin, int nct, int nsl, int slice_major, const int *sexp,
-                               u32x4v *out) {
-    const int64_t total = (int64_t)nct * nsl * 64;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    const int lane = (int)(i & 63);
-    const int64_t tix = i >> 6;
-    const int ct = slice_major ? (int)(tix % nct) : (int)(tix / nsl);
-    const int sl = slice_major ? (int)(tix / nct) : (int)(tix % nsl);
-    const int row = 16 * ct + (lane & 15), q = lane >> 4;
-    const float sc = pow2f(*sexp);
-    float x[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int k = 32 * sl + gru_x3_k(0, q, j);
-        x[j] = (row < C && k < Kin) ? W[(int64_t)row * Kin + k] * sc : 0.f;
-    }
-    u32x4v h, l;
-    split2(x, h, l);
-    const int64_t o = (slice_major ? ((int64_t)sl * nct + ct) : ((int64_t)ct * nsl + sl)) * 2 * 64 + lane;
-    out[o] = h;
-    out[o + 64] = l;
-}
-
-// One-hot input prefix: the first P = n_out inputs may be a one-hot block (the mock env's
-// obs starts with onehot(previous task), mock_constellation_env.py:141-152).  The pack adds
-// W1^T of those P columns ([P][64], one float4 per 4 hidden units), and a wave tile whose
-// prefix rows are verified one-hot (or zero) adds W1[:, a] instead of running the prefix
-// chunks' MFMAs.  P = 0 (no section) unless n_out % 16 == 0 and n_out < K.
+// One-hot input prefix of the f32 / split-bf16 kernels: the first P = n_out inputs may be a
+// one-hot block (the mock env's obs starts with onehot(previous task),
+// mock_constellation_env.py:141-152).  The pack adds W1^T of those P columns ([P][64], one
+// float4 per 4 hidden units), and a wave tile whose prefix rows are verified one-hot (or
+// zero) adds W1[:, a] instead of running the prefix chunks' MFMAs.  P = 0 (no section) unless
+// n_out % 16 == 0 and n_out < K.
 static int onehot_prefix(int K, int nout) { return (nout % 16 == 0 && nout < K && K % 32 == 0) ? nout : 0; }
 // W2 as three bf16 planes for the split fc2: hi + mid planes [c][sl 2][plane 2][lane 64],
 // then the lo planes [c][sl 2][lane 64] (x 8 bf16)
@@ -1683,13 +814,15 @@ static int64_t w2x3_f4(int nout) { return ASG_AGENT_FC2_X3 ? (int64_t)((nout + 1
 // W1 as three bf16 planes for the split fc1 ([K / 32][mt 4][plane 3][lane 64] x 8 bf16)
 static int64_t w1x3_f4(int K) { return ASG_AGENT_FC1_X3 && K % 32 == 0 ? (int64_t)(K / 32) * 4 * 3 * 64 : 0; }
 
-// float4 count of the packed weight buffer
+// float4 count of the packed weight buffer: the split-f16 layout (asg_h2.hip) for every shape
+// it takes, else the f32 / split-bf16 layout below
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn) {
+    if (h2_ok(K, nout)) return h2_packed_f4(K, nout, use_rnn);
     const int64_t w1 = (int64_t)((K + 15) / 16) * 4 * 64;
     const int64_t wr = use_rnn ? 2 * kGruF4 : 4 * 4 * 64;
     const int64_t w2 = 4 * (int64_t)((nout + 15) / 16) * 64;
     const int64_t w1t = (int64_t)onehot_prefix(K, nout) * 16;
-    return w1 + wr + w2 + w1t + w1x3_f4(K) + w2x3_f4(nout) + rnn_agent_h2_f4(K, nout, use_rnn);
+    return w1 + wr + w2 + w1t + w1x3_f4(K) + w2x3_f4(nout);
 }
 
 // W_ih / W_hh [3 * 64][64] -> kGruX3F4 x 8 bf16 (gru_x3_idx order, k order gru_x3_k)
@@ -1741,8 +874,14 @@ __global__ void pack_w1t_kernel(const float *W1, int K, int P, float *out) {
     if (i < P * kHid) out[i] = W1[(int64_t)(i % kHid) * K + i / kHid];
 }
 
+hipError_t launch_w1t_pack(const float *W1, int K, int P, float *out, hipStream_t s) {
+    if (P > 0) hipLaunchKernelGGL(pack_w1t_kernel, dim3((P * kHid + 255) / 256), dim3(256), 0, s, W1, K, P, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
                                  int use_rnn, float4 *packed, hipStream_t s) {
+    if (h2_ok(K, nout)) return launch_h2_pack(W1, Wih, Whh, W2, K, nout, use_rnn, packed, s);
     float4 *p = packed;
     auto one = [&](const float *W, int C, int KK) {
         const int64_t n = (int64_t)((KK + 15) / 16) * ((C + 15) / 16) * 64;
@@ -1766,9 +905,7 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     }
     one(W2, nout, kHid);
     const int P = onehot_prefix(K, nout);
-    if (P)
-        hipLaunchKernelGGL(pack_w1t_kernel, dim3((P * kHid + 255) / 256), dim3(256), 0, s, W1, K, P,
-                           reinterpret_cast<float *>(p));
+    (void)launch_w1t_pack(W1, K, P, reinterpret_cast<float *>(p), s);
     p += (int64_t)P * 16;
     if (const int64_t n3 = w1x3_f4(K))
         hipLaunchKernelGGL(pack_w1_x3_kernel, dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, s, W1, K,
@@ -1777,35 +914,14 @@ hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float 
     if (w2x3_f4(nout))
         hipLaunchKernelGGL(pack_w2_x3_kernel, dim3((unsigned)(((nout + 15) / 16 * 128 + 255) / 256)), dim3(256), 0, s,
                            W2, nout, reinterpret_cast<u32x4v *>(p));
-    p += w2x3_f4(nout);
-    if (h2_shape(K, nout, use_rnn)) {
-        // split-f16 planes of all four matrices, each scaled by its own power of two
-        u32x4v *h2 = reinterpret_cast<u32x4v *>(p);
-        int *hdr = reinterpret_cast<int *>(h2);
-        const float *mats[4] = {W1, Wih, Whh, W2};
-        const int64_t sizes[4] = {(int64_t)kHid * K, 3 * kHid * kHid, 3 * kHid * kHid, (int64_t)nout * kHid};
-        for (int i = 0; i < 4; ++i)
-            hipLaunchKernelGGL(h2_exp_kernel, dim3(1), dim3(1024), 0, s, mats[i], sizes[i], hdr + i);
-        auto pack = [&](const float *W, int C, int Kin, int nct, int nsl, int smaj, int e, u32x4v *out) {
-            const int64_t n = (int64_t)nct * nsl * 64;
-            hipLaunchKernelGGL(h2_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, C, Kin, nct, nsl,
-                               smaj, hdr + e, out);
-        };
-        u32x4v *o = h2 + 1;
-        pack(W1, kHid, K, 4, K / 32, 1, 0, o);
-        o += h2_w1_f4(K);
-        pack(Wih, 3 * kHid, kHid, 12, 2, 0, 1, o);
-        o += kH2GruF4;
-        pack(Whh, 3 * kHid, kHid, 12, 2, 0, 2, o);
-        o += kH2GruF4;
-        pack(W2, nout, kHid, nout / 16, 2, 0, 3, o);
-    }
     return hipGetLastError();
 }
 
-// CUs a stream may run on (hipExtStreamCreateWithCUMask): the persistent grid is sized to
+// CUs a stream may run on (hipExtStreamCreateWithCUMask): the persistent grids are sized to
 // them, so a CU-masked agent stream leaves the other CUs to a concurrent env-step stream.
-static int stream_cus(hipStream_t s, int ncu) {
+int stream_cus(hipStream_t s) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     static thread_local hipStream_t last = nullptr;
     static thread_local int last_n = 0;
     if (!s) return ncu;
@@ -1822,20 +938,10 @@ static int stream_cus(hipStream_t s, int ncu) {
 }
 
 // ASG_AGENT_ONEHOT=0 disables the one-hot prefix shortcut (A/B experiments)
-static bool onehot_prefix_enabled() {
+bool onehot_prefix_enabled() {
     static const int v = [] {
         const char *e = getenv("ASG_AGENT_ONEHOT");
         return e ? atoi(e) : 1;
-    }();
-    return v != 0;
-}
-
-// ASG_AGENT_KERNEL=x3 keeps the three-way bf16 / f32 kernel on shapes the split-f16 kernel
-// takes (A/B experiments); default: split f16
-static bool use_h2_kernel() {
-    static const int v = [] {
-        const char *e = getenv("ASG_AGENT_KERNEL");
-        return (e && strcmp(e, "x3") == 0) ? 0 : 1;
     }();
     return v != 0;
 }
@@ -1853,6 +959,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
                                 const float4 *packed, const float *b1, const float *bih, const float *bhh,
                                 const float *b2, int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel,
                                 hipStream_t s) {
+    if (h2_ok(K, nout)) return launch_h2_agent(X, xs, R, K, Hin, hs, packed, b1, bih, bhh, b2, nout, use_rnn, Hout, Q,
+                                               sel, s);
     const int64_t rows_per_block = 4 * kRowsPerWave;
     const int64_t blocks = (R + rows_per_block - 1) / rows_per_block;
     const float4 *W1p = packed;
@@ -1884,55 +992,8 @@ hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, co
                      nout > 256;
     // (the general-shape instantiation keeps the f32 W2 in that LDS slot)
     const bool fc2x3 = use_rnn && !gen && W2x3g && w2_lds == wr_f4 && w2hm_f4 <= w2_f4;
-    if (!gen && h2_shape(K, nout, use_rnn) && use_h2_kernel()) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        ncu = stream_cus(s, ncu);
-        H2Args ha;
-        ha.X = X;
-        ha.xs = xs;
-        ha.R = R;
-        ha.K = K;
-        const int P1 = onehot_prefix_enabled() ? onehot_prefix(K, nout) : 0;
-        ha.P = P1 % 32 == 0 ? P1 : 0;
-        ha.Hin = Hin;
-        ha.hs = hs;
-        ha.pk = reinterpret_cast<const u32x4v *>(packed + rnn_agent_packed_f4(K, nout, use_rnn) -
-                                                 rnn_agent_h2_f4(K, nout, use_rnn));
-        ha.W1T = W1Tg;
-        ha.b1 = b1;
-        ha.bih = bih;
-        ha.bhh = bhh;
-        ha.b2 = b2;
-        ha.nout = nout;
-        ha.Hout = Hout;
-        ha.Q = Q;
-        ha.sel = sa;
-        // LDS image: GRU planes, biases, then W2 planes when they fit, then as many W1 slices
-        // (from P / 32 on) as fit; what does not fit is read through L2
-        const int64_t base = h2_w2_off(nout);
-        const int64_t cap = (int64_t)(kLdsMax / 16);
-        const bool w2l = base + h2_w2_f4(nout) <= cap;
-        const int64_t w1off = h2_w1_off(nout, w2l);
-        const int64_t slices = K / 32 - ha.P / 32, fit = (cap - w1off) / (4 * 2 * 64);
-        ha.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
-        const size_t lds_b = (size_t)(w1off + (int64_t)ha.w1_lds * 4 * 2 * 64) * 16;
-        const int64_t ntiles = (R + kH2Waves * 16 * kH2NT - 1) / (kH2Waves * 16 * kH2NT);
-        const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
-#define LH_(SEL, W2L) \
-    hipLaunchKernelGGL((rnn_agent_h2_kernel<SEL, W2L>), dim3(grid), dim3(64 * kH2Waves), lds_b, s, ha)
-        if (sel) {
-            if (w2l) LH_(true, true); else LH_(true, false);
-        } else {
-            if (w2l) LH_(false, true); else LH_(false, false);
-        }
-#undef LH_
-        return hipGetLastError();
-    }
     if (use_lds_weights() && lds <= 160 * 1024) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        ncu = stream_cus(s, ncu);
+        const int ncu = stream_cus(s);
         const int64_t ntiles = (R + kLdsWaves * kRowsPerWave - 1) / (kLdsWaves * kRowsPerWave);
         const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
 #define LL_(RNN, SEL, GEN)                                                                                   \
@@ -1977,594 +1038,13 @@ hipError_t launch_rnn_agent_select(const float *X, int64_t xs, int64_t R, int K,
     return launch_rnn_agent_fwd(X, xs, R, K, Hin, hs, packed, b1, bih, bhh, b2, nout, use_rnn, Hout, Q, &sa, s);
 }
 
-// =====================================================================================
-// Fused rollout step (mock env, Philox bumps): the env transition at step k of every env
-// (actions at batch row ts: MockConstellationEnv.step, mock :116-162, with the runner's
-// batch updates -- what step_kernel does), then the RNNAgent forward + epsilon-greedy for
-// row ts + 1 on the observations that transition produces.  Those observation rows are
-// generated in the split-f16 MFMA operand layout (lane (r, q) holds tasks 16 c + 4 q + v of
-// each 32-task chunk), written to the batch, and consumed from registers: the agent never
-// reads them back from HBM (1 KB per agent row at 64 x 64).  One wave per env: agents are
-// lanes for the transition, then the env's n / 32 agent tiles run the h2 path.  Results
-// are bit-identical to step_kernel + rnn_agent_h2_kernel (same bump arithmetic, per-tile fc1
-// scale, slice order and tail).
-// =====================================================================================
-// The A/B switches below (NOSTORE / SKIP: timing-only builds with WRONG results; EARLY 1|2 and
-// NT: slower variants kept for the record) are refused unless the build says
-// it is a timing experiment: the product library never carries them.
-#if !defined(ASG_TIMING_EXPERIMENTS) && (defined(ASG_ROLLOUT_NOSTORE) || defined(ASG_ROLLOUT_SKIP) || \
-                                         defined(ASG_ROLLOUT_EARLY) || defined(ASG_ROLLOUT_NT))
-#error "rollout A/B switches (some give wrong results) need -DASG_TIMING_EXPERIMENTS"
-#endif
-// timing experiments only: skip the observation / one-hot / avail / beta stores (wrong batch)
-#ifndef ASG_ROLLOUT_NOSTORE
-#define ASG_ROLLOUT_NOSTORE 0
-#endif
-// timing experiments only (wrong results): 1 = the L2 fc1 slices read LDS slice 0 instead,
-// 2 = h_t not loaded (constants), 4 = the one-hot W1 columns not gathered (zeros),
-// 8 = the transition's actions / previous tasks not loaded (synthetic)
-#ifndef ASG_ROLLOUT_SKIP
-#define ASG_ROLLOUT_SKIP 0
-#endif
-#ifndef ASG_ROLLOUT_EARLY
-#define ASG_ROLLOUT_EARLY 4
-#endif
-// 1: streaming (nontemporal) stores for the batch rows.  Measured on MI355X boxes of this pool:
-// 0.78 ms on some, 0.89-0.93 ms on others, against 0.82-0.84 ms with plain stores everywhere
-// (the write acknowledgements the in-order vmcnt waits on take box-dependent paths), so off
-#ifndef ASG_ROLLOUT_NT
-#define ASG_ROLLOUT_NT 0
-#endif
-// 1: the transition's actions / previous tasks come through the scalar path (s_load, counted
-// by lgkmcnt): a vector load there sits behind the previous env's ~130 KB of row stores in the
-// in-order vmcnt queue and waits for all their write acknowledgements
-#ifndef ASG_ROLLOUT_SLOAD
-#define ASG_ROLLOUT_SLOAD 1
-#endif
-typedef const int __attribute__((address_space(4))) *cint_sp;
-// lane l < cnt receives the W dwords of element l of the wave-uniform array at base (read-only
-// in this launch: written by the previous launch on the stream, so the scalar cache, which
-// each dispatch starts invalidated, holds no stale line)
-// W dwords per lane (1: int32, 2: int64 as lo / hi), contiguous blocks of 16 lanes so the loads
-// merge into s_load_dwordx16
-template <int W, int CNT>
-__device__ __forceinline__ void sload_spread_n(const void *base, int (&x)[W]) {
-    const cint_sp p = (cint_sp)(uintptr_t)base;
-#pragma unroll
-    for (int w = 0; w < W; ++w) x[w] = 0;
-#pragma unroll
-    for (int l0 = 0; l0 < CNT; l0 += 16) {
-        int v[16 * W];
-#pragma unroll
-        for (int d = 0; d < 16 * W; ++d) v[d] = p[W * l0 + d];
-#pragma unroll
-        for (int l = 0; l < 16; ++l)
-#pragma unroll
-            for (int w = 0; w < W; ++w)
-                asm("v_writelane_b32 %0, %1, %2" : "+v"(x[w]) : "s"(v[W * l + w]), "n"(l0 + l));
-    }
-}
-// cnt is 64 or 32 (the fused rollout takes n % 32 == 0)
-template <int W>
-__device__ __forceinline__ void sload_spread(const void *base, int cnt, int (&x)[W]) {
-    if (cnt >= 64)
-        sload_spread_n<W, 64>(base, x);
-    else
-        sload_spread_n<W, 32>(base, x);
-}
-typedef long long i64x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void ro_st(float *p, float4 v) {
-    const f32x4 x{v.x, v.y, v.z, v.w};
-#if ASG_ROLLOUT_NT
-    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
-#else
-    *reinterpret_cast<f32x4 *>(p) = x;
-#endif
-}
-__device__ __forceinline__ void ro_st(int64_t *p, long long a, long long b) {
-    const i64x2v x{a, b};
-#if ASG_ROLLOUT_NT
-    __builtin_nontemporal_store(x, reinterpret_cast<i64x2v *>(p));
-#else
-    *reinterpret_cast<i64x2v *>(p) = x;
-#endif
-}
-struct RolloutArgs {
-    // the time-major batch rows the step touches, each a contiguous [E][..] slab
-    float *obs1;        // obs row ts + 1        [E][n][K]
-    float *beta1;       // beta row ts + 1       [E][n][m]   (may be NULL)
-    uint8_t *avail1;    // avail row ts + 1      [E][n][m]   (may be NULL)
-    int64_t *onehot0;   // actions_onehot row ts [E][n][m]   (may be NULL)
-    const int64_t *act0;  // actions row ts      [E][n]
-    float *rew0;        // rewards row ts        [E][n]      (may be NULL)
-    int64_t *prev1;     // prev_assigns row ts+1 [E][n]      (may be NULL)
-    uint8_t *term0;     // terminated row ts     [E]         (may be NULL)
-    int64_t *filled1;   // filled row ts + 1     [E]         (may be NULL)
-    // env state
-    int *prev;
-    double *returns;
-    const double *T_trans;
-    int *env_err;
-    double lambda_;
-    uint64_t seed;
-    int64_t env_base, E;
-    uint32_t episode, quirks;
-    int n, m, T, L, k, dense;
-    float wmin, wmax;
-    // agent
-    const u32x4v *pk;
-    const float *W1T, *Hin;
-    int64_t hs;
-    float *Hout;
-    int w1_lds;
-    float epsilon;
-    uint32_t k0, k1, counter;
-    int64_t row_base;
-    int64_t *act1;      // actions row ts + 1 [E][n] (the selection's output)
-    int *sel_err;
-    const float *b1, *bih, *bhh, *b2;
-    int64_t scratch_off;  // per-wave transition scratch in LDS (u32x4v units)
-};
-
-__host__ __device__ static inline int64_t rollout_scratch_bytes(int n, int m) {
-    return ((int64_t)4 * m + 4 * m + 4 * n + 15) / 16 * 16;
-}
-
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-}
-
-// the h2 tail's view of the agent arguments
-__device__ __forceinline__ H2Args rollout_h2args(const RolloutArgs &ra) {
-    H2Args a;
-    a.X = nullptr;
-    a.xs = 0;
-    a.R = ra.E * ra.n;
-    a.K = ra.m * (ra.L + 1);
-    a.P = ra.m;
-    a.Hin = ra.Hin;
-    a.hs = ra.hs;
-    a.pk = ra.pk;
-    a.W1T = ra.W1T;
-    a.b1 = ra.b1;
-    a.bih = ra.bih;
-    a.bhh = ra.bhh;
-    a.b2 = ra.b2;
-    a.nout = ra.m;
-    a.Hout = ra.Hout;
-    a.Q = nullptr;
-    a.sel = SelectArgs{nullptr, 0, 0, ra.n, ra.epsilon, ra.k0, ra.k1, ra.counter, ra.row_base, ra.act1,
-                       (int64_t)ra.n, 1, ra.sel_err};
-    a.w1_lds = ra.w1_lds;
-    return a;
-}
-
-template <bool W2L>
-__device__ __forceinline__ void rollout_rows(const RolloutArgs &ra, int64_t e, int sub, const EnvKey &key,
-                                             const float *s_scale, const int *s_act, const u32x4v *Wl,
-                                             const int (&sw)[4]) {
-    constexpr int NT = kH2NT;
-    const H2Args a = rollout_h2args(ra);
-    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
-    const int n = ra.n, m = ra.m, T = ra.T, L = ra.L, k = ra.k;
-    const int K = m * (L + 1);
-    const int U = m >> 5;
-    constexpr int RT = 16 * NT;  // rows per tile
-    const int64_t row0 = e * n + RT * sub;
-    int64_t rows[NT];
-    bool ok[NT];
-    int ia[NT], act[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        ia[nt] = RT * sub + 16 * nt + r;
-        rows[nt] = e * n + ia[nt];
-        ok[nt] = true;
-        act[nt] = s_act[ia[nt]];
-    }
-    // bit 1: the one-hot block's W1 columns, bit 2: the h_t rows, loaded before the tile's
-    // stores (gfx9's vmcnt retires memory ops in order: a load issued behind the observation
-    // stores waits for their write acknowledgements)
-#if ASG_ROLLOUT_EARLY & 1
-    float4 g0[4][NT];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            g0[t][nt] = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * t + 4 * q);
-#endif
-#if ASG_ROLLOUT_EARLY & 2
-    float4 hB[4][NT];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            hB[t][nt] = a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-#if ASG_ROLLOUT_EARLY & 4
-    // bit 4: fc1's accumulators start from the one-hot block's W1 columns, gathered (and
-    // consumed) before the tile's prefix stores; a rescaled retry gathers them again
-    f32x4 acc[4][NT];
-    int sx = kH2SxInit;
-    {
-        const float scS = pow2f(sw[0] + sx);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
-                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
-            }
-    }
-#endif
-    // obs block 0 = onehot(a) (row ts + 1), actions_onehot (row ts), avail = 1 (row ts + 1)
-    for (int u = 0; u < (ASG_ROLLOUT_NOSTORE ? 0 : U); ++u)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                const int j0 = 32 * u + 16 * c + 4 * q;
-                const int aa = act[nt];
-                ro_st(ra.obs1 + rows[nt] * K + j0, make_float4(aa == j0, aa == j0 + 1, aa == j0 + 2, aa == j0 + 3));
-                if (ra.onehot0) {
-                    ro_st(ra.onehot0 + rows[nt] * m + j0, aa == j0, aa == j0 + 1);
-                    ro_st(ra.onehot0 + rows[nt] * m + j0 + 2, aa == j0 + 2, aa == j0 + 3);
-                }
-            }
-    // avail rows of the tile: RT contiguous rows of m bytes, all 1 -- full 16-B lanes
-    if (ra.avail1 && !ASG_ROLLOUT_NOSTORE) {
-        uint8_t *ab = ra.avail1 + (e * n + RT * sub) * m;
-        int off0 = 16 * lane;
-        asm volatile("" : "+v"(off0));  // not hoisted: a per-lane 64-bit address kept across loops spilled
-        for (int off = off0; off < RT * m; off += 64 * 16)
-            *reinterpret_cast<uint4 *>(ab + off) = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
-    }
-    // ---- fc1 on the generated observation blocks 1..L (times k + 1 .. k + L) -------------
-    BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
-    bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
-    const lds_f4v Bs = (lds_f4v)(Wl + 2 * kH2GruF4);
-    const u32x4v *W1g = a.pk + 1;
-    const int s0 = U, s_l2 = s0 + a.w1_lds;
-#if !(ASG_ROLLOUT_EARLY & 4)
-    f32x4 acc[4][NT];
-    int sx = kH2SxInit;
-#endif
-    for (int attempt = 0;; ++attempt) {
-        const float scx = pow2f(sx), scS = pow2f(sw[0] + sx);
-#if ASG_ROLLOUT_EARLY & 4
-        if (attempt > 0)
-#endif
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-#if ASG_ROLLOUT_EARLY & 1
-                const float4 g = g0[mt][nt];
-#elif ASG_ROLLOUT_SKIP & 4
-                const float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-#else
-                const float4 g = *reinterpret_cast<const float4 *>(a.W1T + act[nt] * kHid + 16 * mt + 4 * q);
-#endif
-                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
-            }
-        float mx = 0.f;
-        for (int u = 0; u < U; ++u) {
-            // bump parameters of the lane's 16 (row, task) pairs of this chunk
-            Bump32 bp[2][4][NT];
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-#if ASG_BUMP_PAIR2
-#pragma unroll
-                    for (int v = 0; v < 4; v += 2) {  // pairs (j, j + 1) share one Philox call (m even)
-                        const int j = 32 * u + 16 * c + 4 * q + v;
-                        philox_bump32x2(key, ra.episode, ia[nt] * m + j, s_scale[j], s_scale[j + 1], bsh, ra.dense != 0,
-                                        bp[c][v][nt], bp[c][v + 1][nt]);
-                    }
-#else
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int j = 32 * u + 16 * c + 4 * q + v;
-                        bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + j, s_scale[j], bsh, ra.dense != 0);
-                    }
-#endif
-                }
-            for (int l = 1; l <= L; ++l) {
-                const int t = k + l;
-                float4 xv[2][NT];
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        float vv[4];
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) vv[v] = (t < T) ? bump32_at(bp[c][v][nt], t) : 0.0f;
-                        xv[c][nt] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-                        if (attempt == 0 && !ASG_ROLLOUT_NOSTORE) {
-                            const int j0 = 32 * u + 16 * c + 4 * q;
-                            ro_st(ra.obs1 + rows[nt] * K + m * l + j0, xv[c][nt]);
-                            if (l == 1 && ra.beta1) ro_st(ra.beta1 + rows[nt] * m + j0, xv[c][nt]);
-                        }
-                    }
-                // the h2 kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
-                const int sl = l * U + u;
-                u32x4v xp[NT][2];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) {
-                    mx = absmax4(absmax4(mx, xv[0][nt]), xv[1][nt]);
-                    const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
-                                         xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
-                    split2s(x8, scx, xp[nt][0], xp[nt][1]);
-                }
-                // two copies of the MFMA block: merged after an LDS-or-global select, the MFMAs
-                // would wait for vmcnt(0) -- every observation store of the tile -- each slice
-                auto mma = [&](bool lds) {
-#pragma unroll
-                    for (int mt = 0; mt < 4; ++mt) {
-                        u32x4v w[2];
-                        if (lds) {
-                            const lds_u4p W1s = (lds_u4p)(Wl + h2_w1_off(a.nout, W2L));
-#pragma unroll
-                            for (int pl = 0; pl < 2; ++pl)
-                                w[pl] = W1s[h2_w1_idx((ASG_ROLLOUT_SKIP & 1) && sl >= s_l2 ? 0 : sl - s0, mt, pl, lane)];
-                        } else {
-#pragma unroll
-                            for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[h2_w1_idx(sl, mt, pl, lane)];
-                        }
-#pragma unroll
-                        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
-                    }
-                };
-                if (sl < s_l2 || (ASG_ROLLOUT_SKIP & 1))
-                    mma(true);
-                else
-                    mma(false);
-            }
-        }
-        const float tmax = wave_max_f32(mx);
-        if (!(tmax * scx >= 32768.f) || attempt > 0) break;
-        sx = h2_scale(tmax, -90, 90 - sw[0]);
-    }
-#if !(ASG_ROLLOUT_EARLY & 2)
-    // h_t rows, issued after fc1 like the h2 kernel
-    float4 hB[4][NT];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-            hB[t][nt] = (ASG_ROLLOUT_SKIP & 2) ? make_float4(0.5f, 0.25f, -0.5f, 0.125f)
-                        : a.Hin ? *reinterpret_cast<const float4 *>(a.Hin + rows[nt] * a.hs + 16 * t + 4 * q)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-    f32x4 xB[4][NT];
-    {
-        const float un = pow2f(-(sw[0] + sx));
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const f32x4 bb = Bs[4 * mt + q];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
-        }
-    }
-    h2_tail<NT, true, W2L, true>(a, Wl, sw, row0, rows, ok, hB, xB);
-}
-
-template <bool W2L>
-__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
-rollout_h2_kernel(RolloutArgs ra) {
-    extern __shared__ u32x4v s_h2[];
-    int sw[4];
-    h2_stage<W2L>(rollout_h2args(ra), s_h2, sw);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n = ra.n, m = ra.m, T = ra.T, k = ra.k;
-    char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
-    float *s_scale = reinterpret_cast<float *>(scr);
-    int *s_cnt = reinterpret_cast<int *>(s_scale + m);
-    int *s_act = s_cnt + m;
-    const int64_t GW = (int64_t)gridDim.x * kH2Waves;
-    for (int64_t e0 = (int64_t)blockIdx.x * kH2Waves + wv; e0 < ra.E; e0 += GW) {
-        // addresses are recomputed from e each env: strength-reduced per-lane pointers carried
-        // across the env loop were spilled around the tile loop, and their reloads waited for
-        // every store of the env
-        int64_t e = e0;
-        asm volatile("" : "+s"(e));
-        const EnvKey key = env_key(ra.seed, ra.env_base + e);
-        // ---- transition (lane = agent): counts, rewards, returns (step_kernel's arithmetic)
-        for (int j = lane; j < m; j += 64) {
-            s_scale[j] = philox_task_scale(key, ra.episode, j);
-            s_cnt[j] = 0;
-        }
-        wave_lds_fence();
-        int err = 0;
-        for (int i0 = 0; i0 < n; i0 += 64) {
-            const int i = i0 + lane;
-#if ASG_ROLLOUT_SLOAD
-            int av[2];
-            sload_spread<2>(ra.act0 + e * n + i0, n - i0 < 64 ? n - i0 : 64, av);
-            if (i >= n) continue;
-            const int64_t a64 = (ASG_ROLLOUT_SKIP & 8)
-                                    ? (int64_t)((i * 7 + (int)e) % m)
-                                    : (int64_t)(((uint64_t)(uint32_t)av[1] << 32) | (uint32_t)av[0]);
-#else
-            if (i >= n) continue;
-            const int64_t a64 = (ASG_ROLLOUT_SKIP & 8) ? (int64_t)((i * 7 + (int)e) % m) : ra.act0[e * n + i];
-#endif
-            int ai = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
-            if (ai < 0) err = ASG_E_ACTION_RANGE;
-            ai = ai < 0 ? 0 : ai;
-            s_act[i] = ai;
-            atomicAdd(&s_cnt[ai], 1);
-        }
-        wave_lds_fence();
-        double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
-        for (int i0 = 0; i0 < n; i0 += 64) {
-            const int i = i0 + lane;
-            double rr = 0.0;
-#if ASG_ROLLOUT_SLOAD
-            int pv[1];
-            sload_spread<1>(ra.prev + e * n + i0, n - i0 < 64 ? n - i0 : 64, pv);
-            // the invariant scalar loads carry no memory ordering: this barrier (fed by their
-            // values) keeps the stores of the same prev row below behind them
-            asm volatile("" : "+v"(pv[0])::"memory");
-#endif
-            if (i < n) {
-                const int j = s_act[i];
-#if ASG_ROLLOUT_SLOAD
-                const int p = (ASG_ROLLOUT_SKIP & 8) ? (i % m) : pv[0];
-#else
-                const int p = (ASG_ROLLOUT_SKIP & 8) ? (i % m) : ra.prev[e * n + i];
-#endif
-                const Bump32 b =
-                    philox_bump32(key, ra.episode, i * m + j, s_scale[j], T, ra.wmin, ra.wmax, ra.dense != 0);
-                const double beta = bump64_at(b, k);
-                const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
-                const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
-                const double bh = beta - ra.lambda_ * pen;
-                rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
-                if (ra.rew0) ra.rew0[e * n + i] = (float)rr;
-                ra.prev[e * n + i] = j;
-                if (ra.prev1) ra.prev1[e * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
-            }
-            const int lo = __double2loint(rr), hi = __double2hiint(rr);
-            const int cnt = n - i0 < 64 ? n - i0 : 64;
-            for (int l2 = 0; l2 < cnt; ++l2)
-                sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
-        }
-        wave_lds_fence();
-        err = wave_or_i32(err);
-        if (lane == 0) {
-            ra.returns[e] += sum;
-            bool term = k + 1 >= T;
-            if (ra.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
-            if (ra.term0) ra.term0[e] = term;
-            if (ra.filled1) ra.filled1[e] = 1;
-            if (err) atomicCAS(ra.env_err, 0, err);
-        }
-        // ---- agent + selection for row ts + 1, tile by tile
-        for (int sub = 0; sub < n / (16 * kH2NT); ++sub) rollout_rows<W2L>(ra, e, sub, key, s_scale, s_act, s_h2, sw);
-        wave_lds_fence();  // the next env reuses the scratch
-    }
-}
-
-// shapes the fused rollout takes (the h2 agent shape with the mock env's obs layout)
-bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn) {
-    return h2_shape(K, nout, use_rnn) && use_h2_kernel() && onehot_prefix_enabled() && nout == st.m &&
-           st.m % 32 == 0 && st.n % 32 == 0 && K == st.m * (st.L + 1) && st.L >= 1;
-}
-
-// LDS plan of the fused rollout: GRU planes, biases, W2 (when it fits), as many fc1 slices as
-// fit, then the per-wave transition scratch
-struct RolloutLds {
-    bool w2l;
-    int w1_lds, l2_slices;
-    int64_t scratch_off;
-    size_t bytes;
-};
-static RolloutLds rollout_lds_plan(int n, int m, int L) {
-    constexpr int64_t kCap = 160 * 1024 / 16;
-    const int K = m * (L + 1), nout = m;
-    RolloutLds p{};
-    const int64_t scr_f4 = (rollout_scratch_bytes(n, m) * kH2Waves + 15) / 16;
-    p.w2l = h2_w2_off(nout) + h2_w2_f4(nout) + scr_f4 <= kCap;
-    const int64_t w1off = h2_w1_off(nout, p.w2l);
-    const int64_t slices = K / 32 - nout / 32, fit = (kCap - scr_f4 - w1off) / (4 * 2 * 64);
-    p.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
-    p.l2_slices = (int)(slices - p.w1_lds);
-    p.scratch_off = w1off + (int64_t)p.w1_lds * 4 * 2 * 64;
-    p.bytes = (size_t)(p.scratch_off + scr_f4) * 16;
-    return p;
-}
-
-int rollout_l2_slices(int n, int m, int L) {
-    if (n <= 0 || m <= 0 || L < 1 || m > 256 || n % 32 || m % 32) return -1;
-    EnvState st{};
-    st.n = n;
-    st.m = m;
-    st.L = L;
-    if (!rollout_shape_ok(st, m * (L + 1), m, 1)) return -1;
-    return rollout_lds_plan(n, m, L).l2_slices;
-}
-
-hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
-                                      const float4 *packed, const float *b1, const float *bih, const float *bhh,
-                                      const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,
-                                      uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s) {
-    (void)ts;
-    const int K = st.m * (st.L + 1), nout = st.m;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    ncu = stream_cus(s, ncu);
-    RolloutArgs ra{};
-    ra.obs1 = sl.obs1;
-    ra.beta1 = sl.beta1;
-    ra.avail1 = sl.avail1;
-    ra.onehot0 = sl.onehot0;
-    ra.act0 = sl.act0;
-    ra.rew0 = sl.rew0;
-    ra.prev1 = sl.prev1;
-    ra.term0 = sl.term0;
-    ra.filled1 = sl.filled1;
-    ra.act1 = sl.act1;
-    ra.prev = st.prev;
-    ra.returns = st.returns;
-    ra.T_trans = st.T_trans;
-    ra.env_err = st.err;
-    ra.lambda_ = st.lambda_;
-    ra.seed = st.seed;
-    ra.env_base = st.env_base;
-    ra.E = st.E;
-    ra.episode = st.episode;
-    ra.quirks = st.quirks;
-    ra.n = st.n;
-    ra.m = st.m;
-    ra.T = st.T;
-    ra.L = st.L;
-    ra.k = k;
-    ra.dense = st.benefit_mode == ASG_BENEFIT_DENSE;
-    ra.wmin = (float)st.wmin;
-    ra.wmax = (float)st.wmax;
-    ra.pk = reinterpret_cast<const u32x4v *>(packed + rnn_agent_packed_f4(K, nout, 1) - rnn_agent_h2_f4(K, nout, 1));
-    const int64_t w2_f4 = 4 * (int64_t)((nout + 15) / 16) * 64;
-    const float4 *W2p = packed + (int64_t)((K + 15) / 16) * 4 * 64 + 2 * kGruF4;  // as launch_rnn_agent_fwd
-    ra.W1T = reinterpret_cast<const float *>(W2p + w2_f4);
-    ra.Hin = Hin;
-    ra.hs = hs;
-    ra.Hout = Hout;
-    ra.epsilon = epsilon;
-    ra.k0 = (uint32_t)seed;
-    ra.k1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
-    ra.counter = counter;
-    ra.row_base = row_base;
-    ra.sel_err = err;
-    ra.b1 = b1;
-    ra.bih = bih;
-    ra.bhh = bhh;
-    ra.b2 = b2;
-    const RolloutLds plan = rollout_lds_plan(st.n, st.m, st.L);
-    const bool w2l = plan.w2l;
-    ra.w1_lds = plan.w1_lds;
-    ra.scratch_off = plan.scratch_off;
-    const size_t lds_b = plan.bytes;
-    const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
-    const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
-    if (w2l)
-        hipLaunchKernelGGL((rollout_h2_kernel<true>), dim3(grid), dim3(64 * kH2Waves), lds_b, s, ra);
-    else
-        hipLaunchKernelGGL((rollout_h2_kernel<false>), dim3(grid), dim3(64 * kH2Waves), lds_b, s, ra);
-    return hipGetLastError();
-}
-
 }  // namespace asg
 
 extern "C" int asg_rnn_agent_mfma_mode(void) { return (ASG_AGENT_GRU_X3 ? 1 : 0) | (ASG_AGENT_FC1_X3 ? 2 : 0); }
 extern "C" int asg_rnn_agent_mode(int K, int hidden, int n_out, int use_rnn) {
+    (void)use_rnn;
     if (hidden != 64) return -1;
-    if (asg::h2_shape(K, n_out, use_rnn) && asg::use_h2_kernel()) return 4;
+    if (asg::h2_ok(K, n_out)) return 4;  // split-f16 (asg_h2.hip), GRU or Linear
     return asg_rnn_agent_mfma_mode();
 }
 

@@ -1,0 +1,1487 @@
+// asg_h2.hip -- the RNNAgent forward on two-way-split f16 MFMAs (gfx950), and the fused
+// rollout kernel that runs the mock env's transitions, the agent and the epsilon-greedy
+// selection for a range of steps of every env -- a whole episode in one launch.
+//
+// Reference: modules/agents/rnn_agent.py:23-31 (fc1 -> ReLU -> GRUCell | Linear + ReLU ->
+// fc2), controllers/basic_controller.py:19-48 (select_actions), action_selectors/
+// classic_selectors.py:28-54 (epsilon-greedy), envs/mock_constellation_env.py:94-175 (reset,
+// step, pre-transition data), runners/episode_runner.py:60-127 (the loop this kernel fuses:
+// select(0); for t: step(t), select(t + 1)).
+//
+// Split-f16 products.  Every f32 operand x (pre-scaled by a power of two so |x| < 2^15) is
+// split x ~ h + l with h = RNE_f16(x), l = RNE_f16(x - h) (x - h is exact in f32):
+// |x - h - l| <= 2^-22 |x|, and a product is summed as wh.xh + wh.xl + wl.xh on
+// v_mfma_f32_16x16x32_f16 (the dropped wl.xl is below 2^-22 relative): 3 MFMAs per 32-deep
+// slice, products exact in the f32 accumulator, summation in f32 -- fp32-level accuracy
+// (tests/test_gpu_agent.py measures it against float64).
+//
+// Transposed layers: out^T = W . act^T.  The MFMA A operand is a packed weight fragment (1 KiB
+// per wave, contiguous), the B operand an activation fragment; with the 16x16 layouts the
+// accumulator of output tile mt IS the B operand of the next layer's k-chunk, so fc1 ->
+// recurrent layer -> fc2 hand activations over in registers.  One wave owns 32 agent rows
+// (two 16-row tiles nt); lane (r, q) = (l & 15, l >> 4) holds rows r and 16 + r.
+//
+// Scales are per ROW (each lane's accumulator column is one row): weights by 2^sw per
+// matrix (pack time), a row's activations by 2^s from the row's own max |x| (a reduction
+// over its 4 lanes).  So every row's result is a function of that row's inputs alone -- the
+// same whichever rows share its wave tile (envs of 20 agents in 32-row tiles, sharded runs,
+// the fused rollout's one-env tiles vs the agent kernel's flat tiles: bit-identical).  fc1's
+// input scale is chosen before the values are seen (2^11: |x| < 16 needs no retry) and a
+// tile re-runs fc1 when some row would exceed 2^15 (that row at its own smaller scale).
+//
+// Geometry.  The input row is NB blocks of P values; each block is zero-padded to
+// Pp = roundup(P, 32) so a 32-deep slice never straddles two blocks.  For the mock env's
+// obs ([onehot(previous task) | B(k) .. B(k + L - 1)], P = m, NB = L + 1) block 0 is the
+// one-hot prefix: a tile whose block 0 is verified one-hot (or zero) adds W1[:, a] (one
+// gathered column per row) instead of running those slices' MFMAs.  Any other input is one
+// block (P = K).
+#include "asg_agent_common.h"
+
+#pragma clang fp contract(fast)
+
+namespace asg {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef long long i64x2v __attribute__((ext_vector_type(2)));
+typedef const u32x4v __attribute__((address_space(3))) * lds_u4p;
+typedef const f32x4 __attribute__((address_space(3))) * lds_f4v;
+
+__device__ __forceinline__ f32x4 mfma_h(const u32x4v &a, const u32x4v &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+}
+// (wh, wl) . (xh, xl) = wh.xh + wh.xl + wl.xh; the correction terms first
+__device__ __forceinline__ f32x4 mfma_h2(const u32x4v (&w)[2], const u32x4v (&x)[2], f32x4 c) {
+    c = mfma_h(w[1], x[0], c);
+    c = mfma_h(w[0], x[1], c);
+    c = mfma_h(w[0], x[0], c);
+    return c;
+}
+// 8 (scaled) f32 -> f16 planes h, l (element j in half j & 1 of dword j >> 1)
+__device__ __forceinline__ void split2(const float (&x)[8], u32x4v &h, u32x4v &l) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f16x2v hh = {(_Float16)x[2 * p], (_Float16)x[2 * p + 1]};
+        const float ra = x[2 * p] - (float)hh[0], rb = x[2 * p + 1] - (float)hh[1];
+        const f16x2v ll = {(_Float16)ra, (_Float16)rb};
+        h[p] = __builtin_bit_cast(uint32_t, hh);
+        l[p] = __builtin_bit_cast(uint32_t, ll);
+    }
+}
+// The split of 8 UNSCALED values at scale sc (a power of two): h = RNE_f16(x * sc) and the
+// residual fma(x, sc, -h) (exact in f32) rounded once to f16 by v_fma_mix{lo,hi}_f16.
+__device__ __forceinline__ void split2s(const float (&x)[8], float sc, u32x4v &h, u32x4v &l) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f16x2v hh = {(_Float16)(x[2 * p] * sc), (_Float16)(x[2 * p + 1] * sc)};
+        const uint32_t hv = __builtin_bit_cast(uint32_t, hh);
+        uint32_t lv = 0;
+        asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "+v"(lv) : "v"(x[2 * p]), "v"(sc), "v"(hv));
+        asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "+v"(lv)
+            : "v"(x[2 * p + 1]), "v"(sc), "v"(hv));
+        h[p] = hv;
+        l[p] = lv;
+    }
+}
+// max(m, |a|, |b|) in one v_max3_f32
+__device__ __forceinline__ float max3_abs(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float absmax4(float m, const float4 &v) { return max3_abs(max3_abs(m, v.x, v.y), v.z, v.w); }
+__device__ __forceinline__ float absmax4(float m, const f32x4 &v) {
+    return max3_abs(max3_abs(m, v[0], v[1]), v[2], v[3]);
+}
+// 2^s as a float (s clamped to the normal range [-126, 127])
+__device__ __forceinline__ float pow2f(int s) {
+    s = s < -126 ? -126 : (s > 127 ? 127 : s);
+    return __builtin_bit_cast(float, (uint32_t)(s + 127) << 23);
+}
+// the scale exponent s with m * 2^s < 2^15 (m = max |x| >= 0), clamped to [lo, hi]
+__device__ __forceinline__ int h2_scale(float m, int lo, int hi) {
+    const int e = m > 0.f ? (int)((__builtin_bit_cast(uint32_t, m) >> 23) & 0xff) - 126 : -200;  // m < 2^e
+    const int s = 15 - e;
+    return s < lo ? lo : (s > hi ? hi : s);
+}
+// maximum over the 4 lanes of a row (q = 0..3: lanes l, l ^ 16, l ^ 32, l ^ 48); v >= 0
+__device__ __forceinline__ float row_max4(float v) {
+    const SwapPair a = swap16(__builtin_bit_cast(uint32_t, v));
+    const float x = fmaxf(__builtin_bit_cast(float, a.a), __builtin_bit_cast(float, a.b));
+    const SwapPair b = swap32(__builtin_bit_cast(uint32_t, x));
+    return fmaxf(__builtin_bit_cast(float, b.a), __builtin_bit_cast(float, b.b));
+}
+// element j of lane quad q of a 32-deep slice: units 4q + v of its two 16-tiles (the
+// accumulator layout of the layer before, so activations feed the MFMA in place)
+__host__ __device__ inline int slice_k(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + j - 4; }
+
+// ---- geometry and packed layout -----------------------------------------------------------
+H2Geom h2_geom(int K, int nout) {
+    H2Geom g;
+    g.K = K;
+    g.nout = nout;
+    g.nct = (nout + 15) / 16;
+    const bool blocked = nout >= 16 && K % nout == 0 && K / nout >= 2;
+    g.P = blocked ? nout : K;
+    g.NB = blocked ? K / nout : 1;
+    g.prefix = blocked ? 1 : 0;
+    g.Pp = (g.P + 31) / 32 * 32;
+    g.Kp = g.Pp * g.NB;
+    return g;
+}
+bool h2_ok(int K, int nout) { return K >= 1 && nout >= 1 && nout <= 256; }
+
+// packed h2 section (u32x4v units): [header: int sw1, sw_r1, sw_r2, sw2]
+//   [W1 planes: slice Kp / 32][mt 4][plane 2][lane 64]
+//   [recurrent planes: GRU W_ih (gate 3)(hb 4)(slice 2)(plane 2)(lane 64), then W_hh; or the
+//    Linear W_rnn as one gate]
+//   [W2 planes: tile nct][slice 2][plane 2][lane 64]
+// preceded (one-hot prefix geometry) by W1^T of block 0: [P][64] f32
+constexpr int kGateF4 = 4 * 2 * 2 * 64;
+__host__ __device__ inline int64_t rec_f4(bool rnn) { return rnn ? 6 * kGateF4 : kGateF4; }
+__host__ __device__ inline int64_t w1s_f4(int Kp) { return (int64_t)(Kp / 32) * 4 * 2 * 64; }
+__host__ __device__ inline int64_t w2s_f4(int nct) { return (int64_t)nct * 2 * 2 * 64; }
+__device__ __forceinline__ int gate_idx(int g, int hb, int sl, int pl, int lane) {
+    return (((g * 4 + hb) * 2 + sl) * 2 + pl) * 64 + lane;
+}
+__device__ __forceinline__ int64_t w1_idx(int sl, int mt, int pl, int lane) {
+    return (((int64_t)sl * 4 + mt) * 2 + pl) * 64 + lane;
+}
+__device__ __forceinline__ int w2_idx(int c, int sl, int pl, int lane) { return ((c * 2 + sl) * 2 + pl) * 64 + lane; }
+static int64_t w1t_f4(const H2Geom &g) { return g.prefix ? (int64_t)g.P * 16 : 0; }
+int64_t h2_packed_f4(int K, int nout, int use_rnn) {
+    const H2Geom g = h2_geom(K, nout);
+    return w1t_f4(g) + 1 + w1s_f4(g.Kp) + rec_f4(use_rnn != 0) + w2s_f4(g.nct);
+}
+
+// LDS image (u32x4v units): [recurrent planes][biases][W2 planes (W2L)][W1 slices][scratch]
+// biases (floats): b1 [64] | GRU: b_ir + b_hr, b_iz + b_hz, b_in, b_hn [4 x 64]; Linear: b_rnn,
+// 0, 0, 0 | b2 [16 nct] (zero past n_out)
+__host__ __device__ inline int64_t bias_f4(int nct) { return 80 + 4 * (int64_t)nct; }
+__host__ __device__ inline int64_t lds_w2_off(bool rnn, int nct) { return rec_f4(rnn) + bias_f4(nct); }
+__host__ __device__ inline int64_t lds_w1_off(bool rnn, int nct, bool w2l) {
+    return lds_w2_off(rnn, nct) + (w2l ? w2s_f4(nct) : 0);
+}
+
+struct H2Args {
+    const float *X;
+    int64_t xs, R;
+    H2Geom g;
+    int pre;           // one-hot gather shortcut on block 0 (prefix geometry, ASG_AGENT_ONEHOT)
+    const float *Hin;
+    int64_t hs;
+    const u32x4v *pk;  // h2 section
+    const float *W1T;  // [P][64] f32: W1 columns of block 0
+    const float *b1, *bi, *bh, *b2;  // GRU: b_ih, b_hh; Linear: b_rnn, unused
+    float *Hout, *Q;
+    SelectArgs sel;
+    int w1_lds;        // W1 slices [s0, s0 + w1_lds) staged in LDS (s0 = pre ? Pp / 32 : 0)
+};
+
+constexpr int kH2NT = 2;                        // 16-row tiles per wave: 32 rows
+constexpr int kH2WavesPerSimd = 2;              // register budget 256 VGPRs
+constexpr int kH2Waves = 4 * kH2WavesPerSimd;   // waves per workgroup (one workgroup per CU)
+constexpr int kH2XBuf = 2;                      // observation slices in flight per wave in fc1
+constexpr int kH2SxInit = 11;                   // fc1 input scale of the first attempt
+
+__device__ __forceinline__ int h2_s0(const H2Args &a) { return a.pre ? (a.g.Pp >> 5) : 0; }
+
+template <bool RNN, bool W2L>
+__device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4]) {
+    const H2Geom &g = a.g;
+    const u32x4v *rec = a.pk + 1 + w1s_f4(g.Kp);  // recurrent planes, then W2
+    const int64_t nrec = rec_f4(RNN);
+    for (int64_t i = threadIdx.x; i < nrec; i += blockDim.x) s[i] = rec[i];
+    float *bs = reinterpret_cast<float *>(s + nrec);
+    for (int i = threadIdx.x; i < 5 * kHid + 16 * g.nct; i += blockDim.x) {
+        const int blk = i >> 6, u = i & 63;
+        float v;
+        if (blk == 0) v = a.b1[u];
+        else if (blk < 5) {
+            if (RNN) v = blk == 1 ? a.bi[u] + a.bh[u]
+                       : blk == 2 ? a.bi[kHid + u] + a.bh[kHid + u]
+                       : blk == 3 ? a.bi[2 * kHid + u] : a.bh[2 * kHid + u];
+            else v = blk == 1 ? a.bi[u] : 0.f;
+        } else {
+            const int j = i - 5 * kHid;
+            v = j < g.nout ? a.b2[j] : 0.f;
+        }
+        bs[i] = v;
+    }
+    if (W2L) {
+        const int64_t n2 = w2s_f4(g.nct), off = lds_w2_off(RNN, g.nct);
+        for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) s[off + i] = rec[nrec + i];
+    }
+    {
+        const u32x4v *w1 = a.pk + 1 + w1_idx(h2_s0(a), 0, 0, 0);
+        const int64_t n1 = (int64_t)a.w1_lds * 4 * 2 * 64, off = lds_w1_off(RNN, g.nct, W2L);
+        for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) s[off + i] = w1[i];
+    }
+    const int4 hdr = *reinterpret_cast<const int4 *>(a.pk);
+    sw[0] = hdr.x;
+    sw[1] = hdr.y;
+    sw[2] = hdr.z;
+    sw[3] = hdr.w;
+}
+
+// The recurrent layer, fc2 and selection of one 32-row wave tile (shared by the agent kernel
+// and the rollout kernel): xB = relu(fc1) fragments, hB = h_in rows (GRU).
+// ALLAV: every task is available (the rollout wrote avail = 1 itself).  act_lds (rollout):
+// also receives each row's selected task (index lrow0 + row within the tile).
+template <int NT, bool RNN, bool SEL, bool W2L, bool ALLAV, bool GEN>
+__device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
+                                        const int64_t (&rows)[NT], const bool (&ok)[NT], const float4 (&hB)[4][NT],
+                                        const f32x4 (&xB)[4][NT], uint16_t *act_lds = nullptr, int lrow0 = 0) {
+    // lane-derived addresses are recomputed here, not hoisted out of the callers' step / env
+    // loops (there they would be live across every tile and spill; their reloads would wait
+    // behind the tile stores in the in-order vmcnt queue)
+    int lane_ = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane_));
+    const int lane = lane_, r = lane & 15, q = lane >> 4;
+    const int nout = a.g.nout, nct = a.g.nct;
+    const lds_u4p Wr = (lds_u4p)Wl;
+    const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));  // biases
+    // availability words of fc2's first four output tiles: issued now, used after the
+    // recurrent layer
+    const SelectArgs &sel = a.sel;
+    const uint8_t *arow[NT];
+    int64_t oidx[NT];
+    bool av4 = false;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        arow[nt] = nullptr;
+        oidx[nt] = 0;
+    }
+    if (SEL) {
+        const int64_t b0 = row0 / sel.n;
+        const int i0 = (int)(row0 - b0 * sel.n);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            int64_t b = b0;
+            int i = i0 + 16 * nt + r;
+            while (i >= sel.n) {
+                i -= sel.n;
+                ++b;
+            }
+            arow[nt] = ALLAV ? nullptr : sel.avail + (ok[nt] ? b * sel.a0 + (int64_t)i * sel.a1 : 0);
+            oidx[nt] = b * sel.o0 + (int64_t)i * sel.o1;
+        }
+        av4 = !ALLAV && !GEN && ((reinterpret_cast<uintptr_t>(sel.avail) | (uintptr_t)sel.a0 | (uintptr_t)sel.a1) & 3u) == 0;
+    }
+    // 4 availability bytes of tasks 16 c + 4 q .. + 3 (0 past n_out)
+    auto load_av = [&](int c, int nt) -> uint32_t {
+        const int j0 = 16 * c + 4 * q;
+        if (!SEL || !ok[nt]) return 0u;
+        if (ALLAV) {
+            if (!GEN) return 0x01010101u;
+            const int nv = nout - j0;
+            return nv >= 4 ? 0x01010101u : (nv <= 0 ? 0u : (0x01010101u & ((1u << (8 * nv)) - 1u)));
+        }
+        const uint8_t *ap = arow[nt] + j0;
+        if (av4) return *reinterpret_cast<const uint32_t *>(ap);
+        uint32_t w = 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            if (!GEN || j0 + v < nout) w |= (uint32_t)ap[v] << (8 * v);
+        return w;
+    };
+    uint32_t avw[4][NT];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) avw[c][nt] = c < nct ? load_av(c, nt) : 0u;
+
+    // ---- recurrent layer: per-row scales, operand planes ---------------------------------
+    float mx[NT], mh[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        mx[nt] = 0.f;
+        mh[nt] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            mx[nt] = absmax4(mx[nt], xB[t][nt]);
+            if (RNN) mh[nt] = absmax4(mh[nt], hB[t][nt]);
+        }
+        mx[nt] = row_max4(mx[nt]);
+        if (RNN) mh[nt] = row_max4(mh[nt]);
+    }
+    int Sg[NT];
+    bool hz_all = true;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const bool hz = !RNN || !(mh[nt] > 0.f);  // zero h rows (init_hidden): no W_hh products
+        hz_all = hz_all && hz;
+        int s = min(sw[1] + h2_scale(mx[nt], -90, 90), hz ? 1000 : sw[2] + h2_scale(mh[nt], -90, 90));
+        Sg[nt] = s > 100 ? 100 : (s < -100 ? -100 : s);
+    }
+    const bool h_zero = !RNN || __ballot(!hz_all) == 0;  // wave-uniform: skip the W_hh MFMAs
+    u32x4v xP[2][NT][2], hP[2][NT][2];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            float v8[8], h8[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    v8[4 * c + v] = xB[2 * sl + c][nt][v];
+                    h8[4 * c + v] = RNN ? comp(hB[2 * sl + c][nt], v) : 0.f;
+                }
+            split2s(v8, pow2f(Sg[nt] - sw[1]), xP[sl][nt][0], xP[sl][nt][1]);
+            if (RNN) split2s(h8, pow2f(Sg[nt] - sw[2]), hP[sl][nt][0], hP[sl][nt][1]);
+        }
+    f32x4 hp[4][NT];
+    if (RNN) {
+        // sigmoid(g 2^-S) = 1 / (1 + 2^(g c1)), tanh(y 2^-S) = 2 / (1 + 2^(y c2)) - 1
+        float c1[NT], c2[NT], hun[NT], scS[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            c1[nt] = -1.4426950408889634f * pow2f(-Sg[nt]);
+            c2[nt] = 2.0f * c1[nt];
+            hun[nt] = pow2f(sw[2] - Sg[nt]);  // unscale of the h planes
+            scS[nt] = pow2f(Sg[nt]);
+        }
+        const lds_u4p Wih = Wr, Whh = (lds_u4p)(Wl + 3 * kGateF4);
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) {
+            // r and z sum the input and hidden products in one accumulator, from b_i + b_h;
+            // n keeps them apart (n = tanh(i_n + r * h_n))
+            const f32x4 br = Bs[16 + 4 * hb + q], bz = Bs[32 + 4 * hb + q], bn = Bs[48 + 4 * hb + q],
+                        bhn = Bs[64 + 4 * hb + q];
+            f32x4 gr[NT], gz[NT], gni[NT], gnh[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                gr[nt] = br * scS[nt];
+                gz[nt] = bz * scS[nt];
+                gni[nt] = bn * scS[nt];
+                gnh[nt] = bhn * scS[nt];
+            }
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    const u32x4v w[2] = {Wih[gate_idx(g, hb, sl, 0, lane)], Wih[gate_idx(g, hb, sl, 1, lane)]};
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        f32x4 &acc_ = g == 0 ? gr[nt] : (g == 1 ? gz[nt] : gni[nt]);
+                        acc_ = mfma_h2(w, xP[sl][nt], acc_);
+                    }
+                }
+            if (!h_zero) {
+#pragma unroll
+                for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+                    for (int g = 0; g < 3; ++g) {
+                        const u32x4v w[2] = {Whh[gate_idx(g, hb, sl, 0, lane)], Whh[gate_idx(g, hb, sl, 1, lane)]};
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            f32x4 &acc_ = g == 0 ? gr[nt] : (g == 1 ? gz[nt] : gnh[nt]);
+                            acc_ = mfma_h2(w, hP[sl][nt], acc_);
+                        }
+                    }
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float rg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gr[nt][v] * c1[nt]));
+                    const float zg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(gz[nt][v] * c1[nt]));
+                    const float ng =
+                        2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((gni[nt][v] + rg * gnh[nt][v]) * c2[nt])) -
+                        1.0f;
+                    // h from its planes (h_hi + h_lo = h 2^sh to 2^-22 relative)
+                    const int j = 4 * (hb & 1) + v;
+                    const uint32_t dh = hP[hb >> 1][nt][0][j >> 1], dl = hP[hb >> 1][nt][1][j >> 1];
+                    const f16x2v ph = __builtin_bit_cast(f16x2v, dh), pl = __builtin_bit_cast(f16x2v, dl);
+                    const float hv = ((float)ph[j & 1] + (float)pl[j & 1]) * hun[nt];
+                    hp[hb][nt][v] = ng + zg * (hv - ng);
+                }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                if (ok[nt])
+                    *reinterpret_cast<float4 *>(a.Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
+                        make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
+        }
+    } else {
+        // Linear + ReLU (use_rnn = False): h' = relu(W_rnn x + b_rnn), one gate of planes
+        float scS[NT], un[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            scS[nt] = pow2f(Sg[nt]);
+            un[nt] = pow2f(-Sg[nt]);
+        }
+#pragma unroll
+        for (int hb = 0; hb < 4; ++hb) {
+            const f32x4 bb = Bs[16 + 4 * hb + q];
+            f32x4 acc[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[nt] = bb * scS[nt];
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl) {
+                const u32x4v w[2] = {Wr[gate_idx(0, hb, sl, 0, lane)], Wr[gate_idx(0, hb, sl, 1, lane)]};
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma_h2(w, xP[sl][nt], acc[nt]);
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) hp[hb][nt][v] = fmaxf(acc[nt][v] * un[nt], 0.f);
+                if (ok[nt])
+                    *reinterpret_cast<float4 *>(a.Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
+                        make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
+            }
+        }
+    }
+
+    // ---- fc2 (+ selection state), per-row scale --------------------------------------------
+    int S3[NT];
+    u32x4v hq[2][NT][2];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        float m3 = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m3 = absmax4(m3, hp[t][nt]);
+        m3 = row_max4(m3);
+        const int s3 = h2_scale(m3, -90, 90 - sw[3]);
+        S3[nt] = sw[3] + s3;
+        const float c3 = pow2f(s3);
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+            float v8[8];
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) v8[4 * c + v] = hp[2 * sl + c][nt][v];
+            split2s(v8, c3, hq[sl][nt][0], hq[sl][nt][1]);
+        }
+    }
+    float best[NT], un3[NT];
+    int bj[NT];
+    uint64_t amask[NT][2];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        best[nt] = -__builtin_inff();
+        bj[nt] = 0x7fffffff;
+        amask[nt][0] = amask[nt][1] = 0;
+        un3[nt] = pow2f(-S3[nt]);
+    }
+    int lane2 = lane;
+    // the rollout recomputes the lane's W2 address here each tile (hoisted, it was spilled and
+    // its reload waited for every store of the tile)
+    if (ALLAV) asm volatile("" : "+v"(lane2));
+    const lds_u4p W2s = (lds_u4p)(Wl + lds_w2_off(RNN, nct));
+    const u32x4v *W2g = a.pk + 1 + w1s_f4(a.g.Kp) + rec_f4(RNN);
+    for (int c0 = 0; c0 < nct; c0 += 4) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = c0 + cc;
+            if (c >= nct) break;
+            const int j0 = 16 * c + 4 * q;
+            uint32_t av[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const uint32_t w = avw[cc][nt];
+                av[nt] = ((w & 0xffu) != 0) | (((w >> 8) & 0xffu) != 0) << 1 | (((w >> 16) & 0xffu) != 0) << 2 |
+                         ((w >> 24) != 0) << 3;
+                if (c + 4 < nct) avw[cc][nt] = load_av(c + 4, nt);  // the ring: 4 tiles ahead
+            }
+            f32x4 a2[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) a2[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl) {
+                u32x4v w[2];
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl)
+                    w[pl] = W2L ? W2s[w2_idx(c, sl, pl, lane2)] : W2g[w2_idx(c, sl, pl, lane2)];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) a2[nt] = mfma_h2(w, hq[sl][nt], a2[nt]);
+            }
+            const f32x4 bq = Bs[80 + 4 * c + q];  // b2[16 c + 4 q ..] (zero past n_out)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const f32x4 qv = a2[nt] * un3[nt] + bq;
+                if (a.Q && ok[nt]) {
+                    float *qp = a.Q + rows[nt] * nout + j0;
+                    if (!GEN) {
+                        *reinterpret_cast<float4 *>(qp) = make_float4(qv[0], qv[1], qv[2], qv[3]);
+                    } else {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            if (j0 + v < nout) qp[v] = qv[v];
+                    }
+                }
+                if (SEL) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        // a lane meets its tasks in increasing j, so torch.max order reduces
+                        // to: the first candidate, then strictly greater, or the first NaN
+                        const int j = j0 + v;
+                        const float x = ((av[nt] >> v) & 1u) ? qv[v] : -__builtin_inff();
+                        const bool b = ((bj[nt] == 0x7fffffff) & (j < nout)) |
+                                       ((best[nt] == best[nt]) & !(x <= best[nt]) & (j < nout));
+                        best[nt] = b ? x : best[nt];
+                        bj[nt] = b ? j : bj[nt];
+                    }
+                    amask[nt][0] |= (uint64_t)av[nt] << (4 * (c & 15));
+                }
+            }
+        }
+    }
+    if (SEL) {
+        const int act = select_finish<false, NT>(best, bj, amask, rows, ok, oidx, nct, sel, q);
+        const int nt = NT == 1 ? 0 : (q & 1);
+        if (act_lds && q < NT && ok[nt]) act_lds[lrow0 + 16 * nt + r] = (uint16_t)act;
+    }
+}
+
+// One wave, 32 agent rows of a flat [R][K] input: fc1 -> recurrent layer -> fc2 (+ selection).
+template <int NT, bool RNN, bool SEL, bool W2L, bool GEN>
+__device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, const u32x4v *Wl, const int (&sw)[4]) {
+    const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+    if (row0 >= a.R) return;
+    const H2Geom &g = a.g;
+    int64_t rows[NT];
+    bool ok[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        rows[nt] = row0 + 16 * nt + r;
+        ok[nt] = rows[nt] < a.R;
+    }
+    const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));
+    const u32x4v *W1g = a.pk + 1;
+    const float *xr[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) xr[nt] = a.X + (ok[nt] ? rows[nt] : 0) * a.xs;
+    const int Ub = g.Pp >> 5, nsl = g.Kp >> 5;
+    const int s0 = h2_s0(a);
+
+    // padded slice sl of every row: block sl / Ub, inputs 32 (sl % Ub) + 16 c + 4 q + e of it
+    auto load_x = [&](int sl, float4 (&xv)[2][NT]) {
+        if (!GEN) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    xv[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + 32 * sl + 16 * c + 4 * q);
+        } else {
+            const int blk = sl / Ub, jj0 = 32 * (sl - blk * Ub);
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int jj = jj0 + 16 * c + 4 * q;
+                    const float *p = xr[nt] + (int64_t)blk * g.P + jj;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = (ok[nt] && jj + e < g.P) ? p[e] : 0.f;
+                    xv[c][nt] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+        }
+    };
+    // block 0 chunks t4 .. t4 + 3 (16 inputs each)
+    auto load_pa = [&](int t4, float4 (&pa)[4][NT]) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int jj = 16 * (t4 + c) + 4 * q;
+                if (t4 + c >= (g.Pp >> 4)) {
+                    pa[c][nt] = make_float4(0.f, 0.f, 0.f, 0.f);
+                } else if (!GEN) {
+                    pa[c][nt] = *reinterpret_cast<const float4 *>(xr[nt] + jj);
+                } else {
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = (ok[nt] && jj + e < g.P) ? xr[nt][jj + e] : 0.f;
+                    pa[c][nt] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            }
+    };
+    float4 pa[4][NT];
+    if (a.pre) load_pa(0, pa);
+    // main-loop slice order: with the prefix geometry (blocks 1 .. NB - 1 of Ub chunks), chunk
+    // u outer and block inner -- the order in which the rollout kernel generates them
+    const int nmain = nsl - s0;
+    const int nblk = g.NB - 1;
+    auto sl_of = [&](int idx) { return a.pre ? (idx % nblk + 1) * Ub + idx / nblk : idx; };
+    float4 xbuf[kH2XBuf][2][NT];
+#pragma unroll
+    for (int b = 0; b < kH2XBuf; ++b)
+        if (b < nmain) load_x(sl_of(b), xbuf[b]);
+
+    // ---- one-hot prefix: rows whose block 0 is onehot(a) or zero add W1[:, a] (W1T, f32)
+    // instead of running those slices' MFMAs
+    int pos[NT];
+    bool onehot = false;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) pos[nt] = -1;
+    if (a.pre) {
+        bool bad = false;
+        for (int t4 = 0; t4 < (g.Pp >> 4); t4 += 4) {
+            if (t4 > 0) load_pa(t4, pa);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float v = comp(pa[c][nt], e);
+                        const bool one = v == 1.0f;
+                        bad |= (one && pos[nt] >= 0) || (!one && v != 0.0f);
+                        pos[nt] = one ? 16 * (t4 + c) + 4 * q + e : pos[nt];
+                    }
+        }
+        bool rows_ok = true;  // a row's 1 may sit in only one of its 4 lanes
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const uint64_t mk = __ballot(pos[nt] >= 0);
+            const uint64_t g0 = mk & 0xffffull, g1 = (mk >> 16) & 0xffffull, g2 = (mk >> 32) & 0xffffull, g3 = mk >> 48;
+            rows_ok = rows_ok && ((g0 & g1) | (g0 & g2) | (g0 & g3) | (g1 & g2) | (g1 & g3) | (g2 & g3)) == 0;
+            int p = pos[nt];
+            p = max(p, __shfl_xor(p, 16));
+            p = max(p, __shfl_xor(p, 32));
+            pos[nt] = p;
+        }
+        onehot = rows_ok && __ballot(bad) == 0;
+    }
+    // ---- fc1 on split f16 MFMAs, per-row input scale ----------------------------------------
+    f32x4 acc[4][NT];
+    int sx[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) sx[nt] = kH2SxInit;
+    float4 hB[4][NT];
+    auto load_h = [&]() {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                hB[t][nt] = (RNN && a.Hin) ? *reinterpret_cast<const float4 *>(a.Hin + (ok[nt] ? rows[nt] : 0) * a.hs +
+                                                                              16 * t + 4 * q)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    for (int attempt = 0;; ++attempt) {
+        if (attempt > 0) {
+#pragma unroll
+            for (int b = 0; b < kH2XBuf; ++b)
+                if (b < nmain) load_x(sl_of(b), xbuf[b]);
+        }
+        float scx[NT], rmax[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            scx[nt] = pow2f(sx[nt]);
+            rmax[nt] = 0.f;
+            const float scS = pow2f(sw[0] + sx[nt]);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float4 gv = (onehot && pos[nt] >= 0)
+                                      ? *reinterpret_cast<const float4 *>(a.W1T + pos[nt] * kHid + 16 * mt + 4 * q)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc[mt][nt] = f32x4{gv.x, gv.y, gv.z, gv.w} * scS;
+            }
+        }
+        auto slice = [&](int sl, const float4 (&xv)[2][NT], bool lds) {
+            u32x4v xp[NT][2];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                rmax[nt] = absmax4(absmax4(rmax[nt], xv[0][nt]), xv[1][nt]);
+                const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
+                                     xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
+                split2s(x8, scx[nt], xp[nt][0], xp[nt][1]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                u32x4v w[2];
+                if (lds) {
+                    const lds_u4p W1s = (lds_u4p)(Wl + lds_w1_off(RNN, g.nct, W2L));
+#pragma unroll
+                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[w1_idx(sl - s0, mt, pl, lane)];
+                } else {
+#pragma unroll
+                    for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[w1_idx(sl, mt, pl, lane)];
+                }
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
+            }
+        };
+        // block 0 of a tile that is not one-hot: its slices through L2
+        for (int sl = 0; sl < ((a.pre && !onehot) ? s0 : 0); ++sl) {
+            float4 xv[2][NT];
+            load_x(sl, xv);
+            slice(sl, xv, false);
+        }
+        const int s_l2 = s0 + a.w1_lds;  // first slice read through L2
+        for (int i0 = 0; i0 < nmain; i0 += kH2XBuf) {
+#pragma unroll
+            for (int b = 0; b < kH2XBuf; ++b) {
+                if (i0 + b < nmain) {
+                    const int sl = sl_of(i0 + b);
+                    if (sl < s_l2) slice(sl, xbuf[b], true);
+                    else slice(sl, xbuf[b], false);
+                    if (i0 + b + kH2XBuf < nmain) load_x(sl_of(i0 + b + kH2XBuf), xbuf[b]);
+                }
+            }
+        }
+        if (attempt == 0 && RNN) load_h();  // after fc1: 32 fewer VGPRs live through it
+        // the split needs |x| 2^sx < 2^15 (|h| <= 65504): rows that overflow redo at their own
+        // smaller scale (the others keep theirs, so their values are unchanged)
+        bool over[NT], any = false;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const float rm = row_max4(rmax[nt]);
+            over[nt] = rm * scx[nt] >= 32768.f;
+            any = any || over[nt];
+            if (over[nt]) sx[nt] = h2_scale(rm, -90, 90 - sw[0]);
+        }
+        if (attempt > 0 || __ballot(any) == 0) break;
+    }
+    f32x4 xB[4][NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const float un = pow2f(-(sw[0] + sx[nt]));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const f32x4 bb = Bs[4 * mt + q];  // b1[16 mt + 4 q ..]
+#pragma unroll
+            for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
+        }
+    }
+    h2_tail<NT, RNN, SEL, W2L, false, GEN>(a, Wl, sw, row0, rows, ok, hB, xB);
+}
+
+// Persistent: one 512-thread workgroup per CU stages the LDS image, then its 8 waves walk
+// 256-row tiles.
+template <bool RNN, bool SEL, bool W2L, bool GEN>
+__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
+rnn_agent_h2_kernel(H2Args a) {
+    extern __shared__ u32x4v s_h2[];
+    int sw[4];
+    h2_stage<RNN, W2L>(a, s_h2, sw);
+    __syncthreads();
+    constexpr int NT = kH2NT;
+    const int64_t ntiles = (a.R + kH2Waves * (16 * NT) - 1) / (kH2Waves * (16 * NT));
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t row0 = (tile * kH2Waves + (threadIdx.x >> 6)) * (16 * NT);
+        agent_rows_h2<NT, RNN, SEL, W2L, GEN>(row0, a, s_h2, sw);
+    }
+}
+
+// ---- packing: max|W| -> scale exponent, then the scaled f16 planes ------------------------
+__global__ void h2_exp_kernel(const float *W, int64_t n, int *out) {
+    __shared__ float s_m[16];
+    float m = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, __builtin_fabsf(W[i]));
+    m = wave_allreduce(m, [](float a, float b) { return fmaxf(a, b); });
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, s_m[w]);
+        *out = h2_scale(m, -60, 60);
+    }
+}
+// W [C][Kin] row-major -> planes of tiles (ct, sl): lane l = (r, q) holds the 8 values of
+// padded inputs 32 sl + slice_k(q, j) of row 16 ct + r, scaled by 2^s and split into (h, l).
+// Padded input kp is block kp / Pp, element kp % Pp of it (zero past P); order slice-major
+// (W1: [sl][ct]) or unit-major (recurrent [ct = 4 g + hb][sl], W2 [c][sl]).
+__global__ void h2_pack_kernel(const float *W, int C, int Kin, int P, int Pp, int nct, int nsl, int slice_major,
+                               const int *sexp, u32x4v *out) {
+    const int64_t total = (int64_t)nct * nsl * 64;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int lane = (int)(i & 63);
+    const int64_t tix = i >> 6;
+    const int ct = slice_major ? (int)(tix % nct) : (int)(tix / nsl);
+    const int sl = slice_major ? (int)(tix / nct) : (int)(tix % nsl);
+    const int row = 16 * ct + (lane & 15), q = lane >> 4;
+    const float sc = pow2f(*sexp);
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int kp = 32 * sl + slice_k(q, j);
+        const int blk = kp / Pp, jj = kp - blk * Pp;
+        const int k = blk * P + jj;
+        x[j] = (row < C && jj < P && k < Kin) ? W[(int64_t)row * Kin + k] * sc : 0.f;
+    }
+    u32x4v h, l;
+    split2(x, h, l);
+    const int64_t o = (slice_major ? ((int64_t)sl * nct + ct) : ((int64_t)ct * nsl + sl)) * 2 * 64 + lane;
+    out[o] = h;
+    out[o + 64] = l;
+}
+
+hipError_t launch_h2_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
+                          int use_rnn, float4 *packed, hipStream_t s) {
+    const H2Geom g = h2_geom(K, nout);
+    const bool rnn = use_rnn != 0;
+    if (g.prefix) (void)launch_w1t_pack(W1, K, g.P, reinterpret_cast<float *>(packed), s);
+    u32x4v *sec = reinterpret_cast<u32x4v *>(packed + w1t_f4(g));
+    int *hdr = reinterpret_cast<int *>(sec);
+    const float *mats[4] = {W1, Wih, rnn ? Whh : Wih, W2};
+    const int64_t sizes[4] = {(int64_t)kHid * K, (rnn ? 3 : 1) * kHid * kHid, (rnn ? 3 : 1) * kHid * kHid,
+                              (int64_t)nout * kHid};
+    for (int i = 0; i < 4; ++i)
+        hipLaunchKernelGGL(h2_exp_kernel, dim3(1), dim3(1024), 0, s, mats[i], sizes[i], hdr + i);
+    auto pack = [&](const float *W, int C, int Kin, int P, int Pp, int nct, int nsl, int smaj, int e, u32x4v *out) {
+        const int64_t n = (int64_t)nct * nsl * 64;
+        hipLaunchKernelGGL(h2_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, C, Kin, P, Pp, nct,
+                           nsl, smaj, hdr + e, out);
+    };
+    u32x4v *o = sec + 1;
+    pack(W1, kHid, K, g.P, g.Pp, 4, g.Kp / 32, 1, 0, o);
+    o += w1s_f4(g.Kp);
+    if (rnn) {
+        pack(Wih, 3 * kHid, kHid, kHid, kHid, 12, 2, 0, 1, o);
+        o += 3 * kGateF4;
+        pack(Whh, 3 * kHid, kHid, kHid, kHid, 12, 2, 0, 2, o);
+        o += 3 * kGateF4;
+    } else {
+        pack(Wih, kHid, kHid, kHid, kHid, 4, 2, 0, 1, o);
+        o += kGateF4;
+    }
+    pack(W2, nout, kHid, kHid, kHid, g.nct, 2, 0, 3, o);
+    return hipGetLastError();
+}
+
+// LDS plan: recurrent planes, biases, W2 planes when they fit, then as many W1 slices (from
+// s0) as fit; `reserve` bytes per workgroup kept for a per-wave scratch
+struct H2Lds {
+    bool w2l;
+    int w1_lds, l2_slices;
+    int64_t scratch_off;  // u32x4v units
+    size_t bytes;
+};
+static H2Lds h2_lds_plan(const H2Geom &g, bool rnn, int s0, int64_t reserve_f4) {
+    constexpr int64_t kCap = 160 * 1024 / 16;
+    H2Lds p{};
+    p.w2l = lds_w2_off(rnn, g.nct) + w2s_f4(g.nct) + reserve_f4 <= kCap;
+    const int64_t w1off = lds_w1_off(rnn, g.nct, p.w2l);
+    const int64_t slices = g.Kp / 32 - s0, fit = (kCap - reserve_f4 - w1off) / (4 * 2 * 64);
+    p.w1_lds = (int)(fit < slices ? (fit > 0 ? fit : 0) : slices);
+    p.l2_slices = (int)(slices - p.w1_lds);
+    p.scratch_off = w1off + (int64_t)p.w1_lds * 4 * 2 * 64;
+    p.bytes = (size_t)(p.scratch_off + reserve_f4) * 16;
+    return p;
+}
+
+hipError_t launch_h2_agent(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
+                           const float4 *packed, const float *b1, const float *bih, const float *bhh, const float *b2,
+                           int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel, hipStream_t s) {
+    const H2Geom g = h2_geom(K, nout);
+    const bool rnn = use_rnn != 0;
+    H2Args ha{};
+    ha.X = X;
+    ha.xs = xs;
+    ha.R = R;
+    ha.g = g;
+    ha.pre = g.prefix && onehot_prefix_enabled();
+    ha.Hin = Hin;
+    ha.hs = hs;
+    ha.W1T = reinterpret_cast<const float *>(packed);
+    ha.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
+    ha.b1 = b1;
+    ha.bi = bih;
+    ha.bh = bhh;
+    ha.b2 = b2;
+    ha.Hout = Hout;
+    ha.Q = Q;
+    ha.sel = sel ? *sel : SelectArgs{};
+    const H2Lds plan = h2_lds_plan(g, rnn, ha.pre ? g.Pp / 32 : 0, 0);
+    ha.w1_lds = plan.w1_lds;
+    const bool gen = g.P % 32 != 0 || (xs & 3) != 0 || (reinterpret_cast<uintptr_t>(X) & 15) != 0 || nout % 16 != 0;
+    const int ncu = stream_cus(s);
+    const int64_t ntiles = (R + kH2Waves * 16 * kH2NT - 1) / (kH2Waves * 16 * kH2NT);
+    const unsigned grid = (unsigned)(ntiles < ncu ? ntiles : ncu);
+    if (grid == 0) return hipSuccess;
+#define LH_(RNN, SEL, W2L, GEN) \
+    hipLaunchKernelGGL((rnn_agent_h2_kernel<RNN, SEL, W2L, GEN>), dim3(grid), dim3(64 * kH2Waves), plan.bytes, s, ha)
+#define LH2_(RNN, SEL)                                                      \
+    do {                                                                    \
+        if (plan.w2l) {                                                     \
+            if (gen) LH_(RNN, SEL, true, true); else LH_(RNN, SEL, true, false);   \
+        } else {                                                            \
+            if (gen) LH_(RNN, SEL, false, true); else LH_(RNN, SEL, false, false); \
+        }                                                                   \
+    } while (0)
+    if (rnn) {
+        if (sel) LH2_(true, true); else LH2_(true, false);
+    } else {
+        if (sel) LH2_(false, true); else LH2_(false, false);
+    }
+#undef LH2_
+#undef LH_
+    return hipGetLastError();
+}
+
+// =====================================================================================
+// Fused rollout (mock env, Philox bumps): for every env, transitions k0 .. k1 - 1 and the
+// agent forward + epsilon-greedy selection of the rows in between, in one launch.  One wave
+// per env (persistent over envs): the transition runs with lane = agent (collision counts,
+// float64 rewards summed in agent order, the env's previous / selected tasks and task scales
+// in the wave's LDS scratch -- never re-read from HBM); the env's 32-agent tiles then
+// generate the next observation row in the split-f16 MFMA operand layout (lane (r, q)
+// evaluates the Philox bumps of tasks 32 u + 16 c + 4 q + v), write it to the batch and feed
+// fc1 from registers: the agent never reads an observation back.  Selected tasks go to the
+// batch's actions row and to the LDS, where the next transition reads them.  The hidden
+// state lives in Hout between passes (Hin for the first).  Results are those of the separate
+// launches: asg_reset / asg_step rows, and the agent kernel's actions and hidden state
+// (per-row scales make a row's result independent of its tile's other rows).
+// =====================================================================================
+struct RolloutArgs {
+    // time-major batch: row 0 of each field ([T+1][E][..] storage: row t at base + t * E * ..,
+    // the row strides derived from E, n, m, K); NULL = absent
+    float *obs, *beta, *rew;
+    uint8_t *avail, *term;
+    int64_t *onehot, *act, *prevb, *filled;
+    int ts0;  // batch row of transition k0
+    // env state
+    int *prev;
+    double *returns;
+    const double *T_trans;
+    int *env_err;
+    double lambda_;
+    uint64_t seed;
+    int64_t env_base, E;
+    uint32_t episode, quirks;
+    int n, m, T, L, dense;
+    float wmin, wmax;
+    int k0, k1, select_first, select_last;
+    // agent
+    const u32x4v *pk;
+    const float *W1T, *Hin;
+    int64_t hs;
+    float *Hout;
+    const float *b1, *bi, *bh, *b2;
+    int w1_lds;
+    float epsilon;
+    uint32_t sk0, sk1, counter;
+    int *sel_err;
+    int64_t scratch_off;  // per-wave LDS scratch (u32x4v units)
+};
+
+__host__ __device__ inline int rollout_mp(int m) { return (m + 31) / 32 * 32; }
+__host__ __device__ inline int rollout_np(int n) { return (n + 31) / 32 * 32; }
+// per wave: task-scale bits [4] u64 | collision counts [mp] int | selected / previous tasks [np] u16 each
+__host__ __device__ inline int rollout_scratch_bytes(int n, int m) {
+    return (32 + 4 * rollout_mp(m) + 4 * rollout_np(n) + 15) / 16 * 16;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ H2Args rollout_h2args(const RolloutArgs &ra) {
+    H2Args a{};
+    a.R = ra.E * ra.n;
+    a.g.K = ra.m * (ra.L + 1);
+    a.g.P = ra.m;
+    a.g.NB = ra.L + 1;
+    a.g.Pp = rollout_mp(ra.m);
+    a.g.Kp = a.g.Pp * (ra.L + 1);
+    a.g.prefix = 1;
+    a.g.nout = ra.m;
+    a.g.nct = (ra.m + 15) / 16;
+    a.pre = 1;
+    a.pk = ra.pk;
+    a.W1T = ra.W1T;
+    a.b1 = ra.b1;
+    a.bi = ra.bi;
+    a.bh = ra.bh;
+    a.b2 = ra.b2;
+    a.Hout = ra.Hout;
+    a.w1_lds = ra.w1_lds;
+    a.sel = SelectArgs{nullptr, 0, 0, ra.n, ra.epsilon, ra.sk0, ra.sk1, ra.counter, ra.env_base * ra.n, nullptr,
+                       (int64_t)ra.n, 1, ra.sel_err};
+    return a;
+}
+
+__device__ __forceinline__ float task_scale(const uint64_t *s_scl, int j) {
+    return ((s_scl[j >> 6] >> (j & 63)) & 1ull) ? 10.0f : 1.0f;
+}
+
+// one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
+// terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
+// launch) or, for the launch's first transition without a selection before it, from the
+// batch's actions row
+__device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_t e, int k, int ts, bool from_batch,
+                                                   const EnvKey &key, const uint64_t *s_scl, int *s_cnt,
+                                                   uint16_t *s_act, uint16_t *s_prev, double &ret) {
+    asm volatile("" : "+s"(e), "+s"(ts));
+    const int lane = threadIdx.x & 63;
+    const int n = ra.n, m = ra.m, mp = rollout_mp(m);
+    for (int j = lane; j < mp; j += 64) s_cnt[j] = 0;
+    wave_lds_fence();
+    int err = 0;
+    for (int i = lane; i < n; i += 64) {
+        int a;
+        if (from_batch) {
+            const int64_t a64 = ra.act[((int64_t)ts * ra.E + e) * n + i];
+            a = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
+            if (a < 0) err = ASG_E_ACTION_RANGE;
+            a = a < 0 ? 0 : a;
+            s_act[i] = (uint16_t)a;
+        } else {
+            a = s_act[i];
+        }
+        atomicAdd(&s_cnt[a], 1);
+    }
+    wave_lds_fence();
+    const BumpShape bsh = bump_shape(ra.T, ra.wmin, ra.wmax);
+    double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        double rr = 0.0;
+        if (i < n) {
+            const int j = s_act[i], p = s_prev[i];
+            const Bump32 b = philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
+            const double beta = bump64_at(b, k);
+            const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+            const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+            const double bh = beta - ra.lambda_ * pen;
+            rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+            if (ra.rew) ra.rew[((int64_t)ts * ra.E + e) * n + i] = (float)rr;
+            s_prev[i] = (uint16_t)j;
+            if (ra.prevb)
+                ra.prevb[((int64_t)(ts + 1) * ra.E + e) * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+        }
+        const int lo = __double2loint(rr), hi = __double2hiint(rr);
+        const int cnt = n - i0 < 64 ? n - i0 : 64;
+        for (int l2 = 0; l2 < cnt; ++l2)
+            sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
+    }
+    err = wave_or_i32(err);
+    if (lane == 0) {
+        ret += sum;
+        bool term = k + 1 >= ra.T;  // terminated = done != info.get("T", False)
+        if (ra.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
+        if (ra.term) ra.term[(int64_t)ts * ra.E + e] = term;
+        if (ra.filled) ra.filled[(int64_t)(ts + 1) * ra.E + e] = 1;
+        if (err) atomicCAS(ra.env_err, 0, err);
+    }
+    wave_lds_fence();
+}
+
+__device__ __forceinline__ void st_f4(float *p, float a, float b, float c, float d) {
+    *reinterpret_cast<f32x4 *>(p) = f32x4{a, b, c, d};
+}
+__device__ __forceinline__ void st_i64x2(int64_t *p, long long a, long long b) {
+    *reinterpret_cast<i64x2v *>(p) = i64x2v{a, b};
+}
+
+// One 32-agent tile of env e for observation row kk (batch row tsr): write the row (STORES:
+// one-hot block and actions_onehot of the transition before it, avail, lookahead blocks,
+// beta) and, AGENT, run fc1 on the generated blocks plus the recurrent layer, fc2 and the
+// selection of row kk.  have_act: block 0 is onehot(s_act) (else zeros: the reset row).
+template <bool RNN, bool W2L, bool GEN, bool AGENT>
+__device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, int sub, int kk, int tsr, bool stores,
+                                             bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
+                                             uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4]) {
+    constexpr int NT = kH2NT;
+    constexpr int RT = 16 * NT;  // rows per tile
+    // opaque env / row indices and lane: addresses are formed here from them, not hoisted out
+    // of the step and env loops (live across every tile they spill)
+    asm volatile("" : "+s"(e), "+s"(tsr), "+s"(kk));
+    int lane_ = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane_));
+    const int lane = lane_, r = lane & 15, q = lane >> 4;
+    const int n = ra.n, m = ra.m, T = ra.T, L = ra.L;
+    const int K = m * (L + 1);
+    const int Ub = rollout_mp(m) >> 5;
+    const int64_t row0 = e * n + RT * sub;
+    int64_t rows[NT];
+    bool ok[NT];
+    int ia[NT], act[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        ia[nt] = RT * sub + 16 * nt + r;
+        ok[nt] = !GEN || ia[nt] < n;
+        rows[nt] = e * n + ia[nt];
+        act[nt] = (have_act && ok[nt]) ? (int)s_act[ia[nt]] : -1;
+    }
+    float *obs_r = ra.obs + (int64_t)tsr * ra.E * n * K;
+    // fc1 accumulators start from the one-hot block's W1 columns, gathered (and consumed)
+    // before the tile's stores (a load behind them would wait for their acknowledgements:
+    // gfx9's vmcnt retires memory operations in order); a rescaled retry gathers again
+    f32x4 acc[4][NT];
+    int sx[NT];
+    if (AGENT) {
+        const float scS = pow2f(sw[0] + kH2SxInit);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            sx[nt] = kH2SxInit;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const float4 g = act[nt] >= 0
+                                     ? *reinterpret_cast<const float4 *>(ra.W1T + act[nt] * kHid + 16 * mt + 4 * q)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
+            }
+        }
+    }
+    if (stores) {
+        // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
+        int64_t *oh_r = ra.onehot ? ra.onehot + (int64_t)(tsr - 1) * ra.E * n * m : nullptr;
+        for (int u = 0; u < Ub; ++u)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int j0 = 32 * u + 16 * c + 4 * q;
+                    const int aa = act[nt];
+                    if (!GEN) {
+                        st_f4(obs_r + rows[nt] * K + j0, aa == j0, aa == j0 + 1, aa == j0 + 2, aa == j0 + 3);
+                        if (oh_r) {
+                            st_i64x2(oh_r + rows[nt] * m + j0, aa == j0, aa == j0 + 1);
+                            st_i64x2(oh_r + rows[nt] * m + j0 + 2, aa == j0 + 2, aa == j0 + 3);
+                        }
+                    } else if (ok[nt]) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            if (j0 + v < m) {
+                                obs_r[rows[nt] * K + j0 + v] = aa == j0 + v ? 1.0f : 0.0f;
+                                if (oh_r) oh_r[rows[nt] * m + j0 + v] = aa == j0 + v;
+                            }
+                    }
+                }
+        if (ra.avail) {
+            uint8_t *ab = ra.avail + ((int64_t)tsr * ra.E * n + row0) * m;
+            const int nrow = GEN ? min(RT, n - RT * sub) : RT;
+            int off0 = (GEN ? 1 : 16) * lane;
+            asm volatile("" : "+v"(off0));  // not hoisted: a per-lane 64-bit address kept across loops spilled
+            if (!GEN) {
+                for (int off = off0; off < RT * m; off += 64 * 16)
+                    *reinterpret_cast<uint4 *>(ab + off) = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+            } else {
+                for (int off = off0; off < nrow * m; off += 64) ab[off] = 1;
+            }
+        }
+    }
+    // ---- the lookahead blocks 1..L (times kk .. kk + L - 1), fc1 on them -------------------
+    BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
+    bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
+    const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));
+    const u32x4v *W1g = ra.pk + 1;
+    const int s0 = Ub, s_l2 = s0 + ra.w1_lds;
+    float *beta_r = ra.beta ? ra.beta + (int64_t)tsr * ra.E * n * m : nullptr;
+    const bool live = kk < T;  // rows past T are zeros: no bump parameters needed
+    for (int attempt = 0;; ++attempt) {
+        float scx[NT], rmax[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            scx[nt] = pow2f(AGENT ? sx[nt] : 0);
+            rmax[nt] = 0.f;
+        }
+        if (AGENT && attempt > 0) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const float scS = pow2f(sw[0] + sx[nt]);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    const float4 g = act[nt] >= 0
+                                         ? *reinterpret_cast<const float4 *>(ra.W1T + act[nt] * kHid + 16 * mt + 4 * q)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
+                }
+            }
+        }
+        const bool st_now = stores && attempt == 0;
+        for (int u = 0; u < Ub; ++u) {
+            // bump parameters of the lane's 16 (row, task) pairs of this chunk
+            Bump32 bp[2][4][NT];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int jw = 32 * u + 16 * c + 4 * q;
+                const uint64_t sbits = s_scl[jw >> 6];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    if (!live) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) bp[c][v][nt] = Bump32{0.f, 0.f, 0.f};
+                    } else if (!GEN) {
+#pragma unroll
+                        for (int v = 0; v < 4; v += 2) {  // pairs (j, j + 1) share one Philox call (m even)
+                            const int j = jw + v;
+                            const float s0v = ((sbits >> (j & 63)) & 1ull) ? 10.0f : 1.0f;
+                            const float s1v = ((sbits >> ((j + 1) & 63)) & 1ull) ? 10.0f : 1.0f;
+                            philox_bump32x2(key, ra.episode, ia[nt] * m + j, s0v, s1v, bsh, ra.dense != 0,
+                                            bp[c][v][nt], bp[c][v + 1][nt]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const int j = jw + v;
+                            const bool in = j < m;
+                            const float sv = ((sbits >> (j & 63)) & 1ull) ? 10.0f : 1.0f;
+                            bp[c][v][nt] = philox_bump32(key, ra.episode, ia[nt] * m + (in ? j : 0), sv, bsh,
+                                                         ra.dense != 0);
+                            if (!in) bp[c][v][nt].scale = 0.f;
+                        }
+                    }
+                }
+            }
+            for (int l = 1; l <= L; ++l) {
+                const int t = kk + l - 1;
+                float4 xv[2][NT];
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        float vv[4];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) vv[v] = (t < T) ? bump32_at(bp[c][v][nt], t) : 0.0f;
+                        xv[c][nt] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                        if (st_now) {
+                            const int j0 = 32 * u + 16 * c + 4 * q;
+                            if (!GEN) {
+                                st_f4(obs_r + rows[nt] * K + m * l + j0, vv[0], vv[1], vv[2], vv[3]);
+                                if (l == 1 && beta_r) st_f4(beta_r + rows[nt] * m + j0, vv[0], vv[1], vv[2], vv[3]);
+                            } else if (ok[nt]) {
+#pragma unroll
+                                for (int v = 0; v < 4; ++v)
+                                    if (j0 + v < m) {
+                                        obs_r[rows[nt] * K + m * l + j0 + v] = vv[v];
+                                        if (l == 1 && beta_r) beta_r[rows[nt] * m + j0 + v] = vv[v];
+                                    }
+                            }
+                        }
+                    }
+                if (AGENT) {
+                    // the agent kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
+                    const int sl = l * Ub + u;
+                    u32x4v xp[NT][2];
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        rmax[nt] = absmax4(absmax4(rmax[nt], xv[0][nt]), xv[1][nt]);
+                        const float x8[8] = {xv[0][nt].x, xv[0][nt].y, xv[0][nt].z, xv[0][nt].w,
+                                             xv[1][nt].x, xv[1][nt].y, xv[1][nt].z, xv[1][nt].w};
+                        split2s(x8, scx[nt], xp[nt][0], xp[nt][1]);
+                    }
+                    // two copies of the MFMA block: merged after an LDS-or-global select, the
+                    // MFMAs would wait for vmcnt(0) -- every store of the tile -- each slice
+                    auto mma = [&](bool lds) {
+#pragma unroll
+                        for (int mt = 0; mt < 4; ++mt) {
+                            u32x4v w[2];
+                            if (lds) {
+                                const lds_u4p W1s = (lds_u4p)(Wl + lds_w1_off(RNN, (m + 15) / 16, W2L));
+#pragma unroll
+                                for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[w1_idx(sl - s0, mt, pl, lane)];
+                            } else {
+#pragma unroll
+                                for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[w1_idx(sl, mt, pl, lane)];
+                            }
+#pragma unroll
+                            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
+                        }
+                    };
+                    if (sl < s_l2)
+                        mma(true);
+                    else
+                        mma(false);
+                }
+            }
+        }
+        if (!AGENT) return;
+        bool over[NT], any = false;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const float rm = row_max4(rmax[nt]);
+            over[nt] = rm * scx[nt] >= 32768.f;
+            any = any || over[nt];
+            if (over[nt]) sx[nt] = h2_scale(rm, -90, 90 - sw[0]);
+        }
+        if (attempt > 0 || __ballot(any) == 0) break;
+    }
+    if constexpr (AGENT) {
+        H2Args a = rollout_h2args(ra);
+        a.sel.counter = ra.counter + (uint32_t)pass;
+        a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
+        // h_t rows, issued after fc1 (32 fewer VGPRs live through it)
+        const float *hin = pass == 0 ? ra.Hin : ra.Hout;
+        const int64_t hs = pass == 0 ? ra.hs : kHid;
+        float4 hB[4][NT];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                hB[t][nt] = (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
+                                                                            16 * t + 4 * q)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        f32x4 xB[4][NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const float un = pow2f(-(sw[0] + sx[nt]));
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) {
+                const f32x4 bb = Bs[4 * mt + q];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
+            }
+        }
+        h2_tail<NT, RNN, true, W2L, true, GEN>(a, Wl, sw, row0, rows, ok, hB, xB, s_act, RT * sub);
+    }
+}
+
+template <bool RNN, bool W2L, bool GEN>
+__global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
+rollout_kernel(RolloutArgs ra) {
+    extern __shared__ u32x4v s_h2[];
+    int sw[4];
+    h2_stage<RNN, W2L>(rollout_h2args(ra), s_h2, sw);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n = ra.n, m = ra.m, mp = rollout_mp(m), np = rollout_np(n);
+    char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
+    uint64_t *s_scl = reinterpret_cast<uint64_t *>(scr);
+    int *s_cnt = reinterpret_cast<int *>(scr + 32);
+    uint16_t *s_act = reinterpret_cast<uint16_t *>(s_cnt + mp);
+    uint16_t *s_prev = s_act + np;
+    const int ntile = np / (16 * kH2NT);
+    const int64_t GW = (int64_t)gridDim.x * kH2Waves;
+    for (int64_t e0 = (int64_t)blockIdx.x * kH2Waves + wv; e0 < ra.E; e0 += GW) {
+        // addresses are recomputed from e each env: strength-reduced per-lane pointers carried
+        // across the env loop were spilled around the tile loop, and their reloads waited for
+        // every store of the env
+        int64_t e = e0;
+        asm volatile("" : "+s"(e));
+        const EnvKey key = env_key(ra.seed, ra.env_base + e);
+        // task scales (choice([1, 1, 1, 10]) per task) as bits, the env's previous tasks
+        for (int c = 0; c < (mp + 63) / 64; ++c) {
+            const int j = 64 * c + lane;
+            const bool ten = j < m && philox_task_scale(key, ra.episode, j) == 10.0f;
+            const uint64_t bits = __ballot(ten);
+            if (lane == 0) s_scl[c] = bits;
+        }
+        for (int i = lane; i < np; i += 64) {
+            s_prev[i] = (uint16_t)(i < n ? ra.prev[e * n + i] : 0);
+            s_act[i] = 0;
+        }
+        double ret = lane == 0 ? ra.returns[e] : 0.0;
+        wave_lds_fence();
+        // iteration 0 with select_first: the selection on the reset row (no transition);
+        // every other iteration: transition k, then the agent tiles of row k + 1 (or, past the
+        // launch's last selection, the row alone) -- one call site per tile kind
+        const int sf = ra.select_first ? 1 : 0;
+        int pass = 0;
+        for (int it = 0; it < ra.k1 - ra.k0 + sf; ++it) {
+            const int k = ra.k0 + it - sf;  // k0 - 1 on the select_first iteration
+            const int ts = ra.ts0 + (k - ra.k0);
+            const bool first_sel = it < sf;
+            if (!first_sel)
+                rollout_transition(ra, e, k, ts, k == ra.k0 && !sf, key, s_scl, s_cnt, s_act, s_prev, ret);
+            const int kk = k + 1;
+            const bool agent = kk < ra.T && (kk < ra.k1 || ra.select_last);
+            if (agent) {
+                for (int sub = 0; sub < ntile; ++sub)
+                    rollout_tile<RNN, W2L, GEN, true>(ra, e, sub, kk, ts + 1, !first_sel, !first_sel, pass, key, s_scl,
+                                                      s_act, s_h2, sw);
+                ++pass;
+            } else {
+                for (int sub = 0; sub < ntile; ++sub)
+                    rollout_tile<RNN, W2L, GEN, false>(ra, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
+                                                       sw);
+            }
+            wave_lds_fence();
+        }
+        for (int i = lane; i < n; i += 64) ra.prev[e * n + i] = s_prev[i];
+        if (lane == 0) ra.returns[e] = ret;
+        wave_lds_fence();  // the next env reuses the scratch
+    }
+}
+
+// shapes the rollout kernel takes: the split-f16 agent with the mock env's obs layout
+// (K = m (L + 1), one-hot prefix geometry), n, m <= 256
+bool rollout_shape_ok(int n, int m, int L, int K) {
+    if (n < 1 || m < 16 || m > 256 || n > 256 || L < 1 || K != m * (L + 1) || !h2_ok(K, m)) return false;
+    return onehot_prefix_enabled() && h2_geom(K, m).prefix;
+}
+
+int rollout_l2_slices(int n, int m, int L, int use_rnn) {
+    if (!rollout_shape_ok(n, m, L, m * (L + 1))) return -1;
+    const H2Geom g = h2_geom(m * (L + 1), m);
+    const int64_t scr = ((int64_t)rollout_scratch_bytes(n, m) * kH2Waves + 15) / 16;
+    return h2_lds_plan(g, use_rnn != 0, g.Pp / 32, scr).l2_slices;
+}
+
+hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
+                          int select_last, const float4 *packed, const float *b1, const float *bi, const float *bh,
+                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
+                          uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s) {
+    const int K = st.m * (st.L + 1), nout = st.m;
+    const H2Geom g = h2_geom(K, nout);
+    const bool rnn = use_rnn != 0;
+    RolloutArgs ra{};
+    ra.obs = sl.obs;
+    ra.beta = sl.beta;
+    ra.avail = sl.avail;
+    ra.onehot = sl.onehot;
+    ra.act = sl.act;
+    ra.rew = sl.rew;
+    ra.prevb = sl.prevb;
+    ra.term = sl.term;
+    ra.filled = sl.filled;
+    ra.ts0 = ts;
+    ra.prev = st.prev;
+    ra.returns = st.returns;
+    ra.T_trans = st.T_trans;
+    ra.env_err = st.err;
+    ra.lambda_ = st.lambda_;
+    ra.seed = st.seed;
+    ra.env_base = st.env_base;
+    ra.E = st.E;
+    ra.episode = st.episode;
+    ra.quirks = st.quirks;
+    ra.n = st.n;
+    ra.m = st.m;
+    ra.T = st.T;
+    ra.L = st.L;
+    ra.dense = st.benefit_mode == ASG_BENEFIT_DENSE;
+    ra.wmin = (float)st.wmin;
+    ra.wmax = (float)st.wmax;
+    ra.k0 = k0;
+    ra.k1 = k0 + steps;
+    ra.select_first = select_first;
+    ra.select_last = select_last;
+    ra.W1T = reinterpret_cast<const float *>(packed);
+    ra.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
+    ra.Hin = Hin;
+    ra.hs = hs;
+    ra.Hout = Hout;
+    ra.b1 = b1;
+    ra.bi = bi;
+    ra.bh = bh;
+    ra.b2 = b2;
+    ra.epsilon = epsilon;
+    ra.sk0 = (uint32_t)seed;
+    ra.sk1 = (uint32_t)(seed >> 32) ^ 0x5bd1e995u;
+    ra.counter = counter;
+    (void)row_base;  // = env_base * n (the selection keys by global row)
+    ra.sel_err = err;
+    const int64_t scr_f4 = ((int64_t)rollout_scratch_bytes(st.n, st.m) * kH2Waves + 15) / 16;
+    const H2Lds plan = h2_lds_plan(g, rnn, g.Pp / 32, scr_f4);
+    ra.w1_lds = plan.w1_lds;
+    ra.scratch_off = plan.scratch_off;
+    const bool gen = st.m % 32 != 0 || st.n % 32 != 0;
+    const int ncu = stream_cus(s);
+    const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
+    const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
+#define LR_(RNN, W2L, GEN) \
+    hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN>), dim3(grid), dim3(64 * kH2Waves), plan.bytes, s, ra)
+#define LR2_(RNN)                                                        \
+    do {                                                                 \
+        if (plan.w2l) {                                                  \
+            if (gen) LR_(RNN, true, true); else LR_(RNN, true, false);   \
+        } else {                                                         \
+            if (gen) LR_(RNN, false, true); else LR_(RNN, false, false); \
+        }                                                                \
+    } while (0)
+    if (rnn) LR2_(true); else LR2_(false);
+#undef LR2_
+#undef LR_
+    return hipGetLastError();
+}
+
+}  // namespace asg

@@ -90,26 +90,52 @@ hipError_t launch_filtered_soft_map(const int64_t *picked, const int64_t *topm, 
                                     hipStream_t s);
 
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
+int stream_cus(hipStream_t s);        // CUs the stream may run on (persistent grids)
+bool onehot_prefix_enabled();         // ASG_AGENT_ONEHOT (default on)
+hipError_t launch_w1t_pack(const float *W1, int K, int P, float *out, hipStream_t s);
 
-// fused rollout step (asg_agent.hip): the contiguous [E][..] slabs of the time-major batch
-// rows it touches
-struct RolloutSlabs {
-    float *obs1, *beta1;
-    uint8_t *avail1;
-    int64_t *onehot0;
-    const int64_t *act0;
-    float *rew0;
-    int64_t *prev1;
-    uint8_t *term0;
-    int64_t *filled1;
-    int64_t *act1;
+// split-f16 agent path (asg_h2.hip): input geometry -- NB blocks of P inputs, each padded to
+// Pp = roundup(P, 32) (Kp = Pp NB); prefix: block 0 may be the one-hot prefix (P = n_out)
+struct H2Geom {
+    int K, P, NB, Pp, Kp, prefix, nout, nct;
 };
-bool rollout_shape_ok(const EnvState &st, int K, int nout, int use_rnn);
-int rollout_l2_slices(int n, int m, int L);
-hipError_t launch_rollout_step_select(const RolloutSlabs &sl, const EnvState &st, int ts, int k,
-                                      const float4 *packed, const float *b1, const float *bih, const float *bhh,
-                                      const float *b2, const float *Hin, int64_t hs, float *Hout, float epsilon,
-                                      uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
+H2Geom h2_geom(int K, int nout);
+bool h2_ok(int K, int nout);
+int64_t h2_packed_f4(int K, int nout, int use_rnn);
+hipError_t launch_h2_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
+                          int use_rnn, float4 *packed, hipStream_t s);
+hipError_t launch_h2_agent(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
+                           const float4 *packed, const float *b1, const float *bih, const float *bhh, const float *b2,
+                           int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel, hipStream_t s);
+
+// fused rollout (asg_h2.hip): the time-major batch fields it touches, as row-0 pointers and
+// row strides in elements ([T+1][E][..] storage: row t is a contiguous [E][..] slab)
+struct RolloutSlabs {
+    float *obs;
+    int64_t obs_row;
+    float *beta;
+    int64_t beta_row;
+    uint8_t *avail;
+    int64_t avail_row;
+    int64_t *onehot;
+    int64_t onehot_row;
+    int64_t *act;
+    int64_t act_row;
+    float *rew;
+    int64_t rew_row;
+    int64_t *prevb;
+    int64_t prevb_row;
+    uint8_t *term;
+    int64_t term_row;
+    int64_t *filled;
+    int64_t filled_row;
+};
+bool rollout_shape_ok(int n, int m, int L, int K);
+int rollout_l2_slices(int n, int m, int L, int use_rnn);
+hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
+                          int select_last, const float4 *packed, const float *b1, const float *bi, const float *bh,
+                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
+                          uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
                                  int use_rnn, float4 *packed, hipStream_t s);
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,

@@ -146,29 +146,40 @@ class AssignEnvBatch(MultiAgentEnv):
         self.k += 1
         return self.k >= self.T
 
-    def can_step_select(self, prefer=True):
-        """Whether asg_step_select (the fused env step + next selection) takes this env:
-        Philox bump/dense benefits, integer actions, n and m multiples of 32, m <= 256.
-        `prefer` (kept for callers that ask whether it is also the faster schedule): measured
-        on MI355X it is wherever it applies -- 64 x 64 +15 %, 256 x 256 dense +8-13 % against
-        asg_step + asg_rnn_agent_select (asg_step_select_l2_slices reports the fc1 weight
-        slices it streams through L2: 1 and 20 there)."""
+    def can_step_select(self, prefer=True, use_rnn=True):
+        """Whether asg_rollout (env steps fused with the agent forward + epsilon-greedy
+        selections, up to a whole episode per launch) takes this env: Philox bump/dense
+        benefits, integer actions, 16 <= m <= 256, n <= 256, L >= 1 -- with the GRU or the
+        Linear RNNAgent.  `prefer` (kept for callers that ask whether it is also the faster
+        schedule): measured on MI355X it is wherever it applies."""
         return (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
-                and self.n % 32 == 0 and self.m % 32 == 0 and self.m <= 256 and self.L >= 1
-                and _lib.lib().asg_step_select_l2_slices(self.n, self.m, self.L) >= 0)
+                and _lib.lib().asg_rollout_l2_slices(self.n, self.m, self.L, int(bool(use_rnn))) >= 0)
 
     def step_select(self, batch, ts, agent, hidden_state, epsilon, seed, counter, status):
         """asg_step at row ts and the fused agent forward + epsilon-greedy for row ts + 1 in
-        one kernel (asg_step_select): the observations of ts + 1 are written to the batch and
-        consumed on the chip.  `agent` is the RNNFusedAgent; returns the new hidden state
-        [E n, hidden].  Same batch, returns, actions and hidden state as env.step(batch, ts)
-        followed by mac.select_actions(batch, ts + 1)."""
+        one kernel: the observations of ts + 1 are written to the batch and consumed on the
+        chip.  `agent` is the RNNFusedAgent; returns the new hidden state [E n, hidden].  Same
+        batch, returns, actions and hidden state as env.step(batch, ts) followed by
+        mac.select_actions(batch, ts + 1)."""
+        return self.rollout(batch, ts, 1, agent, hidden_state, epsilon, seed, counter, status, select_first=False,
+                            select_last=True)
+
+    def rollout(self, batch, ts, steps, agent, hidden_state, epsilon, seed, counter, status, select_first=True,
+                select_last=False):
+        """asg_rollout: `steps` env transitions from the current step (batch rows ts ..) with
+        the agent forward + epsilon-greedy selections in between, in one kernel --
+        select_first: also the selection on the reset row ts (k == 0); select_last: also the
+        selection after the last transition.  The selections use Philox counters counter,
+        counter + 1, ... in row order.  Returns the hidden state after the last selection
+        [E n, hidden] (the MAC's hidden_states).  A whole episode after reset():
+        rollout(batch, 0, T, ...)."""
         args = agent.step_select_args(hidden_state, batch["obs"].shape[-1], self.device, self.num_envs * self.n)
         h_out = args[-1]
-        self._call("asg_step_select", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
-                   ctypes.c_void_p(h_out.data_ptr()), float(epsilon), seed & 0xFFFFFFFFFFFFFFFF, int(counter),
-                   ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(self.device))
-        self.k += 1
+        self._call("asg_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps), int(bool(select_first)),
+                   int(bool(select_last)), *args[:-1], ctypes.c_void_p(h_out.data_ptr()), float(epsilon),
+                   seed & 0xFFFFFFFFFFFFFFFF, int(counter), ctypes.c_void_p(status.data_ptr()),
+                   _lib.stream_ptr(self.device))
+        self.k += int(steps)
         return h_out
 
     def random_actions(self, batch, ts):

@@ -100,8 +100,9 @@ class RNNFusedAgent(RNNAgent):
         return h_out
 
     def step_select_args(self, hidden_state, K, device, R):
-        """The agent half of asg_step_select's arguments: packed weights, biases, K, hidden,
-        h_in (+ row stride), and a fresh h_out tensor (last)."""
+        """The agent half of asg_rollout's arguments: packed weights, biases (GRU: b_ih, b_hh;
+        Linear: its bias, NULL), K, hidden, use_rnn, h_in (+ row stride), and a fresh h_out
+        tensor (last)."""
         H = self.args.hidden_dim
         h = hidden_state
         if h.dim() == 3 and h.stride(0) == 0 and h.stride(1) == 0 and h.stride(2) == 1:
@@ -113,11 +114,13 @@ class RNNFusedAgent(RNNAgent):
             hs = h.stride(0)
         if hs and h.shape[0] != R:
             raise ValueError(f"hidden state has {h.shape[0]} rows, the batch {R}")
-        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         self._h_keep = h  # alive until the kernel has read it (stream order)
         h_out = torch.empty((R, H), dtype=torch.float32, device=device)
-        return [p(self._packed(K, device)), p(self.fc1.bias), p(self.rnn.bias_ih), p(self.rnn.bias_hh),
-                p(self.fc2.bias), int(K), int(H), p(h), int(hs), h_out]
+        rnn = bool(self.args.use_rnn)
+        return [p(self._packed(K, device)), p(self.fc1.bias), p(self.rnn.bias_ih if rnn else self.rnn.bias),
+                p(self.rnn.bias_hh) if rnn else None, p(self.fc2.bias), int(K), int(H), int(rnn), p(h), int(hs),
+                h_out]
 
     def _packed(self, K, device):
         """Weights in the kernel's fragment order, re-packed only when a weight changed

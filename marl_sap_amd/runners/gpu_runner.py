@@ -8,7 +8,8 @@ in HBM behind one C-ABI handle and every step is:
 
     mac.select_actions (PyTorch-ROCm)  ->  actions row write  ->  asg_step (one HIP kernel)
 
-with the EpisodeBatch kept resident on the GPU in time-major storage.  Under
+or, with the fused RNN agent and epsilon-greedy, the whole episode in one asg_rollout
+kernel -- with the EpisodeBatch kept resident on the GPU in time-major storage.  Under
 torch.distributed (one process per GPU, RCCL) each rank owns the contiguous global envs
 [sum(E_<r), sum(E_<r) + E_r) -- [rank*E, (rank+1)*E) for equal shards; the rank env counts
 are all-gathered once at construction, so the env-step counter of an episode is
@@ -94,20 +95,26 @@ class GpuVecRunner:
     # ------------------------------------------------------------------ rollout
     @torch.no_grad()
     def rollout(self, test_mode=False):
-        """One episode of every env, fully asynchronous (no host sync)."""
+        """One episode of every env, fully asynchronous (no host sync).  When the MAC and env
+        allow it the whole loop -- select(0); for t: env.step(t), select(t + 1) -- is ONE
+        kernel (asg_rollout, mode "episode"), or one kernel per step ("step"): the
+        observations are generated on chip and never re-read, and the batch is the separate
+        launches' bit for bit."""
         self.reset()
         self.mac.init_hidden(batch_size=self.batch_size)
-        # env.step(t) + select_actions(t + 1) as one kernel when the MAC and env allow it
-        # (asg_step_select: bit-identical batches, the t + 1 observations never re-read)
-        fused = hasattr(self.mac, "fused_step_ok") and self.mac.fused_step_ok(self.env, self.batch)
-        self.select_into_batch(0, test_mode)
-        for t in range(self.T):
-            if fused and t + 1 < self.T:
-                self.mac.fused_step_select(self.env, self.batch, t, self.t_env, test_mode)
-                continue
-            self.env.step(self.batch, ts=t)
-            if t + 1 < self.T:
-                self.select_into_batch(t + 1, test_mode)
+        mode = self.mac.fused_mode(self.env, self.batch, self.t_env, test_mode) \
+            if hasattr(self.mac, "fused_mode") else None
+        if mode == "episode":
+            self.mac.fused_episode(self.env, self.batch, self.t_env, test_mode)
+        else:
+            self.select_into_batch(0, test_mode)
+            for t in range(self.T):
+                if mode == "step" and t + 1 < self.T:
+                    self.mac.fused_step_select(self.env, self.batch, t, self.t_env, test_mode)
+                    continue
+                self.env.step(self.batch, ts=t)
+                if t + 1 < self.T:
+                    self.select_into_batch(t + 1, test_mode)
         self.t = self.T
         if self.protocol == "parallel":
             actions = self.mac.select_actions(self.batch, t_ep=self.T, t_env=self.t_env, test_mode=test_mode)

@@ -79,34 +79,53 @@ def test_kernel_entry_points_validate_without_gpu(L):
     assert L.asg_step(None, None, 0) == _lib.ASG_E_INVALID_ARG
 
 
+def _h2_geom(K, m):
+    """asg_h2.hip:h2_geom restated: NB blocks of P inputs, each padded to a multiple of 32;
+    block 0 is the one-hot prefix when the input is m (L + 1) values (m >= 16)."""
+    blocked = m >= 16 and K % m == 0 and K // m >= 2
+    P, NB = (m, K // m) if blocked else (K, 1)
+    Pp = (P + 31) // 32 * 32
+    return P, NB, Pp, blocked
+
+
 def test_agent_pack_layout_without_gpu(L):
-    """Host-only sizing of the packed agent buffer: f32 W1 fragments, the GRU as three bf16
-    planes (split-bf16 MFMAs, asg_rnn_agent_mfma_mode bit 0), f32 W2, and W1^T of the one-hot
-    prefix when n_out % 16 == 0, n_out < K and K % 32 == 0."""
+    """Host-only sizing of the packed agent buffer.  n_out <= 256 (the split-f16 path, GRU or
+    Linear, any K): W1^T of the one-hot prefix (prefix geometry), then the section -- header,
+    W1 planes over the block-padded inputs, the recurrent planes (GRU: W_ih + W_hh, 6 gates;
+    Linear: 1), W2 planes.  n_out > 256: f32 W1 fragments, the GRU as three bf16 planes, f32 W2,
+    W1^T of the one-hot prefix when n_out % 16 == 0, n_out < K and K % 32 == 0."""
     mode = L.asg_rnn_agent_mfma_mode()
     assert mode & 1 == 1
     gru = 3 * 4 * 2 * 3 * 64 if mode & 1 else 4 * 12 * 64
     w1x3 = lambda K: (K // 32) * 4 * 3 * 64 if (mode & 2 and K % 32 == 0) else 0  # noqa: E731
-    for K, m, rnn in [(256, 64, 1), (1024, 256, 1), (70, 16, 1), (256, 64, 0), (490, 450, 1)]:
+    for K, m, rnn in [(256, 64, 1), (1024, 256, 1), (70, 16, 1), (256, 64, 0), (100, 25, 1), (100, 25, 0),
+                      (20, 64, 1), (3, 1, 1), (490, 11, 0)]:
+        P, NB, Pp, blocked = _h2_geom(K, m)
+        size = (16 * P if blocked else 0) + 1 + (Pp * NB // 32) * 512 + (6 if rnn else 1) * 1024 + \
+            ((m + 15) // 16) * 256
+        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * size, (K, m, rnn)
+        assert L.asg_rnn_agent_mode(K, 64, m, rnn) == 4
+    for K, m, rnn in [(490, 450, 1), (576, 300, 0)]:
         wr = 2 * gru if rnn else 4 * 4 * 64
         w1 = ((K + 15) // 16) * 4 * 64
         w2 = 4 * ((m + 15) // 16) * 64
         P = m if (m % 16 == 0 and m < K and K % 32 == 0) else 0
-        # split-f16 section (GRU, K % 32 == 0, 16 <= n_out <= 256, n_out % 16 == 0): header +
-        # two planes of W1, W_ih, W_hh, W2
-        h2 = (1 + (K // 32) * 512 + 2 * 3072 + (m // 16) * 256) if (rnn and K % 32 == 0 and m % 16 == 0
-                                                                    and 16 <= m <= 256) else 0
-        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K) + h2), (K, m, rnn)
+        assert L.asg_rnn_agent_packed_size(K, 64, m, rnn) == 16 * (w1 + wr + w2 + 16 * P + w1x3(K)), (K, m, rnn)
+        assert L.asg_rnn_agent_mode(K, 64, m, rnn) == mode
     assert L.asg_rnn_agent_packed_size(256, 32, 64, 1) < 0  # hidden must be 64
 
 
-def test_step_select_l2_slices_without_gpu(L):
-    """The fused rollout's LDS plan (asg_step_select_l2_slices): fc1 slices read through L2,
-    -1 for shapes asg_step_select rejects."""
-    assert L.asg_step_select_l2_slices(64, 64, 3) == 1
-    assert L.asg_step_select_l2_slices(64, 64, 1) == 0
-    assert L.asg_step_select_l2_slices(256, 256, 3) > 1
-    assert L.asg_step_select_l2_slices(30, 64, 3) == -1
-    assert L.asg_step_select_l2_slices(64, 48, 3) == -1
-    assert L.asg_step_select_l2_slices(64, 512, 3) == -1
-    assert L.asg_step_select_l2_slices(64, 64, 0) == -1
+def test_rollout_l2_slices_without_gpu(L):
+    """The fused rollout's LDS plan (asg_rollout_l2_slices): fc1 slices read through L2, -1 for
+    shapes asg_rollout rejects (m < 16 or > 256, n > 256, L = 0)."""
+    assert L.asg_step_select_l2_slices(64, 64, 3) == L.asg_rollout_l2_slices(64, 64, 3, 1) == 1
+    assert L.asg_rollout_l2_slices(64, 64, 3, 0) == 0      # Linear agent: every slice in LDS
+    assert L.asg_rollout_l2_slices(64, 64, 1, 1) == 0
+    assert L.asg_rollout_l2_slices(256, 256, 3, 1) > 1
+    assert L.asg_rollout_l2_slices(20, 25, 3, 1) == 0      # the reference's default shape
+    assert L.asg_rollout_l2_slices(30, 64, 3, 1) >= 0
+    assert L.asg_rollout_l2_slices(64, 48, 3, 0) >= 0
+    assert L.asg_rollout_l2_slices(8, 8, 3, 1) == -1
+    assert L.asg_rollout_l2_slices(64, 512, 3, 1) == -1
+    assert L.asg_rollout_l2_slices(300, 300, 3, 1) == -1
+    assert L.asg_rollout_l2_slices(64, 64, 0, 1) == -1

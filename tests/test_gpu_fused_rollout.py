@@ -1,8 +1,11 @@
-"""Fused rollout step (asg_step_select: the env transition of step t and the RNNAgent forward
-+ epsilon-greedy for step t + 1 in one kernel, the t + 1 observations generated in the
-agent's operand layout and never re-read).  It must be a pure scheduling change: every
-EpisodeBatch field, the returns, the hidden state and t_env bit-identical to the separate
-asg_step + asg_rnn_agent_select calls (reference loop: episode_runner.py:76-95)."""
+"""Fused rollout (asg_rollout: env transitions and the RNNAgent forward + epsilon-greedy
+selections in one kernel -- a whole episode per launch ("episode"), or one step per launch
+("step"); the observations generated in the agent's operand layout and never re-read).  It
+must be a pure scheduling change: every EpisodeBatch field, the returns, the hidden state and
+t_env bit-identical to the separate asg_step + asg_rnn_agent_select calls (reference loop:
+episode_runner.py:60-127) -- for the GRU and the Linear agent (use_rnn False, the reference's
+mock_constellation_iql / _reda configs), at multiples of 32 and at the reference's default
+20 x 25 shape."""
 from types import SimpleNamespace
 
 import numpy as np
@@ -24,23 +27,24 @@ class _Logger:
         pass
 
 
-def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protocol="episode", seed=7):
+def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protocol="episode", seed=7, use_rnn=True,
+             mac="basic_mac", **extra):
     args = SimpleNamespace(
         batch_size_run=E, env="mock_constellation_env",
         env_args=dict(n=n, m=m, T=T, L=L, lambda_=0.5, bids_as_actions=False, seed=seed, benefits=benefits),
         env_rng="philox", env_quirks=tuple(quirks), runner_protocol=protocol, test_nepisode=1,
-        runner_log_interval=10 ** 12, n=n, m=m, T=T, hidden_dim=64, use_rnn=True, obs_last_action=False,
+        runner_log_interval=10 ** 12, n=n, m=m, T=T, hidden_dim=64, use_rnn=use_rnn, obs_last_action=False,
         obs_agent_id=False, agent_output_type="q", action_selector="epsilon_greedy", agent="rnn_fused",
-        mac="basic_mac", seed=3, epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
-        evaluation_epsilon=0.0, fused_rollout="always" if fused else False)
+        mac=mac, seed=3, epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
+        evaluation_epsilon=0.0, fused_rollout={True: "always", False: False}.get(fused, fused), **extra)
     runner = RUN["gpu"](args, _Logger())
     env = runner.get_env()
     torch.manual_seed(1234)
-    mac = MAC["basic_mac"](env.scheme, {"agents": n}, args)
+    mac = MAC[mac](env.scheme, {"agents": n}, args)
     mac.to(DEV)
     runner.setup(env.scheme, {"agents": n}, env.preprocess, mac)
     with torch.no_grad():
-        assert mac.fused_step_ok(env, runner.new_batch()) == fused
+        assert mac.fused_step_ok(env, runner.new_batch()) == bool(fused)
     out = []
     for _ in range(episodes):
         batch = runner.run(test_mode=False)
@@ -51,17 +55,7 @@ def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protoco
     return res
 
 
-@pytest.mark.parametrize("n,m,T,L,E,eps,benefits", [
-    (64, 64, 6, 3, 24, 0.05, "bump"),   # the bench shape (episode length cut short)
-    (32, 96, 5, 2, 10, 0.3, "dense"),   # three 32-task chunks per block, heavy exploration
-    (96, 128, 4, 1, 7, 0.0, "bump"),    # three agent tiles per env, n > 64 lanes, greedy
-    (32, 256, 4, 3, 5, 0.1, "bump"),    # configs[4]-like task count (W1 slices through L2)
-    (160, 192, 4, 1, 4, 0.1, "bump"),   # scalar-loaded transition rows in 64 + 64 + 32-agent blocks
-    (256, 256, 4, 3, 6, 0.05, "dense"),  # the configs[4] shape (256 x 256 dense, L = 3)
-])
-def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits):
-    a, ta, ra = _rollout(n, m, T, L, E, eps, benefits, fused=True)
-    b, tb, rb = _rollout(n, m, T, L, E, eps, benefits, fused=False)
+def _same(a, ta, ra, b, tb, rb):
     assert ta == tb and ra == rb
     for (fa, reta, ha), (fb, retb, hb) in zip(a, b):
         assert fa.keys() == fb.keys()
@@ -71,16 +65,92 @@ def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits):
         assert torch.equal(ha, hb)
 
 
+@pytest.mark.parametrize("n,m,T,L,E,eps,benefits,use_rnn", [
+    (64, 64, 6, 3, 24, 0.05, "bump", True),    # the bench shape (episode length cut short)
+    (64, 64, 6, 3, 24, 0.05, "bump", False),   # the same with the Linear agent (use_rnn False)
+    (32, 96, 5, 2, 10, 0.3, "dense", True),    # three 32-task chunks per block, heavy exploration
+    (96, 128, 4, 1, 7, 0.0, "bump", True),     # three agent tiles per env, n > 64 lanes, greedy
+    (32, 256, 4, 3, 5, 0.1, "bump", True),     # configs[4]-like task count (W1 slices through L2)
+    (160, 192, 4, 1, 4, 0.1, "bump", False),   # 64 + 64 + 32-agent transition chunks
+    (256, 256, 4, 3, 6, 0.05, "dense", True),  # the configs[4] shape (256 x 256 dense, L = 3)
+    (20, 25, 5, 3, 9, 0.2, "bump", True),      # the reference's default env (envs/mock_constellation_env.yaml)
+    (20, 25, 5, 3, 9, 0.2, "bump", False),
+    (30, 48, 4, 2, 5, 0.1, "dense", True),     # ragged agent tile, m not a multiple of 32
+    (33, 41, 3, 1, 6, 0.5, "bump", False),     # odd m: per-pair Philox calls; a 1-agent second tile
+])
+def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits, use_rnn):
+    b = _rollout(n, m, T, L, E, eps, benefits, fused=False, use_rnn=use_rnn)
+    for mode in ("always", "step"):
+        a = _rollout(n, m, T, L, E, eps, benefits, fused=mode, use_rnn=use_rnn)
+        _same(*a, *b)
+
+
 def test_fused_rollout_quirks_and_parallel_protocol():
     kw = dict(n=32, m=32, T=5, L=3, E=6, eps=0.2, benefits="bump", quirks=("prev_assigns_zero", "parallel_terminated"),
               protocol="parallel")
-    a, ta, ra = _rollout(fused=True, **kw)
-    b, tb, rb = _rollout(fused=False, **kw)
-    assert ta == tb and ra == rb
-    for (fa, reta, ha), (fb, retb, hb) in zip(a, b):
-        for k in fa:
-            assert torch.equal(fa[k], fb[k]), k
-        assert torch.equal(reta, retb)
+    b = _rollout(fused=False, **kw)
+    for mode in ("always", "step"):
+        _same(*_rollout(fused=mode, **kw), *b)
+
+
+def test_fused_rollout_jumpstart_iql():
+    """mock_constellation_iql.yaml: JumpstartMAC (HAA jumpstart selector) + epsilon-greedy +
+    the Linear agent.  The episode's coin flips are drawn when the runner plans it, in the
+    reference's order, so the numpy stream, the jumpstart steps and the RL steps are those of
+    the per-step path; with the jumpstart epsilon at 0.5 both kinds of steps occur, at 0 the
+    whole episode is one kernel."""
+    js = dict(mac="jumpstart_mac", jumpstart_action_selector="haa_selector", jumpstart_epsilon_start=0.5,
+              jumpstart_epsilon_finish=0.5, jumpstart_epsilon_anneal_time=1, jumpstart_evaluation_epsilon=0.0)
+    kw = dict(n=20, m=25, T=6, L=3, E=7, eps=0.1, benefits="bump", use_rnn=False, episodes=3, **js)
+    out = []
+    for fused in (False, "always", "step"):
+        np.random.seed(5)
+        out.append(_rollout(fused=fused, **kw))
+        out[-1] = out[-1] + (np.random.rand(),)  # the numpy stream after the run
+    for o in out[1:]:
+        _same(*o[:3], *out[0][:3])
+        assert o[3] == out[0][3]
+    js0 = dict(js, jumpstart_epsilon_start=0.0, jumpstart_epsilon_finish=0.0)
+    kw0 = dict(kw, **js0)
+    _same(*_rollout(fused="always", **kw0), *_rollout(fused=False, **kw0))
+
+
+def test_rollout_chunks_equal_one_launch():
+    """asg_rollout over an episode in chunks (select_first / select_last at the seams, the
+    bench's timed-window schedule) equals one whole-episode launch and the separate launches."""
+    from marl_sap_amd.envs import AssignEnvBatch
+    from marl_sap_amd.components import EpisodeBatch
+    from marl_sap_amd.modules.agents import RNNFusedAgent
+    from marl_sap_amd.action_selectors.classic_selectors import EpsilonGreedyActionSelector
+    n, m, T, L, E = 64, 64, 7, 3, 12
+
+    def run(chunks):
+        env = AssignEnvBatch(n, m, T, L, 0.5, seed=3, num_envs=E, device=DEV)
+        b = EpisodeBatch(env.scheme, {"agents": n}, E, T + 1, preprocess=env.preprocess, device=DEV, time_major=True)
+        torch.manual_seed(9)
+        agent = RNNFusedAgent(m * (L + 1), SimpleNamespace(hidden_dim=64, use_rnn=True, m=m)).to(DEV)
+        sel = EpsilonGreedyActionSelector(SimpleNamespace(epsilon_start=0.2, epsilon_finish=0.2,
+                                                          epsilon_anneal_time=1, evaluation_epsilon=0.0, seed=4))
+        env.reset(b, 0)
+        h = agent.init_hidden().unsqueeze(0).expand(E, n, -1)
+        t = 0
+        with torch.no_grad():
+            for s in chunks:
+                sf, sl = t == 0, t + s < T
+                eps, seed, c, st, _ = sel.fused_params(0, False, DEV, calls=s + sf + sl - 1)
+                h = env.rollout(b, t, s, agent, h, eps, seed, c, st, select_first=sf, select_last=sl)
+                t += s
+        env.sync()
+        out = {k: v.cpu() for k, v in b.data.transition_data.items()}, env.get_returns().cpu(), h.cpu()
+        env.close()
+        return out
+
+    one = run([T])
+    for chunks in ([2, 5], [1, 1, 1, 4], [6, 1]):
+        other = run(chunks)
+        for k in one[0]:
+            assert torch.equal(one[0][k], other[0][k]), (chunks, k)
+        assert torch.equal(one[1], other[1]) and torch.equal(one[2], other[2])
 
 
 def test_fused_rollout_out_of_range_action_is_reported():
@@ -102,5 +172,9 @@ def test_fused_rollout_out_of_range_action_is_reported():
         env.step_select(batch, 0, agent, h0, 0.0, 1, 1, status)
     with pytest.raises(ValueError):
         env.sync()
+    with pytest.raises(RuntimeError, match="select_first"):
+        env.rollout(batch, 1, 1, agent, h0, 0.0, 1, 1, status, select_first=True)
+    with pytest.raises(RuntimeError, match="k \\+ steps"):
+        env.rollout(batch, 1, 5, agent, h0, 0.0, 1, 1, status, select_first=False)
     env.close()
     assert np.all(np.isfinite(batch["obs"][:, 1].cpu().numpy()))
