@@ -185,6 +185,21 @@ constexpr int kH2WavesPerSimd = 2;              // register budget 256 VGPRs
 constexpr int kH2Waves = 4 * kH2WavesPerSimd;   // waves per workgroup (one workgroup per CU)
 constexpr int kH2XBuf = 2;                      // observation slices in flight per wave in fc1
 constexpr int kH2SxInit = 11;                   // fc1 input scale of the first attempt
+// Timing-only switches (WRONG results; refused without -DASG_TIMING_EXPERIMENTS):
+// ASG_ROLLOUT_XSKIP bit 1: no batch row stores in the rollout tiles; bit 2: no one-hot W1
+// column gather (zeros); bit 4: fc1 slices that live in L2 read LDS slot 0 instead; bit 8:
+// h_t not loaded (constants); bit 16: h' not stored
+#if defined(ASG_ROLLOUT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
+#error "ASG_ROLLOUT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
+#endif
+#ifndef ASG_ROLLOUT_XSKIP
+#define ASG_ROLLOUT_XSKIP 0
+#endif
+// 1: the rollout issues a tile's h_t rows at the tile start, before its row stores (they then
+// wait for nothing the tile wrote: gfx9's vmcnt retires loads and stores in order); 0: after fc1
+#ifndef ASG_ROLLOUT_EARLY_H
+#define ASG_ROLLOUT_EARLY_H 0
+#endif
 
 __device__ __forceinline__ int h2_s0(const H2Args &a) { return a.pre ? (a.g.Pp >> 5) : 0; }
 
@@ -401,7 +416,7 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
                 }
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
-                if (ok[nt])
+                if (ok[nt] && !(ALLAV && (ASG_ROLLOUT_XSKIP & 16)))
                     *reinterpret_cast<float4 *>(a.Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
                         make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
         }
@@ -1114,14 +1129,28 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
             sx[nt] = kH2SxInit;
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
-                const float4 g = act[nt] >= 0
+                const float4 g = (act[nt] >= 0 && !(ASG_ROLLOUT_XSKIP & 2))
                                      ? *reinterpret_cast<const float4 *>(ra.W1T + act[nt] * kHid + 16 * mt + 4 * q)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                 acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
             }
         }
     }
-    if (stores) {
+#if ASG_ROLLOUT_EARLY_H
+    float4 hB[4][NT];
+    if (AGENT) {
+        const float *hin = pass == 0 ? ra.Hin : ra.Hout;
+        const int64_t hs = pass == 0 ? ra.hs : kHid;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                hB[t][nt] = (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
+                                                                            16 * t + 4 * q)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#endif
+    if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
         int64_t *oh_r = ra.onehot ? ra.onehot + (int64_t)(tsr - 1) * ra.E * n * m : nullptr;
         for (int u = 0; u < Ub; ++u)
@@ -1187,7 +1216,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                 }
             }
         }
-        const bool st_now = stores && attempt == 0;
+        const bool st_now = stores && attempt == 0 && !(ASG_ROLLOUT_XSKIP & 1);
         for (int u = 0; u < Ub; ++u) {
             // bump parameters of the lane's 16 (row, task) pairs of this chunk
             Bump32 bp[2][4][NT];
@@ -1268,7 +1297,8 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                             if (lds) {
                                 const lds_u4p W1s = (lds_u4p)(Wl + lds_w1_off(RNN, (m + 15) / 16, W2L));
 #pragma unroll
-                                for (int pl = 0; pl < 2; ++pl) w[pl] = W1s[w1_idx(sl - s0, mt, pl, lane)];
+                                for (int pl = 0; pl < 2; ++pl)
+                                    w[pl] = W1s[w1_idx((ASG_ROLLOUT_XSKIP & 4) && sl >= s_l2 ? 0 : sl - s0, mt, pl, lane)];
                             } else {
 #pragma unroll
                                 for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[w1_idx(sl, mt, pl, lane)];
@@ -1277,7 +1307,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
                         }
                     };
-                    if (sl < s_l2)
+                    if (sl < s_l2 || (ASG_ROLLOUT_XSKIP & 4))
                         mma(true);
                     else
                         mma(false);
@@ -1300,6 +1330,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
         a.sel.counter = ra.counter + (uint32_t)pass;
         a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
         // h_t rows, issued after fc1 (32 fewer VGPRs live through it)
+#if !ASG_ROLLOUT_EARLY_H
         const float *hin = pass == 0 ? ra.Hin : ra.Hout;
         const int64_t hs = pass == 0 ? ra.hs : kHid;
         float4 hB[4][NT];
@@ -1307,9 +1338,11 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
-                hB[t][nt] = (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
-                                                                            16 * t + 4 * q)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                hB[t][nt] = (ASG_ROLLOUT_XSKIP & 8) ? make_float4(0.5f, 0.25f, -0.5f, 0.125f)
+                            : (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
+                                                                              16 * t + 4 * q)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
         f32x4 xB[4][NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {

@@ -15,6 +15,22 @@ import json
 import os
 
 
+def derived(avg, tiles):
+    """The utilisation figures the counters of this pass allow (two passes carry different sets)."""
+    d = {}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
+        d["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] * 128)
+    if "SQ_WAVE_CYCLES" in avg:
+        for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_LDS"):
+            if c in avg:
+                d[c[3:].lower() + "_frac"] = avg[c] / avg["SQ_WAVE_CYCLES"]
+    for c in ("SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_WR",
+              "SQ_INSTS_VMEM_RD", "SQ_INSTS_SMEM", "SQ_LDS_BANK_CONFLICT"):
+        if c in avg:
+            d[c[3:].lower() + "_per_wave_tile"] = avg[c] / tiles
+    return d
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("sq_dir")
@@ -27,6 +43,9 @@ def main():
     p.add_argument("--m", type=int, default=None)
     p.add_argument("--E", type=int, default=None)
     p.add_argument("--L", type=int, default=None)
+    p.add_argument("--steps-per-launch", type=int, default=1,
+                   help="env steps one launch of the kernel runs (the whole-episode rollout: T)")
+    p.add_argument("--use-rnn", type=int, default=1)
     a = p.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     name = None
@@ -42,18 +61,14 @@ def main():
             kt_ms = float(r["AverageNs"]) / 1e6
     tiles = a.rows / 32
     out = {k: getattr(a, k) for k in ("n", "m", "E", "L") if getattr(a, k) is not None}
+    out["steps_per_launch"] = a.steps_per_launch
+    out["use_rnn"] = bool(a.use_rnn)
     out.update({
         "kernel": (name or a.kernel).split("(")[0] + (f" -- {a.note}" if a.note else ""),
         "dispatches_averaged": n,
         "kernel_ms_from_kernel_trace": kt_ms,
         "counters": avg,
-        "derived": {
-            "mfma_busy_frac": avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] * 128),
-            "wait_inst_any_frac": avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"],
-            "wait_any_frac": avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"],
-            "mfma_insts_per_wave_tile": avg["SQ_INSTS_MFMA"] / tiles,
-            "valu_insts_per_wave_tile": avg["SQ_INSTS_VALU"] / tiles,
-        },
+        "derived": derived(avg, tiles),
     })
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out["derived"]))

@@ -34,6 +34,9 @@ def main():
     p.add_argument("--m", type=int, default=64)
     p.add_argument("--L", type=int, default=3)
     p.add_argument("--E", type=int, default=16384)
+    p.add_argument("--steps-per-launch", type=int, default=1,
+                   help="env steps one launch of the kernel runs (the whole-episode rollout: T)")
+    p.add_argument("--use-rnn", type=int, default=1)
     p.add_argument("--fetch-doubled", action="store_true",
                    help="headline bytes with FETCH_SIZE doubled (kernels whose reads are 16-B/lane streams)")
     a = p.parse_args()
@@ -49,7 +52,8 @@ def main():
                          "hbm_bytes_raw": (fk + wk) * 1024, "hbm_bytes_fetch_doubled": (2 * fk + wk) * 1024}
     sel = [k for k in kernels if a.kernel in k]
     main_k = max(sel, key=lambda k: kernels[k]["write_kib"]) if sel else None
-    out = {"n": a.n, "m": a.m, "L": a.L, "E": a.E, "kernel": main_k,
+    out = {"n": a.n, "m": a.m, "L": a.L, "E": a.E, "kernel": main_k, "steps_per_launch": a.steps_per_launch,
+           "use_rnn": bool(a.use_rnn),
            "hbm_bytes_per_launch": round(kernels[main_k]["hbm_bytes_fetch_doubled" if a.fetch_doubled
                                                  else "hbm_bytes_raw"]) if main_k else None,
            "note": ("(2 FETCH_SIZE + WRITE_SIZE)" if a.fetch_doubled else "(FETCH_SIZE + WRITE_SIZE)")
