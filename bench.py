@@ -452,30 +452,40 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
 def lsa_roofline(a, E, res):
     """SAP selector efficiency: augmenting-path steps (scipy's inner-loop iterations, counted
     by the instrumented kernel instance on one selection) per second of the fused
-    noise + LSA kernel, as cycles per step per SIMD; against the VALU issue bound when a
-    PMC summary (SQ_INSTS_VALU of sap_select_kernel) exists in profiles/."""
+    noise + LSA kernel, as cycles per step per SIMD.  With a PMC summary of the kernel in
+    profiles/ (SQ_INSTS_VALU / SQ_INSTS_SALU per step), against both issue bounds: vector
+    (2 cycles per wave64 instruction on a SIMD) and scalar (one scalar unit per CU: 4 cycles
+    per instruction per SIMD).  `frac` is the binding issue bound over the measured cycles;
+    `bound` names that bound when it explains most of the time (frac >= 0.7), else the
+    dependent instruction chain of one step (the serial augmenting path) binds: "latency"."""
     steps, lsa_ms = res.get("path_steps_per_launch"), res.get("lsa_ms")
     if not steps or not lsa_ms:
         return None
     per_s = steps / (lsa_ms * 1e-3)
     cyc = SIMDS * CLOCK_HZ * lsa_ms * 1e-3 / steps
-    out = {"bound": "valu-issue", "kernel": "asg::sap_select_kernel", "kernel_ms": round(lsa_ms, 4),
+    out = {"bound": None, "kernel": "asg::sap_select_kernel", "kernel_ms": round(lsa_ms, 4),
            "path_steps_per_launch": steps, "path_steps_per_s": round(per_s, 1),
            "cycles_per_step_per_simd": round(cyc, 1), "achieved": None, "peak": None, "frac": None,
            "unit": "wave-VALU-instr/s", "traffic": None}
     pm = pmc_lookup("*pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
     if pm and pm.get("valu_insts_per_path_step"):
         vps = pm["valu_insts_per_path_step"]
+        sps = pm.get("salu_insts_per_path_step") or 0.0
         peak = SIMDS * CLOCK_HZ / VALU_CYCLES_PER_WAVE_INSTR
         ach = vps * per_s
+        vb, sb = vps * VALU_CYCLES_PER_WAVE_INSTR, sps * 4
+        bind = max(vb, sb)
+        frac = bind / cyc
         out.update({"achieved": round(ach / 1e9, 2), "peak": round(peak / 1e9, 2), "unit": "G wave-VALU-instr/s",
-                    "frac": round(ach / peak, 4), "valu_insts_per_path_step": round(vps, 2),
-                    "issue_bound_cycles_per_step": round(vps * VALU_CYCLES_PER_WAVE_INSTR, 1),
+                    "valu_frac": round(ach / peak, 4), "valu_insts_per_path_step": round(vps, 2),
+                    "valu_bound_cycles_per_step": round(vb, 1),
+                    "salu_insts_per_path_step": round(sps, 2), "salu_bound_cycles_per_step": round(sb, 1),
+                    "salu_frac": round(sb / cyc, 4), "frac": round(frac, 4),
+                    "bound": ("salu-issue" if sb >= vb else "valu-issue") if frac >= 0.7 else "latency",
                     "pmc": os.path.basename(pm.get("_path", "")) or None})
-        if pm.get("salu_insts_per_path_step"):
-            # the scalar unit is shared by a CU's 4 SIMDs: one SALU issue per SIMD per 4 cycles
-            out["salu_insts_per_path_step"] = round(pm["salu_insts_per_path_step"], 2)
-            out["salu_bound_cycles_per_step"] = round(pm["salu_insts_per_path_step"] * 4, 1)
+        for k in ("wait_any_frac", "wait_inst_any_frac", "active_inst_any_frac", "resident_waves_per_simd"):
+            if k in pm:
+                out[k] = round(pm[k], 3)
     return out
 
 

@@ -287,8 +287,12 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
         uint64_t rem = colmask;                         // columns still in `remaining`
         int nrem = nc;
         double minv = 0.0;
-        int i = cur, sink = -1;
-        bool infeasible = false;
+        int i = cur, jsel, ncand;
+        uint32_t lowest_hi;
+        // Scalar work per step is the issue bound here (one scalar unit serves the CU's four
+        // SIMDs): the common single-candidate step is branch-light, the loop has one exit
+        // (no early returns the control-flow structurizer would turn into flag chains), the
+        // candidate count is one s_bcnt1.
         do {
             i = __builtin_amdgcn_readfirstlane(i);
             if (kCount) ++nsteps;
@@ -305,27 +309,27 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             const float key = remb ? (float)spc : kInfF;
             const float kmin = wave_min_f32_nonan(key);
             const uint64_t cm = __ballot(key == kmin) & rem;
-            // no candidate only if a cost turned NaN during the solve (e.g. a NaN T_trans
-            // entry under HAA): scipy's "invalid numeric entries", never an endless loop
-            if (cm == 0) return ASG_E_LSA_INVALID;
-            const int src0 = (int)__builtin_ctzll(cm);
+            asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
             const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
-            const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)sb, src0);
-            const uint32_t hi0 = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), src0);
-            double lowest = __builtin_bit_cast(double, (uint64_t)lo0 | ((uint64_t)hi0 << 32));
-            int jsel = src0, psel = __builtin_amdgcn_readlane(pos, src0);
-            uint32_t lowest_hi = hi0, lowest_lo = lo0;
-            if (__popcll(cm) != 1) {
+            jsel = (int)__builtin_ctzll(cm);  // the first candidate: the selection when it is the only one
+            uint32_t lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
+            lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
+            int psel = __builtin_amdgcn_readlane(pos, jsel);
+            if (ncand != 1) {
                 // equal keys: exact float64 ties (checked against the first candidate) or,
-                // rarely, distinct doubles rounding to one float (exact minimum first)
+                // rarely, distinct doubles rounding to one float (exact minimum first).  No
+                // candidate (ncand 0) only if a cost turned NaN during the solve (e.g. a NaN
+                // T_trans entry under HAA): scipy's "invalid numeric entries" -- the step
+                // then ends the loop as infeasible and is reported as invalid below
+                double lowest0 = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
                 uint64_t cand = cm;
-                if ((__ballot(spc != lowest) & cm) != 0) {
+                if ((__ballot(spc != lowest0) & cm) != 0) {
                     const double lo = remb ? spc : __builtin_inf();
                     const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));
                     lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
                     lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
-                    lowest = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
-                    cand = __ballot(spc == lowest) & rem;
+                    lowest0 = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+                    cand = __ballot(spc == lowest0) & rem;
                 }
                 // scipy's tie rule: unassigned 2^31 | pos (largest position), else 2^30 - pos
                 // (smallest position), max-reduced
@@ -333,7 +337,8 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
                 const uint32_t k = (r4c == -1) ? (0x80000000u | (uint32_t)pos) : ((1u << 30) - (uint32_t)pos);
                 const uint32_t tk = wave_max_u32_bcast(cb ? k : 0u);
                 psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
-                jsel = (int)__builtin_ctzll(__ballot(pos == psel) & rem);  // positions are distinct
+                jsel = (int)__builtin_ctzll(__ballot(pos == psel) & rem) & 63;  // positions are distinct
+                if (ncand == 0) lowest_hi = 0x7ff00000u;
             }
             // remaining[index] = remaining[--num_remaining]
             const int last = nrem - 1;
@@ -341,13 +346,15 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             pos = __builtin_amdgcn_inverse_ballot_w64(jbit) ? -1 : (pos == last ? psel : pos);
             rem &= ~jbit;
             --nrem;
-            minv = lowest;
-            const int owner = __builtin_amdgcn_readlane(r4c, jsel);
-            infeasible = lowest_hi == 0x7ff00000u && lowest_lo == 0u;  // scipy: minVal == INFINITY
-            if (owner == -1) sink = jsel;
-            i = owner;
-        } while (sink == -1 && !infeasible);
-        if (infeasible) return ASG_E_LSA_INFEASIBLE;
+            minv = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+            i = __builtin_amdgcn_readlane(r4c, jsel);
+            // continue while the column is assigned (owner != -1) and scipy's minVal is not
+            // INFINITY (lowest is never NaN: a NaN key is no candidate and the exact minimum
+            // skips NaN, so the high word decides): one unsigned min, one compare
+        } while (__builtin_elementwise_min((uint32_t)(i + 1), lowest_hi ^ 0x7ff00000u) != 0u);
+        if (ncand == 0) return ASG_E_LSA_INVALID;
+        if (lowest_hi == 0x7ff00000u) return ASG_E_LSA_INFEASIBLE;
+        const int sink = jsel;
         // dual update: u[cur] += minv; u[r] += minv - spc[col4row[r]] for the other visited
         // rows (row r != cur was visited iff its column was scanned); v[j] -= minv - spc[j]
         // for the scanned columns (matrix columns no longer in `remaining`)

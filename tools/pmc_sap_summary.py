@@ -41,6 +41,9 @@ def main():
         out["wait_any_frac"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
         out["wait_inst_any_frac"] = avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
         out["active_inst_any_frac"] = avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
+        if "GRBM_GUI_ACTIVE" in avg:
+            # SQ_WAVE_CYCLES counts quad-cycles summed over waves; GRBM_GUI_ACTIVE sums the 8 XCDs
+            out["resident_waves_per_simd"] = 4 * avg["SQ_WAVE_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "counters"}))
 
