@@ -188,17 +188,13 @@ constexpr int kH2SxInit = 11;                   // fc1 input scale of the first 
 // Timing-only switches (WRONG results; refused without -DASG_TIMING_EXPERIMENTS):
 // ASG_ROLLOUT_XSKIP bit 1: no batch row stores in the rollout tiles; bit 2: no one-hot W1
 // column gather (zeros); bit 4: fc1 slices that live in L2 read LDS slot 0 instead; bit 8:
-// h_t not loaded (constants); bit 16: h' not stored
+// h_t not loaded (constants); bit 16: h' not stored; bit 32: the tile's row stores go to a
+// small region that stays in L2 (env e & 7, batch row 1): same instructions, no HBM writes
 #if defined(ASG_ROLLOUT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
 #error "ASG_ROLLOUT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
 #endif
 #ifndef ASG_ROLLOUT_XSKIP
 #define ASG_ROLLOUT_XSKIP 0
-#endif
-// 1: the rollout issues a tile's h_t rows at the tile start, before its row stores (they then
-// wait for nothing the tile wrote: gfx9's vmcnt retires loads and stores in order); 0: after fc1
-#ifndef ASG_ROLLOUT_EARLY_H
-#define ASG_ROLLOUT_EARLY_H 0
 #endif
 
 __device__ __forceinline__ int h2_s0(const H2Args &a) { return a.pre ? (a.g.Pp >> 5) : 0; }
@@ -1116,7 +1112,10 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
         rows[nt] = e * n + ia[nt];
         act[nt] = (have_act && ok[nt]) ? (int)s_act[ia[nt]] : -1;
     }
-    float *obs_r = ra.obs + (int64_t)tsr * ra.E * n * K;
+    // row stores: batch row tsr (timing variant 32: row 1, env e & 7)
+    const int tss = (ASG_ROLLOUT_XSKIP & 32) ? 1 : tsr;
+    const int64_t sro = (ASG_ROLLOUT_XSKIP & 32) ? ((e & 7) - e) * n : 0;
+    float *obs_r = ra.obs + ((int64_t)tss * ra.E * n + sro) * K;
     // fc1 accumulators start from the one-hot block's W1 columns, gathered (and consumed)
     // before the tile's stores (a load behind them would wait for their acknowledgements:
     // gfx9's vmcnt retires memory operations in order); a rescaled retry gathers again
@@ -1136,23 +1135,9 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
             }
         }
     }
-#if ASG_ROLLOUT_EARLY_H
-    float4 hB[4][NT];
-    if (AGENT) {
-        const float *hin = pass == 0 ? ra.Hin : ra.Hout;
-        const int64_t hs = pass == 0 ? ra.hs : kHid;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                hB[t][nt] = (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
-                                                                            16 * t + 4 * q)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#endif
     if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
-        int64_t *oh_r = ra.onehot ? ra.onehot + (int64_t)(tsr - 1) * ra.E * n * m : nullptr;
+        int64_t *oh_r = ra.onehot ? ra.onehot + ((int64_t)(tss - 1) * ra.E * n + sro) * m : nullptr;
         for (int u = 0; u < Ub; ++u)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
@@ -1176,7 +1161,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                     }
                 }
         if (ra.avail) {
-            uint8_t *ab = ra.avail + ((int64_t)tsr * ra.E * n + row0) * m;
+            uint8_t *ab = ra.avail + ((int64_t)tss * ra.E * n + sro + row0) * m;
             const int nrow = GEN ? min(RT, n - RT * sub) : RT;
             int off0 = (GEN ? 1 : 16) * lane;
             asm volatile("" : "+v"(off0));  // not hoisted: a per-lane 64-bit address kept across loops spilled
@@ -1194,7 +1179,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
     const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));
     const u32x4v *W1g = ra.pk + 1;
     const int s0 = Ub, s_l2 = s0 + ra.w1_lds;
-    float *beta_r = ra.beta ? ra.beta + (int64_t)tsr * ra.E * n * m : nullptr;
+    float *beta_r = ra.beta ? ra.beta + ((int64_t)tss * ra.E * n + sro) * m : nullptr;
     const bool live = kk < T;  // rows past T are zeros: no bump parameters needed
     for (int attempt = 0;; ++attempt) {
         float scx[NT], rmax[NT];
@@ -1330,7 +1315,6 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
         a.sel.counter = ra.counter + (uint32_t)pass;
         a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
         // h_t rows, issued after fc1 (32 fewer VGPRs live through it)
-#if !ASG_ROLLOUT_EARLY_H
         const float *hin = pass == 0 ? ra.Hin : ra.Hout;
         const int64_t hs = pass == 0 ? ra.hs : kHid;
         float4 hB[4][NT];
@@ -1342,7 +1326,6 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                             : (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
                                                                               16 * t + 4 * q)
                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
         f32x4 xB[4][NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
