@@ -11,28 +11,38 @@
   4  256 x 256 dense benefits, 2,048 envs per GPU, BasicMAC + RNNAgent + epsilon-greedy
 Explicit --n/--m/--envs/--selector/--agent/--benefits override the config's values.
 
-One "step" = one transition of every env on every rank: action selection (agent forward +
-selector, writing the actions row of the EpisodeBatch) + one HIP env step kernel; every T
-steps an episode ends (returns all-gathered on the device) and the next one is reset inside
-the timed region; the host-side episode checks (device error words, selector status,
-logging) run once after it (GpuVecRunner.finish_episode(sync=False) / flush_pending).
-value = (sum over ranks of envs) * K / (max over ranks of the K-step time).
+One "step" = one transition of every env on every rank plus the action selection of the
+next row (agent forward + selector, writing the EpisodeBatch).  Default schedule (the
+runner's, args.fused_rollout): asg_reset, then the whole episode -- selection on the reset
+row, T transitions, the selections in between -- in ONE asg_rollout launch of the fused
+rollout kernel (env transition + RNNAgent forward + epsilon-greedy, csrc/asg_h2.hip); the
+timed window's edges cut episodes into chunks (select_first / select_last at the seams).
+--fused-rollout 3 times one launch per step, 0 the separate env-step and agent kernels.
+Every T steps an episode ends (returns all-gathered on the device) and the next one is
+reset inside the timed region; the host-side episode checks (device error words, selector
+status, logging) run once after it (GpuVecRunner.finish_episode(sync=False) /
+flush_pending).  value = (sum over ranks of envs) * K / (max over ranks of the K-step time).
 
 The JSON line also carries:
-  roofline        the env step kernel (the HIP hot path): algorithmic bytes per launch
-                  (B_step * E) / its mean duration, timed live with HIP events on
-                  the stream it is launched on, against the 8 TB/s HBM3E peak; `traffic` is the
-                  PMC-measured HBM bytes per launch from profiles/pmc_step_kernel*.json when one
-                  matches the workload.
-  roofline_agent  the agent forward (fused RNNAgent kernel) against its MFMA roof and HBM.
+  roofline        the dominant kernel: the fused rollout kernel (algorithmic bytes per step
+                  B_step + n (2*4*64 + 8) per env, DESIGN.md §3, over its mean HIP-event time per
+                  step on the stream it is launched on) against 8 TB/s; `traffic` = PMC HBM bytes
+                  (profiles/*pmc_rollout_kernel*.json), `issue` = its SQ figures, `bound` derived
+                  from them (HBM or the store-ordered latency).  On the split schedule: the env
+                  step kernel (SURVEY §8(d)'s B_step * E).
+  roofline_agent  the agent kernel (split-schedule leg) against its MFMA roof and HBM.
+  kernels_ms      per-step kernel times (fused rollout / env step / selection).
   cpu_baseline    rank 0 at N = 1 only: the reference's CPU design (subprocess-per-env
                   ParallelRunner + numpy env + CPU RNN agent, oracle/cpu_parallel_runner.py) on
                   a bounded sample of the same workload: step-loop-only and reset-amortised
                   rates, the worker count used and the host's core count.
-  secondary       (N = 1, --secondary 1, the default then) configs[2] read literally -- the
-                  PyTorch RNNAgent forward + asg_epsilon_greedy -- and the SAP selector (fused
-                  noise + LSA per env) with its LSA efficiency figure; each with its own
-                  value and ms_per_step.
+  secondary       (N = 1, --secondary 1, the default then; each leg with its own value and
+                  ms_per_step): split_rollout (separate launches), step_rollout (one fused
+                  launch per step), pytorch_agent (configs[2] read literally: the PyTorch
+                  RNNAgent + asg_epsilon_greedy), sap (fused noise + LSA per env, roofline_lsa
+                  against both issue bounds), iql / reda (the reference's mock algorithms:
+                  jumpstart_mac + HAA jumpstart, Linear agent, eps-greedy / SAP), config4
+                  (BASELINE configs[4]: 256 x 256 dense, 2,048 envs, fused rollout).
 """
 import argparse
 import glob

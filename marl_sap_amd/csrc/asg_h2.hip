@@ -241,10 +241,17 @@ __device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4
 // and the rollout kernel): xB = relu(fc1) fragments, hB = h_in rows (GRU).
 // ALLAV: every task is available (the rollout wrote avail = 1 itself).  act_lds (rollout):
 // also receives each row's selected task (index lrow0 + row within the tile).
-template <int NT, bool RNN, bool SEL, bool W2L, bool ALLAV, bool GEN>
+struct NoTailHook {
+    __device__ void operator()() const {}
+};
+
+// after_rec: called once the recurrent layer has consumed hB and stored h' (the rollout
+// issues the next agent tile's h_t loads there)
+template <int NT, bool RNN, bool SEL, bool W2L, bool ALLAV, bool GEN, class Hook = NoTailHook>
 __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
                                         const int64_t (&rows)[NT], const bool (&ok)[NT], const float4 (&hB)[4][NT],
-                                        const f32x4 (&xB)[4][NT], uint16_t *act_lds = nullptr, int lrow0 = 0) {
+                                        const f32x4 (&xB)[4][NT], uint16_t *act_lds = nullptr, int lrow0 = 0,
+                                        const Hook &after_rec = Hook{}) {
     // lane-derived addresses are recomputed here, not hoisted out of the callers' step / env
     // loops (there they would be live across every tile and spill; their reloads would wait
     // behind the tile stores in the in-order vmcnt queue)
@@ -447,6 +454,7 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
         }
     }
 
+    after_rec();
     // ---- fc2 (+ selection state), per-row scale --------------------------------------------
     int S3[NT];
     u32x4v hq[2][NT][2];
@@ -1086,10 +1094,23 @@ __device__ __forceinline__ void st_i64x2(int64_t *p, long long a, long long b) {
 // one-hot block and actions_onehot of the transition before it, avail, lookahead blocks,
 // beta) and, AGENT, run fc1 on the generated blocks plus the recurrent layer, fc2 and the
 // selection of row kk.  have_act: block 0 is onehot(s_act) (else zeros: the reset row).
+// The agent tile's h_t rows (RNN): hN holds them on entry when the previous agent tile
+// prefetched them (hpf), else they are loaded at the tile start; either way they are waited
+// for with the one-hot gather, before the tile's stores (a wait after fc1 would drain every
+// store of the tile: gfx9's vmcnt retires memory operations in order).  After the recurrent
+// layer the tile issues the NEXT agent tile's h_t loads into hN (nsrc: its source rows, row
+// nrow0 on, stride nhs; NULL source = zeros; nmode 0 = no next agent tile in this env).
+struct HNext {
+    const float *src;
+    int64_t stride, row0;
+    int mode;
+};
+
 template <bool RNN, bool W2L, bool GEN, bool AGENT>
 __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
-                                             uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4]) {
+                                             uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
+                                             f32x4 (&hN)[4][kH2NT], bool hpf, HNext nx) {
     constexpr int NT = kH2NT;
     constexpr int RT = 16 * NT;  // rows per tile
     // opaque env / row indices and lane: addresses are formed here from them, not hoisted out
@@ -1134,6 +1155,23 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                 acc[mt][nt] = f32x4{g.x, g.y, g.z, g.w} * scS;
             }
         }
+    }
+    if (AGENT && RNN) {
+        if (!hpf) {
+            const float *hin = pass == 0 ? ra.Hin : ra.Hout;
+            const int64_t hs = pass == 0 ? ra.hs : kHid;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    hN[t][nt] = hin ? *reinterpret_cast<const f32x4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs + 16 * t + 4 * q)
+                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        // waited for here, with the gather
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(hN[t][nt]));
     }
     if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
@@ -1314,18 +1352,14 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
         H2Args a = rollout_h2args(ra);
         a.sel.counter = ra.counter + (uint32_t)pass;
         a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
-        // h_t rows, issued after fc1 (32 fewer VGPRs live through it)
-        const float *hin = pass == 0 ? ra.Hin : ra.Hout;
-        const int64_t hs = pass == 0 ? ra.hs : kHid;
         float4 hB[4][NT];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
                 hB[t][nt] = (ASG_ROLLOUT_XSKIP & 8) ? make_float4(0.5f, 0.25f, -0.5f, 0.125f)
-                            : (RNN && hin) ? *reinterpret_cast<const float4 *>(hin + (ok[nt] ? rows[nt] : 0) * hs +
-                                                                              16 * t + 4 * q)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+                            : RNN ? make_float4(hN[t][nt][0], hN[t][nt][1], hN[t][nt][2], hN[t][nt][3])
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         f32x4 xB[4][NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -1337,7 +1371,22 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                 for (int v = 0; v < 4; ++v) xB[mt][nt][v] = fmaxf(acc[mt][nt][v] * un + bb[v], 0.f);
             }
         }
-        h2_tail<NT, RNN, true, W2L, true, GEN>(a, Wl, sw, row0, rows, ok, hB, xB, s_act, RT * sub);
+        // the next agent tile's h_t, issued once this tile's recurrent layer is done
+        auto prefetch = [&]() {
+            if (!RNN || nx.mode == 0) return;
+            const int64_t nb = e * n + nx.row0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int ni = (int)nx.row0 + 16 * nt + r;
+                    const bool nok = !GEN || ni < n;
+                    hN[t][nt] = nx.src ? *reinterpret_cast<const f32x4 *>(nx.src + (nok ? nb + 16 * nt + r : 0) * nx.stride +
+                                                                        16 * t + 4 * q)
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+        };
+        h2_tail<NT, RNN, true, W2L, true, GEN>(a, Wl, sw, row0, rows, ok, hB, xB, s_act, RT * sub, prefetch);
     }
 }
 
@@ -1381,24 +1430,39 @@ rollout_kernel(RolloutArgs ra) {
         // every other iteration: transition k, then the agent tiles of row k + 1 (or, past the
         // launch's last selection, the row alone) -- one call site per tile kind
         const int sf = ra.select_first ? 1 : 0;
+        const int nit = ra.k1 - ra.k0 + sf;
         int pass = 0;
-        for (int it = 0; it < ra.k1 - ra.k0 + sf; ++it) {
+        f32x4 hN[4][kH2NT];  // the next agent tile's h_t rows (prefetched by the tile before it)
+        bool hpf = false;
+        auto has_agent = [&](int it) {
+            const int kk = ra.k0 + it - sf + 1;
+            return it < nit && kk < ra.T && (kk < ra.k1 || ra.select_last);
+        };
+        for (int it = 0; it < nit; ++it) {
             const int k = ra.k0 + it - sf;  // k0 - 1 on the select_first iteration
             const int ts = ra.ts0 + (k - ra.k0);
             const bool first_sel = it < sf;
             if (!first_sel)
                 rollout_transition(ra, e, k, ts, k == ra.k0 && !sf, key, s_scl, s_cnt, s_act, s_prev, ret);
             const int kk = k + 1;
-            const bool agent = kk < ra.T && (kk < ra.k1 || ra.select_last);
-            if (agent) {
-                for (int sub = 0; sub < ntile; ++sub)
+            if (has_agent(it)) {
+                const bool next_agent = has_agent(it + 1);
+                for (int sub = 0; sub < ntile; ++sub) {
+                    // the next agent tile: this pass's next tile (same h_t source), else tile 0
+                    // of the next pass (h_t = the h' this pass writes)
+                    HNext nx{nullptr, kHid, 0, 0};
+                    if (sub + 1 < ntile) nx = HNext{pass == 0 ? ra.Hin : ra.Hout, pass == 0 ? ra.hs : kHid,
+                                                    (int64_t)(16 * kH2NT) * (sub + 1), 1};
+                    else if (next_agent) nx = HNext{ra.Hout, kHid, 0, 1};
                     rollout_tile<RNN, W2L, GEN, true>(ra, e, sub, kk, ts + 1, !first_sel, !first_sel, pass, key, s_scl,
-                                                      s_act, s_h2, sw);
+                                                      s_act, s_h2, sw, hN, hpf, nx);
+                    hpf = nx.mode != 0;
+                }
                 ++pass;
             } else {
                 for (int sub = 0; sub < ntile; ++sub)
                     rollout_tile<RNN, W2L, GEN, false>(ra, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
-                                                       sw);
+                                                       sw, hN, false, HNext{nullptr, kHid, 0, 0});
             }
             wave_lds_fence();
         }
