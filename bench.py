@@ -173,7 +173,13 @@ def pmc_lookup(pattern, **match):
     return None
 
 
-def fused_roofline(a, E, fused_ms, use_rnn=True):
+def reset_bytes(n, m, L):
+    """Algorithmic HBM bytes of one env's reset (asg_reset): the pre-transition row (obs f32
+    n*m*(L+1), beta f32 n*m, avail n*m) plus prev_assigns i64 n and filled 8 B."""
+    return n * m * (4 * (L + 1) + 4 + 1) + 8 * n + 8
+
+
+def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
     """Roofline of the fused rollout kernel (asg_rollout -> rollout_kernel), per env step: the
     env step's bytes plus the agent's h in / h out and the action written -- the observations
     it generates are consumed on chip, never read back -- per env, times E, over its HIP-event
@@ -182,7 +188,10 @@ def fused_roofline(a, E, fused_ms, use_rnn=True):
     profiled (tools/round_profile.sh): "latency/store-ack" when neither VALU issue nor the
     MFMA pipe is at half its capacity and HBM is not near its roof (the waves wait on the
     in-order vmcnt queue behind their own row stores)."""
-    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)) * E
+    # the episode's reset runs in its first launch (asg_reset_rollout): its row counts too
+    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)
+                  + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E
+    per_launch = int(round(per_launch))
     achieved = per_launch / (fused_ms * 1e-3) / 1e9
     frac = achieved / HBM_PEAK_GBS
     pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
@@ -205,7 +214,9 @@ def fused_roofline(a, E, fused_ms, use_rnn=True):
            "traffic": round(pm["hbm_bytes_per_launch"] / pm.get("steps_per_launch", 1)) if pm else None,
            "kernel": "asg::rollout_kernel (env steps + agent/eps-greedy selections, per step)",
            "kernel_ms": round(fused_ms, 4), "bytes_per_launch": per_launch,
-           "per_launch_note": "per env step of the launch (bytes_per_launch, kernel_ms: one step's share)",
+           "per_launch_note": "per env step of the launch (bytes_per_launch, kernel_ms: one step's share; "
+                              "the fused resets' rows amortised over the timed steps)",
+           "resets_per_step": round(resets_per_step, 4),
            "frac_note": "frac is against the 8 TB/s HBM peak"}
     if pm:
         out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
@@ -241,6 +252,9 @@ def parse(argv=None):
                         "(asg_rollout); 3: one asg_rollout launch per step (env step t + selection t + 1); 0: separate "
                         "asg_step + agent select launches; 2: as 1")
     p.add_argument("--use-rnn", type=int, default=1, help="0: the Linear + ReLU RNNAgent (use_rnn: False)")
+    p.add_argument("--fuse-reset", type=int, default=1,
+                   help="1 (default, the runner's): on the episode schedule the env reset runs in the episode's "
+                        "first launch (asg_reset_rollout); 0: asg_reset as its own launch")
     a = p.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("n", "m", "envs", "selector", "agent", "benefits"):
@@ -362,13 +376,18 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     def new_episode():
         if runner.batch is not None and runner.env.k == a.T:
             runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
-        runner.reset()
+        runner.reset(env_reset=False)
         mac.init_hidden(E)
         state["t"] = 0
         state["selected"] = False
-        # planned per episode, as GpuVecRunner.rollout does (JumpstartMAC draws its flips here)
+        # planned per episode, as GpuVecRunner.rollout does (JumpstartMAC draws its flips here);
+        # on the episode schedule the env reset runs in the episode's first launch
+        # (asg_reset_rollout), else as its own launch
         with torch.no_grad():
             state["mode"] = None if selector == "random" else mac.fused_mode(env, runner.batch, runner.t_env)
+        state["fuse_reset"] = state["mode"] == "episode" and bool(a.fuse_reset)
+        if not state["fuse_reset"]:
+            env.reset(runner.batch, ts=0)
 
     def advance(s_):
         """s_ transitions (+ their selections) of the current episode in one asg_rollout launch"""
@@ -378,10 +397,14 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
             eps, seed, counter, status, _ = mac.action_selector.fused_params(runner.t_env, False, dev,
                                                                              calls=s_ + sf + sl - 1)
 
+            rs = sf and state.pop("fuse_reset", False)
+
             def launch():
                 mac.hidden_states = env.rollout(runner.batch, t, s_, mac.selector_agent, mac.hidden_states, eps, seed,
-                                                counter, status, select_first=sf, select_last=sl)
+                                                counter, status, select_first=sf, select_last=sl, reset=rs)
             timed(fused_pairs, launch, s_)
+            if rs and state["timing"]:
+                state["fused_resets"] = state.get("fused_resets", 0) + 1
         state["t"] = t + s_
 
     def one_step():
@@ -432,7 +455,8 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     res = {"elapsed": elapsed, "warmup_elapsed": warm_elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
            "lsa_ms": mean(lsa_pairs) if lsa_pairs else None,
            "fused_ms": mean(fused_pairs) if fused_pairs else None, "mode": state.get("mode"),
-           "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs)}
+           "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs),
+           "fused_resets": state.get("fused_resets", 0)}
     if count_lsa and selector == "sap" and a.n <= a.m <= 64:
         # one more selection on the current state, with the step-counting kernel instance
         sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
@@ -457,6 +481,11 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res
+
+
+def res_resets(res):
+    """Fused resets per timed step of a leg (asg_reset_rollout launches in the timed window)."""
+    return res.get("fused_resets", 0) / res["fused_steps"] if res.get("fused_steps") else 0.0
 
 
 def lsa_roofline(a, E, res):
@@ -515,7 +544,7 @@ def main():
     value = G * a.steps / res["elapsed"]
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     if res.get("fused_ms"):
-        roof = fused_roofline(a, E, res["fused_ms"])
+        roof = fused_roofline(a, E, res["fused_ms"], resets_per_step=res_resets(res))
     else:
         per_launch = step_bytes(a.n, a.m, a.L) * E
         achieved = per_launch / (kern_ms * 1e-3) / 1e9
@@ -591,7 +620,8 @@ def main():
                                    "select": round(rj["sel_ms"], 4) if rj["sel_ms"] else None,
                                    "sap_select": round(rj["lsa_ms"], 4) if rj.get("lsa_ms") else None}}
                 if rj.get("fused_ms"):
-                    extra[name]["roofline"] = fused_roofline(a, E, rj["fused_ms"], use_rnn=False)
+                    extra[name]["roofline"] = fused_roofline(a, E, rj["fused_ms"], use_rnn=False,
+                                                             resets_per_step=res_resets(rj))
         if a.config == 2 and world == 1:
             # BASELINE configs[4] on this GPU: 256 x 256 dense benefits, 2,048 envs, the same
             # BasicMAC + RNNAgent + eps-greedy on the fused rollout schedule
@@ -608,7 +638,7 @@ def main():
                                   "env_step": round(r5["kern_ms"], 4) if r5["kern_ms"] else None,
                                   "select": round(r5["sel_ms"], 4) if r5["sel_ms"] else None}}
             if r5.get("fused_ms"):
-                leg["roofline"] = fused_roofline(c4, c4.envs, r5["fused_ms"])
+                leg["roofline"] = fused_roofline(c4, c4.envs, r5["fused_ms"], resets_per_step=res_resets(r5))
             extra["config4"] = leg
 
     if a.selector == "random":

@@ -46,7 +46,8 @@
  *   asg_rollout                the runner loop select(0); for t: env.step(t) +
  *                              mac.select_actions(t + 1), fused for a range of steps up to a whole
  *                              episode (episode_runner.py:60-127 / parallel_runner.py:113-200);
- *                              asg_step_select = one step of it
+ *                              asg_step_select = one step of it; asg_reset_rollout = env.reset()
+ *                              (mock_constellation_env.py:94-114) + the whole loop in one launch
  */
 #ifndef ASG_H
 #define ASG_H
@@ -330,6 +331,15 @@ int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int s
                 const void *packed, const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K,
                 int hidden, int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon,
                 uint64_t seed, uint64_t counter, int32_t *status, void *hip_stream);
+/* asg_reset(ts) then asg_rollout(ts, steps, select_first = 1, select_last) in ONE launch: the
+ * reset (a fresh Philox episode key, prev_assigns from the permutation draw, returns = 0, the
+ * pre-transition row ts) runs in the rollout kernel's env prologue and its first selection
+ * pass, which stores the reset row it generates.  Batch, returns, hidden state and actions
+ * equal asg_reset + asg_rollout.  Philox bump/dense benefits only. */
+int asg_reset_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_last, const void *packed,
+                      const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K, int hidden,
+                      int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon, uint64_t seed,
+                      uint64_t counter, int32_t *status, void *hip_stream);
 /* asg_rollout with steps = 1, select_first = 0, select_last = 1 and the GRU agent: asg_step
  * at row ts then asg_rnn_agent_select for row ts + 1 (the round-2 per-step entry point). */
 int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,

@@ -83,14 +83,15 @@ class BasicMAC:
         self.hidden_states = env.step_select(ep_batch, t_ep, self.selector_agent, self.hidden_states, eps, seed,
                                              counter, status)
 
-    def fused_episode(self, env, ep_batch, t_env, test_mode=False):
+    def fused_episode(self, env, ep_batch, t_env, test_mode=False, reset=False):
         """select_actions(0), then env.step(t) + select_actions(t + 1) for the whole episode
         (the last step without a selection after it) in ONE kernel launch; selector counters
-        and the hidden state advance as T select_actions calls would advance them."""
+        and the hidden state advance as T select_actions calls would advance them.  reset:
+        the env's reset() runs in the same launch (the runner then skips it)."""
         T = env.T
         eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device, calls=T)
         self.hidden_states = env.rollout(ep_batch, 0, T, self.selector_agent, self.hidden_states, eps, seed, counter,
-                                         status, select_first=True, select_last=False)
+                                         status, select_first=True, select_last=False, reset=reset)
 
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)

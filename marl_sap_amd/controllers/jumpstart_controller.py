@@ -54,9 +54,9 @@ class JumpstartMAC(BasicMAC):
             return None
         return "episode" if base == "episode" and not any(self._flips) else "step"
 
-    def fused_episode(self, env, ep_batch, t_env, test_mode=False):
+    def fused_episode(self, env, ep_batch, t_env, test_mode=False, reset=False):
         self._flips = []  # all RL: consumed by the one kernel
-        super().fused_episode(env, ep_batch, t_env, test_mode)
+        super().fused_episode(env, ep_batch, t_env, test_mode, reset=reset)
 
     def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
         """env.step(t) and select_actions(t + 1): one kernel when the flip for t + 1 picks the

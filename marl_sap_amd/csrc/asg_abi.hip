@@ -523,21 +523,27 @@ static void *tm_base(const asg_field &f, int64_t E, int64_t d2, int64_t d3, int6
 int asg_step_select_l2_slices(int n, int m, int L) { return asg::rollout_l2_slices(n, m, L, 1); }
 int asg_rollout_l2_slices(int n, int m, int L, int use_rnn) { return asg::rollout_l2_slices(n, m, L, use_rnn); }
 
-int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_first, int select_last,
-                const void *packed, const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K,
-                int hidden, int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon,
-                uint64_t seed, uint64_t counter, int32_t *status, void *hip_stream) {
+// asg_rollout and asg_reset_rollout (reset: the envs' reset runs in the same launch, before
+// the selection on row ts)
+static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_first, int select_last,
+                        int reset, const void *packed, const float *b1, const float *b_r0, const float *b_r1,
+                        const float *b2, int K, int hidden, int use_rnn, const float *h_in, int64_t h_stride,
+                        float *h_out, double epsilon, uint64_t seed, uint64_t counter, int32_t *status,
+                        void *hip_stream) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (int rc = check_view(h, b, ts, true)) return rc;
     if (!packed || !b1 || !b_r0 || (use_rnn && !b_r1) || !b2 || !h_out || !status)
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: NULL agent argument");
     const asg::EnvState &st = h->st;
-    if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
-    if (steps < 1 || h->k + steps > st.T)
+    if (!h->has_reset && !reset) return fail(h, ASG_E_STATE, "step called before reset");
+    if (reset && (st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED))
+        return fail(h, ASG_E_INVALID_ARG, "asg_reset_rollout: Philox bump/dense benefits only");
+    const int k0 = reset ? 0 : h->k;
+    if (steps < 1 || k0 + steps > st.T)
         return fail(h, ASG_E_STATE, "asg_rollout: steps must be >= 1 and stay within the episode (k + steps <= T)");
-    if (select_first && h->k != 0)
+    if (select_first && k0 != 0)
         return fail(h, ASG_E_STATE, "asg_rollout: select_first selects on the reset row (k == 0 only)");
-    if (select_last && h->k + steps >= st.T)
+    if (select_last && k0 + steps >= st.T)
         return fail(h, ASG_E_STATE, "asg_rollout: select_last needs a next step to select for (k + steps < T)");
     if (st.bids || st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED)
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: Philox bump/dense benefits with integer actions only");
@@ -566,12 +572,33 @@ int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int s
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: needs a contiguous time-major batch (EpisodeBatch(time_major=True))");
     DeviceGuard g(h->device);
     hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
-    hipError_t e = asg::launch_rollout(sl, st, ts, h->k, steps, select_first, select_last,
+    if (reset && h->has_reset) h->st.episode += 1;  // as asg_reset: a fresh Philox key per episode
+    hipError_t e = asg::launch_rollout(sl, h->st, ts, k0, steps, select_first, select_last, reset,
                                        static_cast<const float4 *>(packed), b1, b_r0, b_r1, b2, use_rnn, h_in, h_stride,
                                        h_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);
     if (e != hipSuccess) return hip_fail(h, e, "asg_rollout");
-    h->k += steps;
+    if (reset) {
+        h->constructed = true;
+        h->has_reset = true;
+    }
+    h->k = k0 + steps;
     return ASG_OK;
+}
+
+int asg_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_first, int select_last,
+                const void *packed, const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K,
+                int hidden, int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon,
+                uint64_t seed, uint64_t counter, int32_t *status, void *hip_stream) {
+    return rollout_impl(h, b, ts, steps, select_first, select_last, 0, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn,
+                        h_in, h_stride, h_out, epsilon, seed, counter, status, hip_stream);
+}
+
+int asg_reset_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int select_last, const void *packed,
+                      const float *b1, const float *b_r0, const float *b_r1, const float *b2, int K, int hidden,
+                      int use_rnn, const float *h_in, int64_t h_stride, float *h_out, double epsilon, uint64_t seed,
+                      uint64_t counter, int32_t *status, void *hip_stream) {
+    return rollout_impl(h, b, ts, steps, 1, select_last, 1, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in,
+                        h_stride, h_out, epsilon, seed, counter, status, hip_stream);
 }
 
 int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,

@@ -967,6 +967,7 @@ struct RolloutArgs {
     int n, m, T, L, dense;
     float wmin, wmax;
     int k0, k1, select_first, select_last;
+    int reset;  // the envs' reset (asg_reset) runs first, in this launch
     // agent
     const u32x4v *pk;
     const float *W1T, *Hin;
@@ -1175,7 +1176,8 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
     }
     if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
-        int64_t *oh_r = ra.onehot ? ra.onehot + ((int64_t)(tss - 1) * ra.E * n + sro) * m : nullptr;
+        // actions_onehot of the transition before the row (none before the reset row)
+        int64_t *oh_r = (ra.onehot && have_act) ? ra.onehot + ((int64_t)(tss - 1) * ra.E * n + sro) * m : nullptr;
         for (int u = 0; u < Ub; ++u)
 #pragma unroll
             for (int c = 0; c < 2; ++c)
@@ -1420,11 +1422,41 @@ rollout_kernel(RolloutArgs ra) {
             const uint64_t bits = __ballot(ten);
             if (lane == 0) s_scl[c] = bits;
         }
-        for (int i = lane; i < np; i += 64) {
-            s_prev[i] = (uint16_t)(i < n ? ra.prev[e * n + i] : 0);
-            s_act[i] = 0;
+        if (ra.reset) {
+            // asg_reset (reset_kernel): prev_assigns = the first n of a Philox Fisher-Yates
+            // permutation of the m tasks (choice(m, n, replace=False), mock :99-105), drawn
+            // from the top; the draws are independent of the permutation, so the lanes make
+            // them in parallel and one lane applies the swaps (u16 halves of s_cnt: perm, draw)
+            uint16_t *s_perm = reinterpret_cast<uint16_t *>(s_cnt), *s_jj = s_perm + mp;
+            for (int j = lane; j < m; j += 64) {
+                s_perm[j] = (uint16_t)j;
+                const u32x4 rr = philox4x32_10(u32x4{(uint32_t)j, 0u, kCtrPerm, ra.episode}, key.k0, key.k1);
+                s_jj[j] = (uint16_t)(((uint64_t)rr.x * (uint64_t)(j + 1)) >> 32);
+            }
+            wave_lds_fence();
+            if (lane == 0)
+                for (int i = m - 1; i >= 1; --i) {
+                    const int jj = s_jj[i];
+                    const uint16_t t = s_perm[i];
+                    s_perm[i] = s_perm[jj];
+                    s_perm[jj] = t;
+                }
+            wave_lds_fence();
+            for (int i = lane; i < np; i += 64) {
+                const int p = i < n ? (int)s_perm[i] : 0;
+                s_prev[i] = (uint16_t)p;
+                s_act[i] = 0;
+                if (i < n && ra.prevb)
+                    ra.prevb[((int64_t)ra.ts0 * ra.E + e) * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : p;
+            }
+            if (lane == 0 && ra.filled) ra.filled[(int64_t)ra.ts0 * ra.E + e] = 1;
+        } else {
+            for (int i = lane; i < np; i += 64) {
+                s_prev[i] = (uint16_t)(i < n ? ra.prev[e * n + i] : 0);
+                s_act[i] = 0;
+            }
         }
-        double ret = lane == 0 ? ra.returns[e] : 0.0;
+        double ret = (lane == 0 && !ra.reset) ? ra.returns[e] : 0.0;
         wave_lds_fence();
         // iteration 0 with select_first: the selection on the reset row (no transition);
         // every other iteration: transition k, then the agent tiles of row k + 1 (or, past the
@@ -1454,8 +1486,9 @@ rollout_kernel(RolloutArgs ra) {
                     if (sub + 1 < ntile) nx = HNext{pass == 0 ? ra.Hin : ra.Hout, pass == 0 ? ra.hs : kHid,
                                                     (int64_t)(16 * kH2NT) * (sub + 1), 1};
                     else if (next_agent) nx = HNext{ra.Hout, kHid, 0, 1};
-                    rollout_tile<RNN, W2L, GEN, true>(ra, e, sub, kk, ts + 1, !first_sel, !first_sel, pass, key, s_scl,
-                                                      s_act, s_h2, sw, hN, hpf, nx);
+                    // the reset row (select_first) is stored here when the reset runs in this launch
+                    rollout_tile<RNN, W2L, GEN, true>(ra, e, sub, kk, ts + 1, !first_sel || ra.reset, !first_sel, pass,
+                                                      key, s_scl, s_act, s_h2, sw, hN, hpf, nx);
                     hpf = nx.mode != 0;
                 }
                 ++pass;
@@ -1487,7 +1520,7 @@ int rollout_l2_slices(int n, int m, int L, int use_rnn) {
 }
 
 hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
-                          int select_last, const float4 *packed, const float *b1, const float *bi, const float *bh,
+                          int select_last, int reset, const float4 *packed, const float *b1, const float *bi, const float *bh,
                           const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
                           uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s) {
     const int K = st.m * (st.L + 1), nout = st.m;
@@ -1525,6 +1558,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.k1 = k0 + steps;
     ra.select_first = select_first;
     ra.select_last = select_last;
+    ra.reset = reset;
     ra.W1T = reinterpret_cast<const float *>(packed);
     ra.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
     ra.Hin = Hin;

@@ -133,7 +133,7 @@ struct RolloutSlabs {
 bool rollout_shape_ok(int n, int m, int L, int K);
 int rollout_l2_slices(int n, int m, int L, int use_rnn);
 hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
-                          int select_last, const float4 *packed, const float *b1, const float *bi, const float *bh,
+                          int select_last, int reset, const float4 *packed, const float *b1, const float *bi, const float *bh,
                           const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
                           uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,

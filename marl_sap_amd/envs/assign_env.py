@@ -165,21 +165,27 @@ class AssignEnvBatch(MultiAgentEnv):
                             select_last=True)
 
     def rollout(self, batch, ts, steps, agent, hidden_state, epsilon, seed, counter, status, select_first=True,
-                select_last=False):
+                select_last=False, reset=False):
         """asg_rollout: `steps` env transitions from the current step (batch rows ts ..) with
         the agent forward + epsilon-greedy selections in between, in one kernel --
         select_first: also the selection on the reset row ts (k == 0); select_last: also the
         selection after the last transition.  The selections use Philox counters counter,
         counter + 1, ... in row order.  Returns the hidden state after the last selection
         [E n, hidden] (the MAC's hidden_states).  A whole episode after reset():
-        rollout(batch, 0, T, ...)."""
+        rollout(batch, 0, T, ...); reset=True folds that reset() into the same launch
+        (asg_reset_rollout; implies select_first)."""
         args = agent.step_select_args(hidden_state, batch["obs"].shape[-1], self.device, self.num_envs * self.n)
         h_out = args[-1]
-        self._call("asg_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps), int(bool(select_first)),
-                   int(bool(select_last)), *args[:-1], ctypes.c_void_p(h_out.data_ptr()), float(epsilon),
-                   seed & 0xFFFFFFFFFFFFFFFF, int(counter), ctypes.c_void_p(status.data_ptr()),
-                   _lib.stream_ptr(self.device))
-        self.k += int(steps)
+        tail = (*args[:-1], ctypes.c_void_p(h_out.data_ptr()), float(epsilon), seed & 0xFFFFFFFFFFFFFFFF, int(counter),
+                ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(self.device))
+        if reset:
+            self._call("asg_reset_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps),
+                       int(bool(select_last)), *tail)
+            self.k = int(steps)
+        else:
+            self._call("asg_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps), int(bool(select_first)),
+                       int(bool(select_last)), *tail)
+            self.k += int(steps)
         return h_out
 
     def random_actions(self, batch, ts):

@@ -86,10 +86,11 @@ class GpuVecRunner:
     def close_env(self):
         self.env.close()
 
-    def reset(self):
+    def reset(self, env_reset=True):
         if self.batch is None or not self.reuse_batch:
             self.batch = self.new_batch()
-        self.env.reset(self.batch, ts=0)
+        if env_reset:
+            self.env.reset(self.batch, ts=0)
         self.t = 0
 
     # ------------------------------------------------------------------ rollout
@@ -100,13 +101,15 @@ class GpuVecRunner:
         kernel (asg_rollout, mode "episode"), or one kernel per step ("step"): the
         observations are generated on chip and never re-read, and the batch is the separate
         launches' bit for bit."""
-        self.reset()
+        self.reset(env_reset=False)
         self.mac.init_hidden(batch_size=self.batch_size)
         mode = self.mac.fused_mode(self.env, self.batch, self.t_env, test_mode) \
             if hasattr(self.mac, "fused_mode") else None
         if mode == "episode":
-            self.mac.fused_episode(self.env, self.batch, self.t_env, test_mode)
+            # the env reset runs in the episode's launch (asg_reset_rollout)
+            self.mac.fused_episode(self.env, self.batch, self.t_env, test_mode, reset=True)
         else:
+            self.env.reset(self.batch, ts=0)
             self.select_into_batch(0, test_mode)
             for t in range(self.T):
                 if mode == "step" and t + 1 < self.T:
