@@ -23,13 +23,6 @@ struct u32x4 {
 #ifndef ASG_PHILOX_BITOP3
 #define ASG_PHILOX_BITOP3 1
 #endif
-#ifndef ASG_BUMP_RCP
-#define ASG_BUMP_RCP 1
-#endif
-// 1: one Philox call per two (agent, task) pairs (philox_bump32x2)
-#ifndef ASG_BUMP_PAIR2
-#define ASG_BUMP_PAIR2 1
-#endif
 __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -76,7 +69,7 @@ __device__ __forceinline__ double bump_value(double scale, double center, double
 
 // purposes of Philox counters (counter.z); counter.w = episode
 enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u,
-                  kCtrSapNoise = 7u, kCtrPair2 = 8u };
+                  kCtrSapNoise = 7u, kCtrPair2 = 8u, kCtrPair4 = 9u };
 
 // "a beats b" in torch.max order: NaN wins, then larger value, then smaller index.
 // Branch-free (bitwise on the predicates) so it lowers to compares + v_cndmask.
@@ -99,10 +92,10 @@ __device__ __forceinline__ EnvKey env_key(uint64_t seed, int64_t global_env) {
 // generate_benefits_over_time, mock_constellation_env.py:281-293): active with probability
 // 0.25 (rand() > 0.75), center ~ U(0, T), width ~ U(wmin, wmax),
 // sigma_2 = sqrt(w^2 / -8 / ln 0.05), value(t) = scale * exp(-(t - c)^2 / sigma_2 / 2)
-// = scale * 2^(-(t - c)^2 * a2) with a2 = log2(e) / (2 sigma_2).  One Philox call per two
-// pairs (ASG_BUMP_PAIR2; one per pair before); the per-task scale (choice([1,1,1,10])) is a per-task draw.  The parameters are float32
-// values; the center is drawn on a grid of 2^-q with q = 24 - bits(T), so t - center is
-// exact in float32 for every integer t < T.
+// = scale * 2^(-(t - c)^2 * a2) with a2 = log2(e) / (2 sigma_2).  One Philox call serves
+// four pairs (one 32-bit word each); the per-task scale (choice([1,1,1,10])) is a per-task
+// draw.  The parameters are float32 values; the center is drawn on a grid of 2^-q with
+// q = 24 - bits(T), so t - center is exact in float32 for every integer t < T.
 struct Bump32 {
     float scale;  // 0 when the pair is inactive
     float center;
@@ -125,63 +118,41 @@ __host__ __device__ inline BumpShape bump_shape(int T, float wmin, float wmax) {
     return BumpShape{T, 24 - bits, wmin, wmax - wmin};
 }
 
-#if ASG_BUMP_PAIR2
-// One Philox call serves two pairs (2k, 2k + 1): a pair needs a 32-bit center word, 24
-// bits of width and 2 activity bits, so 116 of the 128 bits are used, each by one pair.
-//   pair 2k:     center x, width y[31:8], active y[1:0] == 3
-//   pair 2k + 1: center w, width z[31:8], active y[3:2] == 3
-__device__ __forceinline__ Bump32 bump_from_words(uint32_t cw, uint32_t w24, uint32_t act2, float scale,
-                                                  const BumpShape &bs, bool dense) {
+// Pair 4k + s takes word s of Philox call k (counter {k, 0, kCtrPair4, episode}):
+//   center = T * u16 on the 2^-q grid, u16 = w[31:16] * 2^-16: floor(u16 T 2^q) 2^-q
+//   width  = wmin + (wmax - wmin) * w[15:2] * 2^-14
+//   active = w[1:0] == 3 (probability 1/4)
+// (42 bits of entropy per pair are plenty for a bump; one Philox call per four pairs halves
+// the generator's share of the fused rollout's VALU against one per two pairs.)
+__device__ __forceinline__ Bump32 bump_from_word(uint32_t w, float scale, const BumpShape &bs, bool dense) {
     Bump32 b;
-    b.scale = (dense || act2 == 3u) ? scale : 0.0f;  // rand() > 0.75: probability 1/4
-    // center = T * u on the 2^-q grid: floor(u * T * 2^q) * 2^-q, u = cw * 2^-32; the grid
-    // index is < T * 2^q <= 2^24, so the 32-bit convert is exact
-    b.center = __builtin_ldexpf((float)(uint32_t)(((uint64_t)cw * (uint64_t)(uint32_t)bs.T) >> (32 - bs.q)), -bs.q);
-    const float spread = bs.wmin + bs.wspan * ((float)w24 * 0x1p-24f);
+    b.scale = (dense || (w & 3u) == 3u) ? scale : 0.0f;
+    // the grid index (w >> 16) * T * 2^q / 2^16 is < T * 2^q <= 2^24: the 32-bit convert is exact
+    b.center = __builtin_ldexpf(
+        (float)(uint32_t)((((uint64_t)(w >> 16) * (uint64_t)(uint32_t)bs.T) << bs.q) >> 16), -bs.q);
+    const float spread = bs.wmin + bs.wspan * ((float)((w >> 2) & 0x3fffu) * 0x1p-14f);
     // log2(e) / (2 sigma_2), sigma_2 = sqrt(spread^2 / -8 / ln 0.05), is for spread > 0
     // log2(e) sqrt(-2 ln 0.05) / spread: one v_rcp_f32 (<= 1 ulp) and a multiply (within
     // 3e-7 relative of the float64 formula; parity checks use the exported parameters)
     b.a2 = 0x1.c4035ap+1f * __builtin_amdgcn_rcpf(spread);
     return b;
 }
-__device__ __forceinline__ void philox_bump32x2(EnvKey key, uint32_t episode, int pair0, float scale0, float scale1,
-                                                const BumpShape &bs, bool dense, Bump32 &b0, Bump32 &b1) {
-    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair0 >> 1, 0u, kCtrPair2, episode}, key.k0, key.k1);
-    b0 = bump_from_words(r.x, r.y >> 8, r.y & 3u, scale0, bs, dense);
-    b1 = bump_from_words(r.w, r.z >> 8, (r.y >> 2) & 3u, scale1, bs, dense);
+// pairs pair0 .. pair0 + 3 (pair0 % 4 == 0): one Philox call
+__device__ __forceinline__ void philox_bump32x4(EnvKey key, uint32_t episode, int pair0, const float (&scale)[4],
+                                                const BumpShape &bs, bool dense, Bump32 (&b)[4]) {
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair0 >> 2, 0u, kCtrPair4, episode}, key.k0, key.k1);
+    b[0] = bump_from_word(r.x, scale[0], bs, dense);
+    b[1] = bump_from_word(r.y, scale[1], bs, dense);
+    b[2] = bump_from_word(r.z, scale[2], bs, dense);
+    b[3] = bump_from_word(r.w, scale[3], bs, dense);
 }
 __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale,
                                                 const BumpShape &bs, bool dense) {
-    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair >> 1, 0u, kCtrPair2, episode}, key.k0, key.k1);
-    return (pair & 1) ? bump_from_words(r.w, r.z >> 8, (r.y >> 2) & 3u, scale, bs, dense)
-                      : bump_from_words(r.x, r.y >> 8, r.y & 3u, scale, bs, dense);
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair >> 2, 0u, kCtrPair4, episode}, key.k0, key.k1);
+    const int s = pair & 3;
+    const uint32_t w = s == 0 ? r.x : (s == 1 ? r.y : (s == 2 ? r.z : r.w));
+    return bump_from_word(w, scale, bs, dense);
 }
-#else
-__device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale,
-                                                const BumpShape &bs, bool dense) {
-    const u32x4 r = philox4x32_10(u32x4{(uint32_t)pair, 0u, kCtrPair, episode}, key.k0, key.k1);
-    constexpr float k2m32 = 2.3283064365386963e-10f;  // 2^-32
-    const bool active = dense || r.x >= 0xC0000000u;
-    Bump32 b;
-    b.scale = active ? scale : 0.0f;
-    // center = T * u on the 2^-q grid: floor(u * T * 2^q) * 2^-q, u = r.y * 2^-32 (< T * 2^q <= 2^24: exact)
-    // (the grid index is < 2^24: a 32-bit convert is exact)
-    b.center = __builtin_ldexpf((float)(uint32_t)(((uint64_t)r.y * (uint64_t)(uint32_t)bs.T) >> (32 - bs.q)), -bs.q);
-    const float spread = bs.wmin + bs.wspan * ((float)r.z * k2m32);
-#if ASG_BUMP_RCP
-    // log2(e) / (2 sigma_2) with sigma_2 = sqrt(spread^2 / -8 / ln 0.05) is, for spread > 0,
-    // log2(e) sqrt(-2 ln 0.05) / spread: one v_rcp_f32 (<= 1 ulp) and a multiply instead of a
-    // correctly rounded sqrt and two divisions (~30 instructions per pair).  Within 3e-7
-    // relative of the float64 formula; every kernel derives the parameters through this one
-    // function and the parity checks use the exported values (asg_export_bump_params).
-    b.a2 = 0x1.c4035ap+1f * __builtin_amdgcn_rcpf(spread);
-#else
-    const float s2 = sqrtf(spread * spread * -0.125f / (float)kLog005);  // "/ -8" exactly
-    b.a2 = 0.72134752044448170f / s2;  // log2(e) / 2 / sigma_2
-#endif
-    return b;
-}
-#endif
 
 __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, int pair, float scale, int T,
                                                 float wmin, float wmax, bool dense) {

@@ -43,17 +43,19 @@ struct BumpSrc {  // Philox, float32 bumps regenerated on the fly (no table in H
         __device__ Pair pair(int i, int j) const {
             return Pair{philox_bump32(key, episode, i * m + j, scale[j], T, wmin, wmax, dense)};
         }
-        // pairs (i, j) and (i, j + 1): one Philox call when they share one (even pair index)
-        __device__ void pair2(int i, int j, Pair &p0, Pair &p1) const {
-#if ASG_BUMP_PAIR2
+        // pairs (i, j) .. (i, j + 3): one Philox call when they share one (pair index % 4 == 0)
+        __device__ void pair4(int i, int j, Pair (&P)[4]) const {
             const int p = i * m + j;
-            if ((p & 1) == 0) {
-                philox_bump32x2(key, episode, p, scale[j], scale[j + 1], bump_shape(T, wmin, wmax), dense, p0.b, p1.b);
+            if ((p & 3) == 0) {
+                const float sc[4] = {scale[j], scale[j + 1], scale[j + 2], scale[j + 3]};
+                Bump32 b[4];
+                philox_bump32x4(key, episode, p, sc, bump_shape(T, wmin, wmax), dense, b);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) P[q].b = b[q];
                 return;
             }
-#endif
-            p0 = pair(i, j);
-            p1 = pair(i, j + 1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[q] = pair(i, j + q);
         }
     };
     // fills scale[0..m) cooperatively (caller syncs)
@@ -82,9 +84,9 @@ struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
             __device__ double at64(int t) const { return p[t * tstride]; }
         };
         __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, nm}; }
-        __device__ void pair2(int i, int j, Pair &p0, Pair &p1) const {
-            p0 = pair(i, j);
-            p1 = pair(i, j + 1);
+        __device__ void pair4(int i, int j, Pair (&P)[4]) const {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) P[q] = pair(i, j + q);
         }
     };
     __device__ void fill_scale(int64_t, float *) const {}
@@ -113,9 +115,8 @@ __device__ void write_pre_row(const EnvB &src, const asg_batch_view &bv, int64_t
         typename EnvB::Pair P[VEC];
 #pragma unroll
         for (int q = 0; q < VEC; ++q) oh[q] = (a == j0 + q) ? 1.0f : 0.0f;
-        if constexpr (VEC % 2 == 0) {
-#pragma unroll
-            for (int q = 0; q < VEC; q += 2) src.pair2(i, j0 + q, P[q], P[q + 1]);
+        if constexpr (VEC == 4) {
+            src.pair4(i, j0, P);
         } else {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) P[q] = src.pair(i, j0 + q);

@@ -189,7 +189,8 @@ constexpr int kH2SxInit = 11;                   // fc1 input scale of the first 
 // ASG_ROLLOUT_XSKIP bit 1: no batch row stores in the rollout tiles; bit 2: no one-hot W1
 // column gather (zeros); bit 4: fc1 slices that live in L2 read LDS slot 0 instead; bit 8:
 // h_t not loaded (constants); bit 16: h' not stored; bit 32: the tile's row stores go to a
-// small region that stays in L2 (env e & 7, batch row 1): same instructions, no HBM writes
+// small region that stays in L2 (env e & 7, batch row 1): same instructions, no HBM writes;
+// bit 64: the tiles' bump parameters from a cheap hash instead of Philox (VALU)
 #if defined(ASG_ROLLOUT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
 #error "ASG_ROLLOUT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
 #endif
@@ -983,9 +984,10 @@ struct RolloutArgs {
 
 __host__ __device__ inline int rollout_mp(int m) { return (m + 31) / 32 * 32; }
 __host__ __device__ inline int rollout_np(int n) { return (n + 31) / 32 * 32; }
-// per wave: task-scale bits [4] u64 | collision counts [mp] int | selected / previous tasks [np] u16 each
+// per wave: task-scale bits [4] u64 | the env's return f64 | collision counts [mp] int |
+// selected / previous tasks [np] u16 each
 __host__ __device__ inline int rollout_scratch_bytes(int n, int m) {
-    return (32 + 4 * rollout_mp(m) + 4 * rollout_np(n) + 15) / 16 * 16;
+    return (40 + 4 * rollout_mp(m) + 4 * rollout_np(n) + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ void wave_lds_fence() {
@@ -1022,32 +1024,35 @@ __device__ __forceinline__ float task_scale(const uint64_t *s_scl, int j) {
     return ((s_scl[j >> 6] >> (j & 63)) & 1ull) ? 10.0f : 1.0f;
 }
 
+// the launch's first transition without a selection before it: its tasks come from the
+// batch's actions row (read in the env prologue, so the transitions themselves issue no
+// global load -- a wait for one would drain the previous tile's stores every step)
+__device__ __forceinline__ void rollout_actions_from_batch(const RolloutArgs &ra, int64_t e, int ts, uint16_t *s_act) {
+    const int lane = threadIdx.x & 63;
+    const int n = ra.n, m = ra.m;
+    int err = 0;
+    for (int i = lane; i < n; i += 64) {
+        const int64_t a64 = ra.act[((int64_t)ts * ra.E + e) * n + i];
+        int a = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
+        if (a < 0) err = ASG_E_ACTION_RANGE;
+        s_act[i] = (uint16_t)(a < 0 ? 0 : a);
+    }
+    err = wave_or_i32(err);
+    if (lane == 0 && err) atomicCAS(ra.env_err, 0, err);
+}
+
 // one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
 // terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
-// launch) or, for the launch's first transition without a selection before it, from the
-// batch's actions row
-__device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_t e, int k, int ts, bool from_batch,
-                                                   const EnvKey &key, const uint64_t *s_scl, int *s_cnt,
-                                                   uint16_t *s_act, uint16_t *s_prev, double &ret) {
+// launch, or read from the batch by the env prologue)
+__device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_t e, int k, int ts, const EnvKey &key,
+                                                   const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
+                                                   uint16_t *s_prev, double *s_ret) {
     asm volatile("" : "+s"(e), "+s"(ts));
     const int lane = threadIdx.x & 63;
     const int n = ra.n, m = ra.m, mp = rollout_mp(m);
     for (int j = lane; j < mp; j += 64) s_cnt[j] = 0;
     wave_lds_fence();
-    int err = 0;
-    for (int i = lane; i < n; i += 64) {
-        int a;
-        if (from_batch) {
-            const int64_t a64 = ra.act[((int64_t)ts * ra.E + e) * n + i];
-            a = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
-            if (a < 0) err = ASG_E_ACTION_RANGE;
-            a = a < 0 ? 0 : a;
-            s_act[i] = (uint16_t)a;
-        } else {
-            a = s_act[i];
-        }
-        atomicAdd(&s_cnt[a], 1);
-    }
+    for (int i = lane; i < n; i += 64) atomicAdd(&s_cnt[s_act[i]], 1);
     wave_lds_fence();
     const BumpShape bsh = bump_shape(ra.T, ra.wmin, ra.wmax);
     double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
@@ -1072,14 +1077,12 @@ __device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_
         for (int l2 = 0; l2 < cnt; ++l2)
             sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
     }
-    err = wave_or_i32(err);
     if (lane == 0) {
-        ret += sum;
+        *s_ret += sum;  // the return lives in LDS: a register copy spilled, its reload drained the stores
         bool term = k + 1 >= ra.T;  // terminated = done != info.get("T", False)
         if (ra.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
         if (ra.term) ra.term[(int64_t)ts * ra.E + e] = term;
         if (ra.filled) ra.filled[(int64_t)(ts + 1) * ra.E + e] = 1;
-        if (err) atomicCAS(ra.env_err, 0, err);
     }
     wave_lds_fence();
 }
@@ -1254,15 +1257,19 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                     if (!live) {
 #pragma unroll
                         for (int v = 0; v < 4; ++v) bp[c][v][nt] = Bump32{0.f, 0.f, 0.f};
-                    } else if (!GEN) {
+                    } else if (ASG_ROLLOUT_XSKIP & 64) {
 #pragma unroll
-                        for (int v = 0; v < 4; v += 2) {  // pairs (j, j + 1) share one Philox call (m even)
-                            const int j = jw + v;
-                            const float s0v = ((sbits >> (j & 63)) & 1ull) ? 10.0f : 1.0f;
-                            const float s1v = ((sbits >> ((j + 1) & 63)) & 1ull) ? 10.0f : 1.0f;
-                            philox_bump32x2(key, ra.episode, ia[nt] * m + j, s0v, s1v, bsh, ra.dense != 0,
-                                            bp[c][v][nt], bp[c][v + 1][nt]);
-                        }
+                        for (int v = 0; v < 4; ++v)
+                            bp[c][v][nt] = Bump32{1.0f, (float)((jw + v + ia[nt]) & 15), 0.25f};
+                    } else if (!GEN) {
+                        // the lane's 4 pairs (j .. j + 3) are one Philox call (m % 4 == 0)
+                        float sv[4];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) sv[v] = ((sbits >> ((jw + v) & 63)) & 1ull) ? 10.0f : 1.0f;
+                        Bump32 b4[4];
+                        philox_bump32x4(key, ra.episode, ia[nt] * m + jw, sv, bsh, ra.dense != 0, b4);
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) bp[c][v][nt] = b4[v];
                     } else {
 #pragma unroll
                         for (int v = 0; v < 4; ++v) {
@@ -1278,16 +1285,22 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
             }
             for (int l = 1; l <= L; ++l) {
                 const int t = kk + l - 1;
+                // the 2 x NT x 4 bump values, straight-line (rows past T are zeros: a
+                // multiply, not a branch per value -- the evaluations then overlap)
+                const float live_t = t < T ? 1.0f : 0.0f;
                 float4 xv[2][NT];
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt) {
-                        float vv[4];
+                    for (int nt = 0; nt < NT; ++nt)
+                        xv[c][nt] = make_float4(bump32_at(bp[c][0][nt], t) * live_t, bump32_at(bp[c][1][nt], t) * live_t,
+                                                bump32_at(bp[c][2][nt], t) * live_t, bump32_at(bp[c][3][nt], t) * live_t);
+                if (st_now) {
 #pragma unroll
-                        for (int v = 0; v < 4; ++v) vv[v] = (t < T) ? bump32_at(bp[c][v][nt], t) : 0.0f;
-                        xv[c][nt] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-                        if (st_now) {
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            const float vv[4] = {xv[c][nt].x, xv[c][nt].y, xv[c][nt].z, xv[c][nt].w};
                             const int j0 = 32 * u + 16 * c + 4 * q;
                             if (!GEN) {
                                 st_f4(obs_r + rows[nt] * K + m * l + j0, vv[0], vv[1], vv[2], vv[3]);
@@ -1301,7 +1314,7 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
                                     }
                             }
                         }
-                    }
+                }
                 if (AGENT) {
                     // the agent kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
                     const int sl = l * Ub + u;
@@ -1403,7 +1416,8 @@ rollout_kernel(RolloutArgs ra) {
     const int n = ra.n, m = ra.m, mp = rollout_mp(m), np = rollout_np(n);
     char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
     uint64_t *s_scl = reinterpret_cast<uint64_t *>(scr);
-    int *s_cnt = reinterpret_cast<int *>(scr + 32);
+    double *s_ret = reinterpret_cast<double *>(scr + 32);
+    int *s_cnt = reinterpret_cast<int *>(scr + 40);
     uint16_t *s_act = reinterpret_cast<uint16_t *>(s_cnt + mp);
     uint16_t *s_prev = s_act + np;
     const int ntile = np / (16 * kH2NT);
@@ -1456,7 +1470,8 @@ rollout_kernel(RolloutArgs ra) {
                 s_act[i] = 0;
             }
         }
-        double ret = (lane == 0 && !ra.reset) ? ra.returns[e] : 0.0;
+        if (lane == 0) *s_ret = ra.reset ? 0.0 : ra.returns[e];
+        if (!ra.select_first) rollout_actions_from_batch(ra, e, ra.ts0, s_act);
         wave_lds_fence();
         // iteration 0 with select_first: the selection on the reset row (no transition);
         // every other iteration: transition k, then the agent tiles of row k + 1 (or, past the
@@ -1475,7 +1490,7 @@ rollout_kernel(RolloutArgs ra) {
             const int ts = ra.ts0 + (k - ra.k0);
             const bool first_sel = it < sf;
             if (!first_sel)
-                rollout_transition(ra, e, k, ts, k == ra.k0 && !sf, key, s_scl, s_cnt, s_act, s_prev, ret);
+                rollout_transition(ra, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
             const int kk = k + 1;
             if (has_agent(it)) {
                 const bool next_agent = has_agent(it + 1);
@@ -1500,7 +1515,7 @@ rollout_kernel(RolloutArgs ra) {
             wave_lds_fence();
         }
         for (int i = lane; i < n; i += 64) ra.prev[e * n + i] = s_prev[i];
-        if (lane == 0) ra.returns[e] = ret;
+        if (lane == 0) ra.returns[e] = *s_ret;
         wave_lds_fence();  // the next env reuses the scratch
     }
 }

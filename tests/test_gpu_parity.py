@@ -560,10 +560,10 @@ def test_epsilon_greedy_writes_batch_row_in_place():
 
 
 def test_philox_bump_parameter_distribution():
-    """The Philox bump draws (one Philox call per two pairs, asg_device.h:philox_bump32x2)
+    """The Philox bump draws (one Philox call per four pairs, asg_device.h:philox_bump32x4)
     follow generate_benefits_over_time's distribution (mock_constellation_env.py:281-293):
-    active with probability 1/4, center ~ U(0, T), width ~ U(wmin, wmax) -- and the two
-    pairs of one call are independent."""
+    active with probability 1/4, center ~ U(0, T), width ~ U(wmin, wmax) -- and pairs of one
+    call are independent."""
     n = m = 64
     T, E = 20, 64
     env = AssignEnvBatch(n, m, T, 3, 0.5, seed=11, num_envs=E, device=DEV)

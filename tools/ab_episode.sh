@@ -13,7 +13,7 @@ for lib in default "$@"; do
       -k "bit_identical and (64-64-6 or 20-25 or 256-256) or chunks" > "$OUT/tests_$(basename $lib).log" 2>&1 \
       || { echo "tests failed for $lib"; tail -5 "$OUT/tests_$(basename $lib).log"; exit 1; }
 done
-for rep in 1 2 3; do
+for rep in $(seq ${AB_REPS:-3}); do
   for lib in default "$@"; do
     if [ "$lib" = default ]; then unset ASG_LIB_PATH; else export ASG_LIB_PATH=$PWD/$lib; fi
     for cfg in "${AB_CONFIGS:-2}"; do
