@@ -242,6 +242,12 @@ __device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4
 // and the rollout kernel): xB = relu(fc1) fragments, hB = h_in rows (GRU).
 // ALLAV: every task is available (the rollout wrote avail = 1 itself).  act_lds (rollout):
 // also receives each row's selected task (index lrow0 + row within the tile).
+// 1: the GRU's (1 - z) n + z h takes h back from its split-f16 planes (h_hi + h_lo, exact to
+// 2^-22) instead of keeping the f32 h live through the gate products
+#ifndef ASG_H2_H_FROM_PLANES
+#define ASG_H2_H_FROM_PLANES 0
+#endif
+
 struct NoTailHook {
     __device__ void operator()() const {}
 };
@@ -411,11 +417,15 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
                     const float ng =
                         2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((gni[nt][v] + rg * gnh[nt][v]) * c2[nt])) -
                         1.0f;
+#if ASG_H2_H_FROM_PLANES
                     // h from its planes (h_hi + h_lo = h 2^sh to 2^-22 relative)
                     const int j = 4 * (hb & 1) + v;
                     const uint32_t dh = hP[hb >> 1][nt][0][j >> 1], dl = hP[hb >> 1][nt][1][j >> 1];
                     const f16x2v ph = __builtin_bit_cast(f16x2v, dh), pl = __builtin_bit_cast(f16x2v, dl);
                     const float hv = ((float)ph[j & 1] + (float)pl[j & 1]) * hun[nt];
+#else
+                    const float hv = comp(hB[hb][nt], v);  // the exact h (the planes carry it to 2^-22)
+#endif
                     hp[hb][nt][v] = ng + zg * (hv - ng);
                 }
 #pragma unroll
