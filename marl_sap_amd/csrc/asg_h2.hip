@@ -35,6 +35,8 @@
 // one-hot prefix: a tile whose block 0 is verified one-hot (or zero) adds W1[:, a] (one
 // gathered column per row) instead of running those slices' MFMAs.  Any other input is one
 // block (P = K).
+#include <type_traits>
+
 #include "asg_agent_common.h"
 
 #pragma clang fp contract(fast)
@@ -1058,7 +1060,11 @@ __device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_
                                                    const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
                                                    uint16_t *s_prev, double *s_ret) {
     asm volatile("" : "+s"(e), "+s"(ts));
-    const int lane = threadIdx.x & 63;
+    // the lane index is recomputed here, not kept across the step loop (spilled, its reload
+    // waited behind the previous tile's stores every step)
+    int lane_ = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane_));
+    const int lane = lane_;
     const int n = ra.n, m = ra.m, mp = rollout_mp(m);
     for (int j = lane; j < mp; j += 64) s_cnt[j] = 0;
     wave_lds_fence();
@@ -1066,27 +1072,35 @@ __device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_
     wave_lds_fence();
     const BumpShape bsh = bump_shape(ra.T, ra.wmin, ra.wmax);
     double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
-    for (int i0 = 0; i0 < n; i0 += 64) {
-        const int i = i0 + lane;
-        double rr = 0.0;
-        if (i < n) {
-            const int j = s_act[i], p = s_prev[i];
-            const Bump32 b = philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
-            const double beta = bump64_at(b, k);
-            const double tt = ra.T_trans ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
-            const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
-            const double bh = beta - ra.lambda_ * pen;
-            rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
-            if (ra.rew) ra.rew[((int64_t)ts * ra.E + e) * n + i] = (float)rr;
-            s_prev[i] = (uint16_t)j;
-            if (ra.prevb)
-                ra.prevb[((int64_t)(ts + 1) * ra.E + e) * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+    // two copies of the loop, with and without an injected T_trans: merged, the join after
+    // the table load made every transition wait for the previous tile's stores (vmcnt)
+    auto rewards = [&](auto with_table) {
+        constexpr bool TT = decltype(with_table)::value;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            double rr = 0.0;
+            if (i < n) {
+                const int j = s_act[i], p = s_prev[i];
+                const Bump32 b = philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
+                const double beta = bump64_at(b, k);
+                const double tt = TT ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+                const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+                const double bh = beta - ra.lambda_ * pen;
+                rr = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+                if (ra.rew) ra.rew[((int64_t)ts * ra.E + e) * n + i] = (float)rr;
+                s_prev[i] = (uint16_t)j;
+                if (ra.prevb)
+                    ra.prevb[((int64_t)(ts + 1) * ra.E + e) * n + i] =
+                        (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+            }
+            const int lo = __double2loint(rr), hi = __double2hiint(rr);
+            const int cnt = n - i0 < 64 ? n - i0 : 64;
+            for (int l2 = 0; l2 < cnt; ++l2)
+                sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
         }
-        const int lo = __double2loint(rr), hi = __double2hiint(rr);
-        const int cnt = n - i0 < 64 ? n - i0 : 64;
-        for (int l2 = 0; l2 < cnt; ++l2)
-            sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
-    }
+    };
+    if (ra.T_trans) rewards(std::true_type{});
+    else rewards(std::false_type{});
     if (lane == 0) {
         *s_ret += sum;  // the return lives in LDS: a register copy spilled, its reload drained the stores
         bool term = k + 1 >= ra.T;  // terminated = done != info.get("T", False)
@@ -1295,16 +1309,22 @@ __device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, i
             }
             for (int l = 1; l <= L; ++l) {
                 const int t = kk + l - 1;
-                // the 2 x NT x 4 bump values, straight-line (rows past T are zeros: a
-                // multiply, not a branch per value -- the evaluations then overlap)
-                const float live_t = t < T ? 1.0f : 0.0f;
+                // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
+                // past T are zeros)
                 float4 xv[2][NT];
+                if (t < T) {
 #pragma unroll
-                for (int c = 0; c < 2; ++c)
+                    for (int c = 0; c < 2; ++c)
 #pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        xv[c][nt] = make_float4(bump32_at(bp[c][0][nt], t) * live_t, bump32_at(bp[c][1][nt], t) * live_t,
-                                                bump32_at(bp[c][2][nt], t) * live_t, bump32_at(bp[c][3][nt], t) * live_t);
+                        for (int nt = 0; nt < NT; ++nt)
+                            xv[c][nt] = make_float4(bump32_at(bp[c][0][nt], t), bump32_at(bp[c][1][nt], t),
+                                                    bump32_at(bp[c][2][nt], t), bump32_at(bp[c][3][nt], t));
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) xv[c][nt] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
                 if (st_now) {
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
