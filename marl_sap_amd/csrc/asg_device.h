@@ -111,11 +111,12 @@ __device__ __forceinline__ float philox_task_scale(EnvKey key, uint32_t episode,
 struct BumpShape {
     int T, q;
     float wmin, wspan;
+    float cscale;  // T * 2^-16: the center directly from the 16-bit draw when q >= 16 (T < 256)
 };
 __host__ __device__ inline BumpShape bump_shape(int T, float wmin, float wmax) {
     int bits = 0;
     for (unsigned t = (unsigned)(T > 0 ? T : 1); t; t >>= 1) ++bits;
-    return BumpShape{T, 24 - bits, wmin, wmax - wmin};
+    return BumpShape{T, 24 - bits, wmin, wmax - wmin, (float)T * 0x1p-16f};
 }
 
 // Pair 4k + s takes word s of Philox call k (counter {k, 0, kCtrPair4, episode}):
@@ -127,9 +128,14 @@ __host__ __device__ inline BumpShape bump_shape(int T, float wmin, float wmax) {
 __device__ __forceinline__ Bump32 bump_from_word(uint32_t w, float scale, const BumpShape &bs, bool dense) {
     Bump32 b;
     b.scale = (dense || (w & 3u) == 3u) ? scale : 0.0f;
-    // the grid index (w >> 16) * T * 2^q / 2^16 is < T * 2^q <= 2^24: the 32-bit convert is exact
-    b.center = __builtin_ldexpf(
-        (float)(uint32_t)((((uint64_t)(w >> 16) * (uint64_t)(uint32_t)bs.T) << bs.q) >> 16), -bs.q);
+    // the grid index (w >> 16) * T * 2^q / 2^16 is < T * 2^q <= 2^24: the 32-bit convert is exact;
+    // for q >= 16 no bit is dropped and the center is (w >> 16) * T * 2^-16 exactly (a
+    // product < 2^24 of an integer and a power of two): one convert and one multiply
+    if (bs.q >= 16)
+        b.center = (float)(w >> 16) * bs.cscale;
+    else
+        b.center = __builtin_ldexpf(
+            (float)(uint32_t)((((uint64_t)(w >> 16) * (uint64_t)(uint32_t)bs.T) << bs.q) >> 16), -bs.q);
     const float spread = bs.wmin + bs.wspan * ((float)((w >> 2) & 0x3fffu) * 0x1p-14f);
     // log2(e) / (2 sigma_2), sigma_2 = sqrt(spread^2 / -8 / ln 0.05), is for spread > 0
     // log2(e) sqrt(-2 ln 0.05) / spread: one v_rcp_f32 (<= 1 ulp) and a multiply (within
