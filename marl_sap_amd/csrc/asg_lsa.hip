@@ -107,11 +107,25 @@ static size_t lsa_scratch_bytes(int nr0) { return sizeof(int) * nr0 + 64; }
 #ifndef ASG_LSA_REG_WAVES
 #define ASG_LSA_REG_WAVES 5
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) lsa_reg_kernel(const float *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
+// Problems (waves) per workgroup of the register-resident kernels.  One-wave workgroups cap
+// a CU at its 16 resident workgroups = 4 waves per SIMD whatever the register budget allows;
+// four waves per workgroup let the 88-VGPR solver run at its 5 waves per SIMD.
+#ifndef ASG_LSA_WPB
+#define ASG_LSA_WPB 4
+#endif
+constexpr int kLsaWpb = ASG_LSA_WPB;
+static dim3 lsa_reg_grid(int64_t B) { return dim3((unsigned)((B + kLsaWpb - 1) / kLsaWpb)); }
+// this wave's problem index (wave-uniform); >= B for the idle waves of the last workgroup
+__device__ __forceinline__ int64_t lsa_reg_problem() {
+    return (int64_t)blockIdx.x * kLsaWpb + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+__global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) lsa_reg_kernel(const float *C, int64_t s0, int64_t s1, int64_t s2, int nr0,
                                                      int nc0, int maximize, int64_t *row_out, int64_t *col_out,
-                                                     int32_t *status_out) {
-    __shared__ int mark[64];
-    const int64_t b = blockIdx.x;
+                                                     int32_t *status_out, int64_t B) {
+    __shared__ int s_mark[kLsaWpb][64];
+    const int64_t b = lsa_reg_problem();
+    if (b >= B) return;
+    int *mark = s_mark[threadIdx.x >> 6];
     const bool tr = nc0 < nr0;
     const int nr = tr ? nc0 : nr0, nc = tr ? nr0 : nc0;
     const int k = nr;
@@ -124,7 +138,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA
         status = lsa_solve_reg64(rc, nr, nc, c4r);
         if (status == ASG_OK) lsa_emit_wave(c4r, nr0, nc0, mark, ro, co, nullptr);
     }
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
     if (status != ASG_OK) {
         for (int r = lane; r < k; r += kWave) {
             if (ro) ro[r] = -1;
@@ -141,8 +155,8 @@ static hipError_t launch_lsa_t(const IT *C, const int64_t st[3], int64_t B, int 
     const size_t cost_bytes = ((sizeof(CT) * (size_t)nr * nc + 15) / 16) * 16;
     const size_t scratch = lsa_scratch_bytes(nr0);
     if (std::is_same<IT, float>::value && nc <= 64) {
-        hipLaunchKernelGGL(lsa_reg_kernel, dim3(B), dim3(64), 0, s, reinterpret_cast<const float *>(C), st[0], st[1],
-                           st[2], nr0, nc0, maximize, row_out, col_out, status_out);
+        hipLaunchKernelGGL(lsa_reg_kernel, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, reinterpret_cast<const float *>(C),
+                           st[0], st[1], st[2], nr0, nc0, maximize, row_out, col_out, status_out, B);
     } else if (cost_bytes <= kLdsCostBudget) {
 #define L_(CPL)                                                                                                   \
     hipLaunchKernelGGL((lsa_batched_kernel<CPL, IT, CT, true>), dim3(B), dim3(64), cost_bytes + scratch, s, C, \
@@ -176,12 +190,13 @@ hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3]
 // ones * avg * eps * 2, torch.normal, +=, scipy.
 // ------------------------------------------------------------------------------------
 template <bool kCount>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
+__global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
                                                         int64_t env_base, float *col_out, int32_t *status_out,
-                                                        int32_t *steps_out) {
-    const int64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
+                                                        int32_t *steps_out, int64_t B) {
+    const int64_t b = lsa_reg_problem();
+    if (b >= B) return;
+    const int lane = threadIdx.x & (kWave - 1);
     const float *col = q + b * q0 + (int64_t)lane * q2;
     f32x32 lo, hi;
     float asum = 0.0f;
@@ -248,11 +263,11 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
                              int32_t *steps_out, hipStream_t s) {
     if (steps_out)
-        hipLaunchKernelGGL(sap_select_kernel<true>, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon,
-                           seed, counter, env_base, col_out, status_out, steps_out);
+        hipLaunchKernelGGL(sap_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n,
+                           m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
     else
-        hipLaunchKernelGGL(sap_select_kernel<false>, dim3(B), dim3(64), 0, s, q, qs[0], qs[1], qs[2], n, m, epsilon,
-                           seed, counter, env_base, col_out, status_out, steps_out);
+        hipLaunchKernelGGL(sap_select_kernel<false>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n,
+                           m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
     return hipGetLastError();
 }
 
@@ -365,12 +380,13 @@ struct HaaRegCost {
     __device__ double col(int i) const { return (*this)(i, (int)(threadIdx.x & 63)); }
 };
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
+__global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) haa_reg_kernel(const float *beta, int64_t b0, int64_t b1, int64_t b2,
                                                      const int64_t *prev, int64_t p0, int64_t p1, int n, int m,
                                                      const double *T_trans, double lambda_, float *col_out,
-                                                     int32_t *status_out) {
-    const int64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
+                                                     int32_t *status_out, int64_t B) {
+    const int64_t b = lsa_reg_problem();
+    if (b >= B) return;
+    const int lane = threadIdx.x & (kWave - 1);
     HaaRegCost acc;
     // beta_hat is not negated here (the accessor does it): stage with maximize = false,
     // which also rejects NaN; +inf beta (-inf cost) is rejected below
@@ -401,8 +417,8 @@ hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64
     const size_t cost = ((sizeof(float) * (size_t)n * m + 15) / 16) * 16;
     const size_t rest = ((sizeof(int) * n + 15) / 16) * 16 + 64;
     if (m <= 64) {
-        hipLaunchKernelGGL(haa_reg_kernel, dim3(B), dim3(64), 0, s, beta, bs[0], bs[1], bs[2], prev, ps[0], ps[1], n,
-                           m, T_trans, lambda_, col_out, status_out);
+        hipLaunchKernelGGL(haa_reg_kernel, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, beta, bs[0], bs[1], bs[2], prev,
+                           ps[0], ps[1], n, m, T_trans, lambda_, col_out, status_out, B);
     } else if (cost <= kLdsCostBudget) {
 #define L_(CPL)                                                                                                 \
     hipLaunchKernelGGL((haa_select_kernel<CPL, true>), dim3(B), dim3(64), cost + rest, s, beta, bs[0], bs[1], bs[2], \
