@@ -994,6 +994,20 @@ struct RolloutArgs {
     int64_t scratch_off;  // per-wave LDS scratch (u32x4v units)
 };
 
+// The launch arguments as the tiles and transitions read them: a kernarg-segment pointer made
+// opaque per call, so each call re-reads what it uses with scalar loads instead of the kernel
+// keeping ~40 uniform values live from its entry (they overflowed the SGPR file and were spilled
+// to VGPR lanes, ~500 v_readlane reloads in the tile body).  ASG_ROLLOUT_KARG=0: the by-value
+// argument throughout (A/B).
+#ifndef ASG_ROLLOUT_KARG
+#define ASG_ROLLOUT_KARG 1
+#endif
+typedef __attribute__((address_space(4))) const RolloutArgs KRolloutArgs;
+__device__ __forceinline__ KRolloutArgs &rollout_args(KRolloutArgs *p) {
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 __host__ __device__ inline int rollout_mp(int m) { return (m + 31) / 32 * 32; }
 __host__ __device__ inline int rollout_np(int n) { return (n + 31) / 32 * 32; }
 // per wave: task-scale bits [4] u64 | the env's return f64 | collision counts [mp] int |
@@ -1007,7 +1021,8 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ H2Args rollout_h2args(const RolloutArgs &ra) {
+template <class RA>
+__device__ __forceinline__ H2Args rollout_h2args(RA &ra) {
     H2Args a{};
     a.R = ra.E * ra.n;
     a.g.K = ra.m * (ra.L + 1);
@@ -1039,7 +1054,8 @@ __device__ __forceinline__ float task_scale(const uint64_t *s_scl, int j) {
 // the launch's first transition without a selection before it: its tasks come from the
 // batch's actions row (read in the env prologue, so the transitions themselves issue no
 // global load -- a wait for one would drain the previous tile's stores every step)
-__device__ __forceinline__ void rollout_actions_from_batch(const RolloutArgs &ra, int64_t e, int ts, uint16_t *s_act) {
+template <class RA>
+__device__ __forceinline__ void rollout_actions_from_batch(RA &ra, int64_t e, int ts, uint16_t *s_act) {
     const int lane = threadIdx.x & 63;
     const int n = ra.n, m = ra.m;
     int err = 0;
@@ -1056,7 +1072,8 @@ __device__ __forceinline__ void rollout_actions_from_batch(const RolloutArgs &ra
 // one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
 // terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
 // launch, or read from the batch by the env prologue)
-__device__ __forceinline__ void rollout_transition(const RolloutArgs &ra, int64_t e, int k, int ts, const EnvKey &key,
+template <class RA>
+__device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int ts, const EnvKey &key,
                                                    const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
                                                    uint16_t *s_prev, double *s_ret) {
     asm volatile("" : "+s"(e), "+s"(ts));
@@ -1134,8 +1151,8 @@ struct HNext {
     int mode;
 };
 
-template <bool RNN, bool W2L, bool GEN, bool AGENT>
-__device__ __forceinline__ void rollout_tile(const RolloutArgs &ra, int64_t e, int sub, int kk, int tsr, bool stores,
+template <bool RNN, bool W2L, bool GEN, bool AGENT, class RA>
+__device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
                                              uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
                                              f32x4 (&hN)[4][kH2NT], bool hpf, HNext nx) {
@@ -1506,42 +1523,50 @@ rollout_kernel(RolloutArgs ra) {
         // iteration 0 with select_first: the selection on the reset row (no transition);
         // every other iteration: transition k, then the agent tiles of row k + 1 (or, past the
         // launch's last selection, the row alone) -- one call site per tile kind
+#if ASG_ROLLOUT_KARG
+        KRolloutArgs *const kra = (KRolloutArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#define RA_ rollout_args(kra)
+#else
+#define RA_ ra
+#endif
         const int sf = ra.select_first ? 1 : 0;
         const int nit = ra.k1 - ra.k0 + sf;
         int pass = 0;
         f32x4 hN[4][kH2NT];  // the next agent tile's h_t rows (prefetched by the tile before it)
         bool hpf = false;
-        auto has_agent = [&](int it) {
-            const int kk = ra.k0 + it - sf + 1;
-            return it < nit && kk < ra.T && (kk < ra.k1 || ra.select_last);
+        auto has_agent = [&](auto &rr, int it) {
+            const int kk = rr.k0 + it - sf + 1;
+            return it < nit && kk < rr.T && (kk < rr.k1 || rr.select_last);
         };
         for (int it = 0; it < nit; ++it) {
-            const int k = ra.k0 + it - sf;  // k0 - 1 on the select_first iteration
-            const int ts = ra.ts0 + (k - ra.k0);
+            auto &ri = RA_;  // this iteration's reads of the launch arguments
+            const int k = ri.k0 + it - sf;  // k0 - 1 on the select_first iteration
+            const int ts = ri.ts0 + (k - ri.k0);
             const bool first_sel = it < sf;
             if (!first_sel)
-                rollout_transition(ra, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
+                rollout_transition(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
             const int kk = k + 1;
-            if (has_agent(it)) {
-                const bool next_agent = has_agent(it + 1);
+            if (has_agent(ri, it)) {
+                const bool next_agent = has_agent(ri, it + 1);
                 for (int sub = 0; sub < ntile; ++sub) {
                     // the next agent tile: this pass's next tile (same h_t source), else tile 0
                     // of the next pass (h_t = the h' this pass writes)
                     HNext nx{nullptr, kHid, 0, 0};
-                    if (sub + 1 < ntile) nx = HNext{pass == 0 ? ra.Hin : ra.Hout, pass == 0 ? ra.hs : kHid,
+                    if (sub + 1 < ntile) nx = HNext{pass == 0 ? ri.Hin : ri.Hout, pass == 0 ? ri.hs : kHid,
                                                     (int64_t)(16 * kH2NT) * (sub + 1), 1};
-                    else if (next_agent) nx = HNext{ra.Hout, kHid, 0, 1};
+                    else if (next_agent) nx = HNext{ri.Hout, kHid, 0, 1};
                     // the reset row (select_first) is stored here when the reset runs in this launch
-                    rollout_tile<RNN, W2L, GEN, true>(ra, e, sub, kk, ts + 1, !first_sel || ra.reset, !first_sel, pass,
+                    rollout_tile<RNN, W2L, GEN, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
                                                       key, s_scl, s_act, s_h2, sw, hN, hpf, nx);
                     hpf = nx.mode != 0;
                 }
                 ++pass;
             } else {
                 for (int sub = 0; sub < ntile; ++sub)
-                    rollout_tile<RNN, W2L, GEN, false>(ra, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
+                    rollout_tile<RNN, W2L, GEN, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
                                                        sw, hN, false, HNext{nullptr, kHid, 0, 0});
             }
+#undef RA_
             wave_lds_fence();
         }
         for (int i = lane; i < n; i += 64) ra.prev[e * n + i] = s_prev[i];
