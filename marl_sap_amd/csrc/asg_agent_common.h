@@ -22,10 +22,10 @@ __device__ __forceinline__ float comp(const float4 &v, int e) {
 // and availability bits of the row's tasks (task 16 c + 4 q + v is bit 4 c + v of lane q's
 // mask; GEN: a second word for tasks 256-511).  Writes sel.out and returns the action
 // (meaningful on lanes q < NT whose row is ok; row nt = q & 1).
-template <bool GEN, int NT>
+template <bool GEN, int NT, class SA>
 __device__ __forceinline__ int select_finish(float (&best)[NT], int (&bj)[NT], const uint64_t (&amask)[NT][2],
                                              const int64_t (&rows)[NT], const bool (&ok)[NT],
-                                             const int64_t (&oidx)[NT], int nct, const SelectArgs &sel, int q) {
+                                             const int64_t (&oidx)[NT], int nct, SA &sel, int q) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         auto red = [&](auto swp) {

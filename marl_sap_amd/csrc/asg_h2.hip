@@ -200,7 +200,8 @@ constexpr int kH2SxInit = 11;                   // fc1 input scale of the first 
 #define ASG_ROLLOUT_XSKIP 0
 #endif
 
-__device__ __forceinline__ int h2_s0(const H2Args &a) { return a.pre ? (a.g.Pp >> 5) : 0; }
+template <class A>
+__device__ __forceinline__ int h2_s0(A &a) { return a.pre ? (a.g.Pp >> 5) : 0; }
 
 template <bool RNN, bool W2L>
 __device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4]) {
@@ -256,8 +257,8 @@ struct NoTailHook {
 
 // after_rec: called once the recurrent layer has consumed hB and stored h' (the rollout
 // issues the next agent tile's h_t loads there)
-template <int NT, bool RNN, bool SEL, bool W2L, bool ALLAV, bool GEN, class Hook = NoTailHook>
-__device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
+template <int NT, bool RNN, bool SEL, bool W2L, bool ALLAV, bool GEN, class Hook = NoTailHook, class A>
+__device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[4], int64_t row0,
                                         const int64_t (&rows)[NT], const bool (&ok)[NT], const float4 (&hB)[4][NT],
                                         const f32x4 (&xB)[4][NT], uint16_t *act_lds = nullptr, int lrow0 = 0,
                                         const Hook &after_rec = Hook{}) {
@@ -272,7 +273,7 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
     const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));  // biases
     // availability words of fc2's first four output tiles: issued now, used after the
     // recurrent layer
-    const SelectArgs &sel = a.sel;
+    auto &sel = a.sel;
     const uint8_t *arow[NT];
     int64_t oidx[NT];
     bool av4 = false;
@@ -571,11 +572,11 @@ __device__ __forceinline__ void h2_tail(const H2Args &a, const u32x4v *Wl, const
 }
 
 // One wave, 32 agent rows of a flat [R][K] input: fc1 -> recurrent layer -> fc2 (+ selection).
-template <int NT, bool RNN, bool SEL, bool W2L, bool GEN>
-__device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, const u32x4v *Wl, const int (&sw)[4]) {
+template <int NT, bool RNN, bool SEL, bool W2L, bool GEN, class A>
+__device__ __forceinline__ void agent_rows_h2(int64_t row0, A &a, const u32x4v *Wl, const int (&sw)[4]) {
     const int lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
     if (row0 >= a.R) return;
-    const H2Geom &g = a.g;
+    auto &g = a.g;
     int64_t rows[NT];
     bool ok[NT];
 #pragma unroll
@@ -784,6 +785,10 @@ __device__ __forceinline__ void agent_rows_h2(int64_t row0, const H2Args &a, con
     h2_tail<NT, RNN, SEL, W2L, false, GEN>(a, Wl, sw, row0, rows, ok, hB, xB);
 }
 
+#ifndef ASG_H2_KARG
+#define ASG_H2_KARG 1
+#endif
+typedef __attribute__((address_space(4))) const H2Args KH2Args;
 // Persistent: one 512-thread workgroup per CU stages the LDS image, then its 8 waves walk
 // 256-row tiles.
 template <bool RNN, bool SEL, bool W2L, bool GEN>
@@ -797,7 +802,15 @@ rnn_agent_h2_kernel(H2Args a) {
     const int64_t ntiles = (a.R + kH2Waves * (16 * NT) - 1) / (kH2Waves * (16 * NT));
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = (tile * kH2Waves + (threadIdx.x >> 6)) * (16 * NT);
+#if ASG_H2_KARG
+        // each tile re-reads the launch arguments (scalar loads): kept live from the kernel
+        // entry they overflow the SGPR file (see rollout_args)
+        KH2Args *p = (KH2Args *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        agent_rows_h2<NT, RNN, SEL, W2L, GEN>(row0, *p, s_h2, sw);
+#else
         agent_rows_h2<NT, RNN, SEL, W2L, GEN>(row0, a, s_h2, sw);
+#endif
     }
 }
 
