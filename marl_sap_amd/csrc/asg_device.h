@@ -262,10 +262,11 @@ __device__ __forceinline__ int wave_or_i32(int v) {
 // step) -- 4 steps inside each 16-lane row, then row_bcast:15 / row_bcast:31 fold the rows
 // into lane 63.  s_nop 1 covers the VALU-write -> DPP-read hazard.  Call in wave-uniform
 // control flow.
-__device__ __forceinline__ float wave_min_f32_nonan(float x) {
+__device__ __forceinline__ float wave_min_f32_nonan(float x0) {
 #ifndef ASG_LSA_PERMLANE_MIN
+    float x;  // a separate result register: the input stays live without a copy
     asm("s_nop 1\n\t"
-        "v_min_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_min_f32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
         "s_nop 1\n\t"
         "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
         "s_nop 1\n\t"
@@ -276,9 +277,11 @@ __device__ __forceinline__ float wave_min_f32_nonan(float x) {
         "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
         "s_nop 1\n\t"
         "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc"
-        : "+v"(x));
+        : "=&v"(x)
+        : "v"(x0));
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 #else
+    const float x = x0;
     float y, t;
     asm("s_nop 1\n\t"
         "v_min_f32_dpp %0, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"

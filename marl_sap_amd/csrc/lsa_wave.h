@@ -270,6 +270,10 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
 // kCount: also count the augmenting-path steps (iterations of scipy's inner loop, the
 // figure ora_lsa_iterations reports) into *steps -- an instrumentation instance for the
 // LSA efficiency figure; the product instances compile it out.
+// a double from its two 32-bit halves as one register pair (no 64-bit OR)
+typedef uint32_t lsa_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) { return __builtin_bit_cast(double, lsa_u32x2{lo, hi}); }
+
 template <class Acc, bool kCount = false>
 __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1], int *steps = nullptr) {
 #ifdef ASG_LSA_GENERIC_REG
@@ -278,7 +282,12 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
     int nsteps = 0;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t colmask = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);  // lanes that hold a column
-    const float kInfF = __builtin_inff();
+#ifndef ASG_LSA_NAN_KEYS
+#define ASG_LSA_NAN_KEYS 1
+#endif
+    // keys of columns out of `remaining`: a quiet NaN is never equal to the minimum (and
+    // v_min_f32 skips it), so the candidate ballot needs no "& rem"
+    const float kOutF = ASG_LSA_NAN_KEYS ? __builtin_bit_cast(float, 0x7fc00000u) : __builtin_inff();
     double v = 0.0, u = 0.0;
     int r4c = -1, path = -1, c4r = -1;
     for (int cur = 0; cur < nr; ++cur) {
@@ -306,9 +315,9 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             const bool upd = remb && r < spc;
             spc = upd ? r : spc;
             path = upd ? i : path;
-            const float key = remb ? (float)spc : kInfF;
+            const float key = remb ? (float)spc : kOutF;
             const float kmin = wave_min_f32_nonan(key);
-            const uint64_t cm = __ballot(key == kmin) & rem;
+            const uint64_t cm = ASG_LSA_NAN_KEYS ? __ballot(key == kmin) : (__ballot(key == kmin) & rem);
             asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
             const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
             jsel = (int)__builtin_ctzll(cm);  // the first candidate: the selection when it is the only one
@@ -321,14 +330,14 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
                 // candidate (ncand 0) only if a cost turned NaN during the solve (e.g. a NaN
                 // T_trans entry under HAA): scipy's "invalid numeric entries" -- the step
                 // then ends the loop as infeasible and is reported as invalid below
-                double lowest0 = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+                double lowest0 = dbl_of(lowest_lo, lowest_hi);
                 uint64_t cand = cm;
                 if ((__ballot(spc != lowest0) & cm) != 0) {
                     const double lo = remb ? spc : __builtin_inf();
                     const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));
                     lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
                     lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
-                    lowest0 = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+                    lowest0 = dbl_of(lowest_lo, lowest_hi);
                     cand = __ballot(spc == lowest0) & rem;
                 }
                 // scipy's tie rule: unassigned 2^31 | pos (largest position), else 2^30 - pos
@@ -346,7 +355,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             pos = __builtin_amdgcn_inverse_ballot_w64(jbit) ? -1 : (pos == last ? psel : pos);
             rem &= ~jbit;
             --nrem;
-            minv = __builtin_bit_cast(double, (uint64_t)lowest_lo | ((uint64_t)lowest_hi << 32));
+            minv = dbl_of(lowest_lo, lowest_hi);
             i = __builtin_amdgcn_readlane(r4c, jsel);
             // continue while the column is assigned (owner != -1) and scipy's minVal is not
             // INFINITY (lowest is never NaN: a NaN key is no candidate and the exact minimum
