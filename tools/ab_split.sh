@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_agent.py tests/test_gpu_fused_rollout.py tests/test_gpu_runner.py > gpurun_out/ab_split_tests.log 2>&1 || { tail -5 gpurun_out/ab_split_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_agent.py tests/test_gpu_fused_rollout.py tests/test_gpu_runner.py ${AB_TESTS:-} > gpurun_out/ab_split_tests.log 2>&1 || { tail -5 gpurun_out/ab_split_tests.log; exit 1; }
 tail -1 gpurun_out/ab_split_tests.log
 for rep in 1 2 3; do
   for lib in default "$@"; do
