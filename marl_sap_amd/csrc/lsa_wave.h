@@ -351,9 +351,9 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             }
             // remaining[index] = remaining[--num_remaining]
             const int last = nrem - 1;
-            const uint64_t jbit = 1ull << jsel;
-            pos = __builtin_amdgcn_inverse_ballot_w64(jbit) ? -1 : (pos == last ? psel : pos);
-            rem &= ~jbit;
+            // (a removed column keeps a stale position: every read of pos is masked by rem)
+            pos = pos == last ? psel : pos;
+            asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(jsel) : "scc");  // rem &= ~(1 << jsel), one instruction
             --nrem;
             minv = dbl_of(lowest_lo, lowest_hi);
             i = __builtin_amdgcn_readlane(r4c, jsel);
