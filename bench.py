@@ -159,10 +159,21 @@ def agent_roofline(a, E, agent_ms, kernel):
             "kernel": kernel, "kernel_ms": round(agent_ms, 4), "flops_per_launch": flops}
 
 
+def profile_order(path):
+    """Sort key of a profiles/ file: (round, session, name).  Files are named
+    r<round>_<what>_s<session>[suffix].json; the round-1 files carry neither (round 1,
+    session 0).  Numeric, so r3_..._s10 sorts after r3_..._s9."""
+    import re
+    name = os.path.basename(path)
+    mr = re.match(r"r(\d+)_", name)
+    ms = re.search(r"_s(\d+)[a-z]?\.[a-z]+$", name)
+    return (int(mr.group(1)) if mr else 1, int(ms.group(1)) if ms else 0, name)
+
+
 def pmc_lookup(pattern, **match):
-    """First profiles/ summary matching the workload keys (n, m, E, L), else None."""
-    # newest round first: profiles are named r<round>_..., the round-1 files carry no prefix
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+    """Newest profiles/ summary matching the workload keys (n, m, E, L), else None."""
+    # newest first by (round, session) parsed from the name (profile_order)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=profile_order, reverse=True):
         try:
             pm = json.load(open(path))
         except (ValueError, OSError):
@@ -209,9 +220,20 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
     bound = "hbm"
     if issue and issue["valu_issue_frac"] < 0.5 and issue["mfma_busy_frac"] < 0.5 and frac < 0.6:
         bound = "latency/store-ack"
+    traffic = None
+    if pm:
+        # the profiled launch is one whole episode: its reset row + steps_per_launch steps
+        # (resets_per_launch, 1 for tools/round_profile.sh's launches).  Put the reset on the
+        # same side as bytes_per_launch: per step, the profile's reset share is replaced by
+        # this window's (resets_per_step) at the reset's algorithmic size, so that
+        # traffic / bytes_per_launch is the measured-over-algorithmic ratio of the steps
+        spl = pm.get("steps_per_launch", 1)
+        rpl = pm.get("resets_per_launch", 1 if spl > 1 else 0)
+        rb = reset_bytes(a.n, a.m, a.L) * E
+        traffic = round((pm["hbm_bytes_per_launch"] - rpl * rb) / spl + resets_per_step * rb)
     out = {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(frac, 4),
-           "traffic": round(pm["hbm_bytes_per_launch"] / pm.get("steps_per_launch", 1)) if pm else None,
+           "traffic": traffic,
            "kernel": "asg::rollout_kernel (env steps + agent/eps-greedy selections, per step)",
            "kernel_ms": round(fused_ms, 4), "bytes_per_launch": per_launch,
            "per_launch_note": "per env step of the launch (bytes_per_launch, kernel_ms: one step's share; "
@@ -220,6 +242,9 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
            "frac_note": "frac is against the 8 TB/s HBM peak"}
     if pm:
         out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
+        out["traffic_over_algorithmic"] = round(traffic / per_launch, 4)
+        out["traffic_note"] = ("PMC bytes per step of the profiled whole-episode launch, its reset row's share "
+                               "replaced by this window's resets_per_step (same accounting as bytes_per_launch)")
     if issue:
         out["issue"] = issue
     return out
@@ -373,9 +398,13 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         e1.record()
         pairs.append((e0, e1, w))
 
+    gather_pairs = []
+
     def new_episode():
         if runner.batch is not None and runner.env.k == a.T:
-            runner.finish_episode(sync=False)  # returns gathered on the device; host checks deferred
+            # returns gathered on the device; host checks deferred.  Timed with HIP events on the
+            # current stream (a collective's work is joined to it before the end event)
+            timed(gather_pairs, lambda: runner.finish_episode(sync=False))
         runner.reset(env_reset=False)
         mac.init_hidden(E)
         state["t"] = 0
@@ -456,7 +485,8 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
            "lsa_ms": mean(lsa_pairs) if lsa_pairs else None,
            "fused_ms": mean(fused_pairs) if fused_pairs else None, "mode": state.get("mode"),
            "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs),
-           "fused_resets": state.get("fused_resets", 0)}
+           "fused_resets": state.get("fused_resets", 0),
+           "gather_ms": mean(gather_pairs) if gather_pairs else None, "gathers": len(gather_pairs)}
     if count_lsa and selector == "sap" and a.n <= a.m <= 64:
         # one more selection on the current state, with the step-counting kernel instance
         sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
@@ -469,12 +499,20 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         res["path_steps_per_launch"] = int(sel_obj.count_steps.sum().item())
         sel_obj.count_steps = None
     if world > 1:
+        # every rank's figures (one all-gather): the job's time is the slowest rank's; the
+        # per-rank spread of the kernel time and the per-episode returns all-gather are reported
+        # so that a scaling loss can be attributed
         import torch.distributed as tdist
-        t = torch.tensor([res["elapsed"], res["kern_ms"], res["sel_ms"]], dtype=torch.float64, device=dev)
+        keys = ("elapsed", "kern_ms", "sel_ms", "fused_ms", "gather_ms")
+        mine = torch.tensor([float(res[k] or 0.0) for k in keys], dtype=torch.float64, device=dev)
         if tdist.get_backend() == "gloo":
-            t = t.cpu()
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        res["elapsed"], res["kern_ms"], res["sel_ms"] = float(t[0]), float(t[1]), float(t[2])
+            mine = mine.cpu()
+        allr = torch.empty(world * len(keys), dtype=torch.float64, device=mine.device)
+        tdist.all_gather_into_tensor(allr, mine)
+        allr = allr.view(world, len(keys)).cpu()
+        res["per_rank"] = {k: [round(float(x), 5) for x in allr[:, i]] for i, k in enumerate(keys)}
+        res["backend"] = tdist.get_backend()
+        res["elapsed"], res["kern_ms"], res["sel_ms"] = (float(allr[:, i].max()) for i in range(3))
     res["global_envs"] = runner.global_envs
     runner.close_env()
     del runner, mac, env
@@ -562,7 +600,9 @@ def main():
                 "schedule": r.get("mode") or "split"}
 
     if secondary:
-        sk, sw = max(10, a.steps // 2), max(5, a.warmup // 2)
+        # at least one episode per leg, so the window holds a reset at the rate of the profiled
+        # whole-episode launches (fused_roofline's traffic accounting)
+        sk, sw = max(a.T, a.steps // 2), max(5, a.warmup // 2)
         if a.selector != "random":
             r2 = run_leg(a, dev, world, E, sk, sw, selector="eps", agent="rnn")
             extra["pytorch_agent"] = {
@@ -681,6 +721,20 @@ def main():
             "roofline_agent": ra,
             "cpu_baseline": cpu,
         }
+        if world > 1:
+            pr = res["per_rank"]
+            kern = pr["fused_ms"] if any(pr["fused_ms"]) else pr["kern_ms"]
+            line["multi_rank"] = {
+                "backend": res["backend"],
+                "backend_note": "torch.distributed backend initialised ('nccl' is RCCL on ROCm)",
+                "kernel": "fused_rollout_per_step" if any(pr["fused_ms"]) else "env_step",
+                "kernel_ms_max": max(kern), "kernel_ms_min": min(kern),
+                "all_gather_returns_ms_max": max(pr["gather_ms"]), "all_gather_returns_ms_min": min(pr["gather_ms"]),
+                "gathers_per_rank": res.get("gathers"),
+                "elapsed_s_per_rank": pr["elapsed"], "kernel_ms_per_rank": kern,
+                "all_gather_returns_ms_per_rank": pr["gather_ms"],
+                "note": "HIP-event times per rank: the kernel per step, and GpuVecRunner.finish_episode (the "
+                        "per-episode all-gather of the float64 returns) per episode inside the timed window"}
         if a.selector == "sap":
             line["roofline_lsa"] = lsa_roofline(a, E, res)
         if extra:

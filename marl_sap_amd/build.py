@@ -36,13 +36,30 @@ def build(force=False, verbose=False, out=None, extra=()):
     if out is None and not force and not needs_build():
         return LIB
     target = out or LIB
-    cmd = [HIPCC] + FLAGS + list(extra) + [os.path.join(CSRC, s) for s in SOURCES] + ["-o", target + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError("hipcc failed building libmarl_sap_amd.so")
+    # one hipcc per source in parallel (the translation units are independent: -fno-gpu-rdc),
+    # then one link
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with tempfile.TemporaryDirectory(prefix="asg_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+        compile_flags = [f for f in FLAGS if f != "-shared"]
+        cmds = [[HIPCC] + compile_flags + list(extra) + ["-c", os.path.join(CSRC, s), "-o", o]
+                for s, o in zip(SOURCES, objs)]
+        if verbose:
+            for c in cmds:
+                print(" ".join(c))
+        with ThreadPoolExecutor(jobs) as ex:
+            results = list(ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds))
+        for r in results:
+            if r.returncode != 0:
+                sys.stderr.write(r.stdout + r.stderr)
+                raise RuntimeError("hipcc failed building libmarl_sap_amd.so")
+        link = [HIPCC] + FLAGS + list(extra) + objs + ["-o", target + ".tmp"]
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError("hipcc failed linking libmarl_sap_amd.so")
     os.replace(target + ".tmp", target)
     return target
 

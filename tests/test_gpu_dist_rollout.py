@@ -97,6 +97,18 @@ def test_bench_multi_rank_branch(tmp_path):
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_envs"] == 512 and line["value"] > 0
     assert line["scaling"] == "weak" and line["cpu_baseline"] is None
+    # the self-explaining multi-rank keys: backend, per-rank kernel spread, returns all-gather time
+    mr = line["multi_rank"]
+    assert mr["backend"] == "gloo"
+    assert len(mr["kernel_ms_per_rank"]) == 2 and 0 < mr["kernel_ms_min"] <= mr["kernel_ms_max"]
+    # 13 steps from t = 0 at T = 20: the window holds no episode end, so no gather was timed
+    assert mr["gathers_per_rank"] == 0 and mr["all_gather_returns_ms_max"] == 0.0
+    r = subprocess.run(cmd[:-12] + ["--steps", "30", "--warmup", "3", "--envs", "256", "--cpu-baseline", "0",
+                                   "--secondary", "0"], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    mr = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])["multi_rank"]
+    assert mr["gathers_per_rank"] == 1 and mr["all_gather_returns_ms_max"] > 0.0
 
 
 def test_configs3_per_rank_size_and_rccl_rehearsal(tmp_path):

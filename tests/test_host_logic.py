@@ -140,6 +140,30 @@ def test_bench_accounting():
     assert bench.agent_peak(64, 64, 3, 1) == pytest.approx(81920 / (32768 / 157.3 + 49152 / (2500 / 6)))
 
 
+def test_bench_profile_order_and_reset_share(monkeypatch):
+    """pmc_lookup takes the newest summary by (round, session) -- s10 after s9 -- and the
+    fused roofline's PMC traffic carries the same reset share as its bytes_per_launch."""
+    import types
+    import bench
+    names = ["pmc_step_kernel.json", "r3_pmc_x_s9.json", "r3_pmc_x_s10.json", "r2_pmc_x_s4.json",
+             "r3_pmc_x_256_s2.json", "r4_pmc_x_s1.json"]
+    order = sorted(names, key=bench.profile_order)
+    assert order == ["pmc_step_kernel.json", "r2_pmc_x_s4.json", "r3_pmc_x_256_s2.json", "r3_pmc_x_s9.json",
+                     "r3_pmc_x_s10.json", "r4_pmc_x_s1.json"]
+    a = types.SimpleNamespace(n=256, m=256, L=3)
+    E, spl = 2048, 20
+    step = bench.step_bytes(256, 256, 3) + 256 * (2 * 4 * 64 + 8)
+    rb = bench.reset_bytes(256, 256, 3)
+    # a profiled launch = reset + 20 steps, measured at 1.02x its algorithmic bytes
+    prof = {"hbm_bytes_per_launch": 1.02 * E * (spl * step + rb), "steps_per_launch": spl, "_path": "r4_x_s1.json"}
+    monkeypatch.setattr(bench, "pmc_lookup", lambda pattern, **kw: prof if "rollout_kernel" in pattern else None)
+    for rps in (0.0, 1.0 / spl):
+        roof = bench.fused_roofline(a, E, 1.0, resets_per_step=rps)
+        # the profile's reset share swapped for the window's: the ratio stays near 1.02
+        assert roof["traffic_over_algorithmic"] == pytest.approx(1.02, abs=0.002)
+        assert roof["traffic"] / roof["bytes_per_launch"] == pytest.approx(1.02, abs=0.002)
+
+
 @pytest.mark.parametrize("time_major", [False, True])
 def test_replay_buffer_matches_reference(golden, time_major):
     """Ring inserts (a split insert included), counters and seeded sample() against the
