@@ -292,7 +292,9 @@ int asg_filtered_topm(const void *beta, int beta_dtype, const int64_t beta_strid
  * th.rand_like draws, parity mode) or NULL = Philox uniforms keyed (seed, env_index_base + b,
  * counter).  FilteredSAPActionSelector's exploration: gauss_noise [B][n][m] f32 added as given,
  * or, when NULL and gauss_epsilon > 0, N(0, std^2) per env with std = float32(mean|mat[b]| *
- * eps) * 2 (Philox Box-Muller).  q [B][n][M+1] f32 any strides; mat_out [B][n][m] contiguous. */
+ * eps) * 2 (Philox Box-Muller; n <= 8188 agents: the per-agent sums stay in 64 KiB of LDS, else
+ * ASG_E_INVALID_ARG -- pass gauss_noise for larger n).  q [B][n][M+1] f32 any strides; mat_out
+ * [B][n][m] contiguous. */
 int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int64_t *topm, int64_t B, int n, int m,
                           int M, const float *tie_noise, double gauss_epsilon, const float *gauss_noise,
                           uint64_t seed, uint64_t counter, int64_t env_index_base, float *mat_out,

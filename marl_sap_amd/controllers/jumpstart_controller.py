@@ -2,13 +2,16 @@
 probability jumpstart_epsilon (one numpy coin flip per selection for the whole batch, drawn
 from numpy's global stream like the reference) the non-RL selector (HAA) acts.
 
-The GPU runner draws an episode's coin flips when it plans the episode (fused_mode), in the
-reference's order (one per select_actions call, t = 0, 1, ...): nothing else draws from
-numpy's global stream inside the loop, so the stream is consumed exactly as the reference's
-per-step draws consume it.  When every flip picks the RL branch and the RL MAC fuses (the
-RNNAgent + epsilon-greedy: mock_constellation_iql.yaml), the episode is one asg_rollout
-kernel; otherwise the RL steps still fuse env.step(t) with select_actions(t + 1) where they
-can, and the HAA steps run env.step + the HAA selector."""
+When the RL MAC fuses (the RNNAgent + epsilon-greedy: mock_constellation_iql.yaml) the GPU
+runner draws an episode's coin flips when it plans the episode (fused_mode), in the
+reference's order (one per select_actions call, t = 0, 1, ...): the epsilon-greedy selector
+draws nothing from numpy's global stream, so the stream is consumed exactly as the
+reference's per-step draws consume it.  When every flip picks the RL branch the episode is
+one asg_rollout kernel; otherwise the RL steps still fuse env.step(t) with
+select_actions(t + 1), and the HAA steps run env.step + the HAA selector.  Any other RL
+selector may draw from the same stream itself (EpsilonGreedySAPTestActionSelector,
+sap_selectors.py:36): then nothing is pre-drawn and each select_actions draws its flip when
+it runs, interleaved with the selector's draws as in the reference."""
 import numpy as np
 
 from ..action_selectors.non_rl_selectors import REGISTRY as non_rl_REGISTRY
@@ -44,14 +47,17 @@ class JumpstartMAC(BasicMAC):
         return super().select_actions(ep_batch, t_ep, t_env, bs=bs, test_mode=test_mode, out=out)
 
     def fused_mode(self, env, ep_batch, t_env=0, test_mode=False):
-        """Draw the episode's T coin flips now (the reference's order); "episode" when every
-        one picks the RL branch and the RL MAC fuses, else the base class's per-step choice
-        ("step" fuses the RL steps' env.step + selection) or None."""
-        eps = self._eps(t_env, test_mode)
-        self._flips = list(np.random.rand(env.T) < eps)
+        """When the RL MAC fuses (its selector is epsilon-greedy, which draws nothing from
+        numpy's global stream): draw the episode's T coin flips now (the reference's order);
+        "episode" when every one picks the RL branch, else "step" (the RL steps' env.step +
+        selection fused).  Otherwise None, and no flip is pre-drawn: each select_actions
+        draws its own, interleaved with the RL selector's draws as in the reference."""
         base = super().fused_mode(env, ep_batch, t_env, test_mode)
         if base is None:
+            self._flips = []
             return None
+        eps = self._eps(t_env, test_mode)
+        self._flips = list(np.random.rand(env.T) < eps)
         return "episode" if base == "episode" and not any(self._flips) else "step"
 
     def fused_episode(self, env, ep_batch, t_env, test_mode=False, reset=False):

@@ -187,9 +187,13 @@ int asg_reset(asg_handle *h, const asg_batch_view *b, int ts) {
     if (h->st.benefit_mode == ASG_BENEFIT_INJECTED && !h->table_ready)
         return fail(h, ASG_E_STATE, "benefit_mode=injected needs asg_set_benefits before reset");
     DeviceGuard g(h->device);
-    if (h->has_reset) h->st.episode += 1;  // Philox: a fresh key per episode (first = 0)
-    hipError_t e = asg::launch_reset(*b, h->st, ts, !h->constructed, h->stream);
+    // Philox: a fresh key per episode (first = 0), committed to the handle only once the
+    // launch succeeded (a failed launch leaves the handle as it was)
+    asg::EnvState st = h->st;
+    if (h->has_reset) st.episode += 1;
+    hipError_t e = asg::launch_reset(*b, st, ts, !h->constructed, h->stream);
     if (e != hipSuccess) return hip_fail(h, e, "asg_reset");
+    h->st.episode = st.episode;
     h->constructed = true;
     h->has_reset = true;
     h->k = 0;
@@ -460,6 +464,8 @@ int asg_filtered_topm(const void *beta, int beta_dtype, const int64_t beta_strid
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_filtered_topm");
 }
 
+static constexpr int kFilteredGaussMaxAgents = (64 * 1024 - 32) / 8;  // 8188
+
 int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int64_t *topm, int64_t B, int n, int m,
                           int M, const float *tie_noise, double gauss_epsilon, const float *gauss_noise,
                           uint64_t seed, uint64_t counter, int64_t env_index_base, float *mat_out,
@@ -472,8 +478,10 @@ int asg_filtered_benefits(const float *q, const int64_t q_strides[3], const int6
     if (B == 0) return ASG_OK;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     const bool gauss = gauss_noise != nullptr || gauss_epsilon > 0.0;
-    if (gauss && !gauss_noise && (size_t)n * sizeof(double) > 64 * 1024)
-        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: n > 8192 agents with Gaussian noise");
+    // generated noise: the per-agent |row| sums (8 B each) plus the 32-B partials in LDS, within
+    // the 64 KiB a workgroup may hold on every CDNA part (gfx950's 160 KiB not assumed)
+    if (gauss && !gauss_noise && n > kFilteredGaussMaxAgents)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_filtered_benefits: n > 8188 agents with generated Gaussian noise");
     hipError_t e = asg::launch_filtered_matrix(q, q_strides, topm, B, n, m, M, tie_noise, seed, (uint32_t)counter,
                                                env_index_base, mat_out, nullptr, s);
     if (e == hipSuccess && gauss)
@@ -547,6 +555,9 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
         return fail(h, ASG_E_STATE, "asg_rollout: select_first selects on the reset row (k == 0 only)");
     if (select_last && k0 + steps >= st.T)
         return fail(h, ASG_E_STATE, "asg_rollout: select_last needs a next step to select for (k + steps < T)");
+    // the kernel writes batch rows ts .. ts + steps of the [T + 1]-row time-major batch
+    if (ts < 0 || ts + steps > st.T)
+        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: batch rows ts .. ts + steps must lie in the [T + 1]-row batch");
     if (st.bids || st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED)
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: Philox bump/dense benefits with integer actions only");
     if (hidden != 64 || !asg::rollout_shape_ok(st.n, st.m, st.L, K))
@@ -574,11 +585,14 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: needs a contiguous time-major batch (EpisodeBatch(time_major=True))");
     DeviceGuard g(h->device);
     hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
-    if (reset && h->has_reset) h->st.episode += 1;  // as asg_reset: a fresh Philox key per episode
-    hipError_t e = asg::launch_rollout(sl, h->st, ts, k0, steps, select_first, select_last, reset,
+    // as asg_reset: a fresh Philox key per episode, committed once the launch succeeded
+    asg::EnvState lst = h->st;
+    if (reset && h->has_reset) lst.episode += 1;
+    hipError_t e = asg::launch_rollout(sl, lst, ts, k0, steps, select_first, select_last, reset,
                                        static_cast<const float4 *>(packed), b1, b_r0, b_r1, b2, use_rnn, h_in, h_stride,
                                        h_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);
     if (e != hipSuccess) return hip_fail(h, e, "asg_rollout");
+    h->st.episode = lst.episode;
     if (reset) {
         h->constructed = true;
         h->has_reset = true;

@@ -306,6 +306,15 @@ __device__ int lsa_solve_wave(const Acc &acc, int nr, int nc, int (&col4row)[CPL
 typedef uint32_t lsa_u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double dbl_of(uint32_t lo, uint32_t hi) { return __builtin_bit_cast(double, lsa_u32x2{lo, hi}); }
 
+// index of the lowest set bit of a wave-uniform 64-bit mask as one s_ff1_i32_b64, defined for
+// every input (-1 for an empty mask, whose low six bits read lane 63); __builtin_ctzll(0) would
+// be poison the optimizer may reason from
+__device__ __forceinline__ int sff1(uint64_t x) {
+    int r;
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(x));
+    return r;
+}
+
 template <class Acc, bool kCount = false>
 __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1], int *steps = nullptr) {
 #ifdef ASG_LSA_GENERIC_REG
@@ -352,7 +361,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
             const uint64_t cm = ASG_LSA_NAN_KEYS ? __ballot(key == kmin) : (__ballot(key == kmin) & rem);
             asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
             const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
-            jsel = (int)__builtin_ctzll(cm);  // the first candidate: the selection when it is the only one
+            jsel = sff1(cm);  // the first candidate: the selection when it is the only one (ncand 0: -1)
             uint32_t lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
             lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
             int psel = __builtin_amdgcn_readlane(pos, jsel);
@@ -378,7 +387,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
                 const uint32_t k = (r4c == -1) ? (0x80000000u | (uint32_t)pos) : ((1u << 30) - (uint32_t)pos);
                 const uint32_t tk = wave_max_u32_bcast(cb ? k : 0u);
                 psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
-                jsel = (int)__builtin_ctzll(__ballot(pos == psel) & rem) & 63;  // positions are distinct
+                jsel = sff1(__ballot(pos == psel) & rem) & 63;  // positions are distinct
                 if (ncand == 0) lowest_hi = 0x7ff00000u;
             }
             // remaining[index] = remaining[--num_remaining]
@@ -559,7 +568,7 @@ __device__ __forceinline__ void lsa_pick(LsaLane &L, LsaScal &Sc, float key, flo
     asm("s_bcnt1_i32_b64 %0, %1" : "=s"(nc) : "s"(cm));
     Sc.cm = cm;
     Sc.ncand = nc;
-    const int j = cm ? (int)__builtin_ctzll(cm) : 0;
+    const int j = sff1(cm) & 63;  // cm == 0: lane 63, any lane would do
     const uint64_t sb = __builtin_bit_cast(uint64_t, L.spc);
     Sc.jsel = j;
     Sc.lo_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, j);
@@ -585,7 +594,7 @@ __device__ __forceinline__ void lsa_tie(LsaLane &L, LsaScal &Sc) {
     const uint32_t tk = wave_max_u32_bcast(cb ? k : 0u);
     Sc.psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
     const uint64_t own = __ballot(L.pos == Sc.psel) & Sc.rem;  // positions are distinct
-    Sc.jsel = own ? (int)__builtin_ctzll(own) : 0;
+    Sc.jsel = sff1(own) & 63;
     if (Sc.ncand == 0) Sc.lo_hi = 0x7ff00000u;  // leaves the row loop; reported as invalid
 }
 // step, part 3: column jsel leaves `remaining` (swap-with-last positions), minv = lowest, the

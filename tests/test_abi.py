@@ -80,6 +80,13 @@ def test_kernel_entry_points_validate_without_gpu(L):
     agent = [None] * 5 + [256, 64, 1, None, 0, None, 0.05, 0, 1, None, None]
     assert L.asg_rollout(None, None, 0, 1, 1, 0, *agent) == _lib.ASG_E_INVALID_ARG
     assert L.asg_reset_rollout(None, None, 0, 1, 0, *agent) == _lib.ASG_E_INVALID_ARG
+    # asg_filtered_benefits with generated Gaussian noise: n <= 8188 agents (64 KiB of LDS per
+    # workgroup on every CDNA part); rejected before any device call above that
+    fake = ctypes.c_void_p(16)
+    args = lambda n: (fake, st, fake, 1, n, 8, 4, None, 0.5, None, 0, 0, 0, fake, None)  # noqa: E731
+    assert L.asg_filtered_benefits(*args(8189)) == _lib.ASG_E_INVALID_ARG
+    assert "8188" in _lib.last_error()
+    assert L.asg_sap_slots(-1) in (0, 1, 2, 3)  # query only
 
 
 def _h2_geom(K, m):

@@ -183,3 +183,40 @@ def test_continuous_selector_cpu():
     torch.manual_seed(0)
     y = sel.select_action(x, None, 200)  # annealed to epsilon_finish
     assert sel.variance == 0.1 and 0.05 < float((y - x).std()) < 0.15
+
+
+@pytest.mark.parametrize("selector", ["epsilon_greedy_sap_test", "sap"])
+def test_jumpstart_flips_keep_reference_stream_order(selector):
+    """JumpstartMAC pre-draws an episode's coin flips only when its RL MAC fuses (the
+    epsilon-greedy selector draws nothing from numpy's global stream).  With an RL selector
+    that does draw (EpsilonGreedySAPTestActionSelector, reference sap_selectors.py:36) nothing
+    is pre-drawn: each step draws its flip, then the selector its own -- the reference's
+    order (jumpstart_controller.py:33)."""
+    from types import SimpleNamespace
+    import numpy as np
+    import torch
+    from marl_sap_amd.controllers import REGISTRY as mac_REGISTRY
+    n, m, T = 4, 4, 5
+    args = SimpleNamespace(n=n, m=m, T=T, agent="rnn", hidden_dim=64, use_rnn=True, obs_last_action=False,
+                           obs_agent_id=False, agent_output_type="q", action_selector=selector, seed=0,
+                           epsilon_start=0.5, epsilon_finish=0.5, epsilon_anneal_time=1, evaluation_epsilon=0.0,
+                           jumpstart_action_selector="haa_selector", jumpstart_epsilon_start=0.5,
+                           jumpstart_epsilon_finish=0.5, jumpstart_epsilon_anneal_time=1,
+                           jumpstart_evaluation_epsilon=0.0, fused_rollout=True)
+    scheme = {"obs": {"vshape": m * 4}, "actions_onehot": {"vshape": (m,)}}
+    mac = mac_REGISTRY["jumpstart_mac"](scheme, {"agents": n}, args)
+    env = SimpleNamespace(T=T, m=m, can_step_select=lambda **k: True)
+    batch = SimpleNamespace(time_major=True)
+    np.random.seed(123)
+    with torch.no_grad():
+        mode = mac.fused_mode(env, batch, 0)
+    assert mode is None and mac._flips == []
+    # nothing drawn yet: the next draw is the stream's first
+    first = np.random.rand()
+    np.random.seed(123)
+    assert np.random.rand() == first
+    # per step: the flip is drawn when the step runs
+    np.random.seed(7)
+    flips = [mac._coin(0, False) for _ in range(3)]
+    np.random.seed(7)
+    assert flips == list(np.random.rand(3) < 0.5)
