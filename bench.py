@@ -64,18 +64,19 @@ BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 X3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6
 SIMDS, CLOCK_HZ = 1024, 2.4e9  # 256 CUs x 4 SIMDs, max clock (MI355X_MICROARCH.md)
 VALU_CYCLES_PER_WAVE_INSTR = 2  # wave64 VALU over a SIMD-32 (MI355X_MICROARCH.md "Wave scheduling")
+FUSED_AGENTS = ("rnn", "rnn_fused")  # agent names that resolve to RNNFusedAgent (modules/agents)
 CPU_WORKER_CAP = 16  # CPU share of one GPU on the gpurun box (os.cpu_count() shows the whole host)
 
 CONFIGS = {
-    0: dict(n=4, m=4, envs=1, selector="eps", agent="rnn_fused", benefits="bump",
+    0: dict(n=4, m=4, envs=1, selector="eps", agent="rnn", benefits="bump",
             label="4-agent/4-task assignment env, batch_size_run=1 (configs[0]: the reference's plumbing case)"),
-    1: dict(n=16, m=16, envs=4096, selector="random", agent="rnn_fused", benefits="bump",
+    1: dict(n=16, m=16, envs=4096, selector="random", agent="rnn", benefits="bump",
             label="16-agent/16-task assignment env, 4096 envs per GPU, random policy (configs[1])"),
-    2: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn_fused", benefits="bump",
+    2: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn", benefits="bump",
             label="64-agent/64-task assignment env, 16384 envs per GPU, BasicMAC+RNN (configs[2])"),
-    3: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn_fused", benefits="bump",
+    3: dict(n=64, m=64, envs=16384, selector="eps", agent="rnn", benefits="bump",
             label="64-agent/64-task assignment env, 16384 envs per GPU sharded over the node (configs[3])"),
-    4: dict(n=256, m=256, envs=2048, selector="eps", agent="rnn_fused", benefits="dense",
+    4: dict(n=256, m=256, envs=2048, selector="eps", agent="rnn", benefits="dense",
             label="256-agent/256-task dense-benefit assignment env, 2048 envs per GPU (configs[4])"),
 }
 
@@ -128,7 +129,7 @@ def agent_roofline(a, E, agent_ms, kernel):
     against HBM (both reported; `bound` names the larger fraction)."""
     if agent_ms is None or agent_ms <= 0:
         return None
-    fused = a.agent == "rnn_fused"
+    fused = a.agent in FUSED_AGENTS
     onehot = fused and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
     flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
     tfs = flops / (agent_ms * 1e-3) / 1e12
@@ -263,8 +264,9 @@ def parse(argv=None):
     p.add_argument("--L", type=int, default=3)
     p.add_argument("--selector", default=None, choices=["eps", "sap", "random"])
     p.add_argument("--benefits", default=None, choices=["bump", "dense"])
-    p.add_argument("--agent", default=None, choices=["rnn_fused", "rnn"],
-                   help="rnn_fused: the same RNNAgent (weights, fp32) with its inference forward as one HIP kernel")
+    p.add_argument("--agent", default=None, choices=["rnn", "rnn_fused", "rnn_torch"],
+                   help="rnn (the reference's name; default): the RNNAgent with its inference forward as one HIP "
+                        "kernel wherever the shape allows (= rnn_fused); rnn_torch: the plain PyTorch module")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-episodes", type=int, default=2, help="minimum CPU-baseline episodes")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample length (s)")
@@ -604,13 +606,13 @@ def main():
         # whole-episode launches (fused_roofline's traffic accounting)
         sk, sw = max(a.T, a.steps // 2), max(5, a.warmup // 2)
         if a.selector != "random":
-            r2 = run_leg(a, dev, world, E, sk, sw, selector="eps", agent="rnn")
+            r2 = run_leg(a, dev, world, E, sk, sw, selector="eps", agent="rnn_torch")
             extra["pytorch_agent"] = {
                 **leg_base(r2, sk, sw),
-                "what": "configs[2] read literally: BasicMAC + the PyTorch RNNAgent module (hipBLASLt linears + "
-                        "GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
+                "what": "agent rnn_torch (the explicit opt-out): BasicMAC + the plain PyTorch RNNAgent module "
+                        "(hipBLASLt linears + GRUCell, fp32) + asg_epsilon_greedy kernel, same env step",
                 "select_ms": round(r2["sel_ms"], 4), "env_step_ms": round(r2["kern_ms"], 4)}
-        if a.selector == "eps" and a.agent == "rnn_fused":
+        if a.selector == "eps" and a.agent in FUSED_AGENTS:
             # the other schedules of the same workload: one fused launch per step, and separate
             # env-step + agent launches
             r4 = run_leg(a, dev, world, E, sk, sw, fused=3)
@@ -626,7 +628,7 @@ def main():
                 "what": "same workload with --fused-rollout 0: asg_step then the fused agent forward + eps-greedy "
                         "kernel (rnn_agent_h2_kernel), one launch each per step"}
         if a.n <= a.m <= 64 and a.selector != "sap":
-            r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn_fused", count_lsa=True)
+            r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn", count_lsa=True)
             agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)
             extra["sap"] = {
                 **leg_base(r3, sk, sw),
@@ -647,7 +649,7 @@ def main():
             for name, sel_, yaml in (("iql", "eps", "mock_constellation_iql.yaml"),
                                      ("reda", "sap", "mock_constellation_reda.yaml")):
                 eps_over = dict(epsilon_start=1.0, epsilon_finish=0.0, epsilon_anneal_time=20000)
-                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn_fused", **js, **eps_over)
+                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn", **js, **eps_over)
                 extra[name] = {
                     **leg_base(rj, sk, a.T),
                     "what": f"{yaml}: jumpstart_mac (haa_selector jumpstart) + "
@@ -671,7 +673,7 @@ def main():
             c4.config = 4
             r5 = run_leg(c4, dev, world, c4.envs, sk, sw)
             leg = {**leg_base(r5, sk, sw),
-                   "workload": CONFIGS[4]["label"] + f"; T={a.T}, L={a.L}, BasicMAC+rnn_fused(GRU 64, fp32) + "
+                   "workload": CONFIGS[4]["label"] + f"; T={a.T}, L={a.L}, BasicMAC+rnn(GRU 64, fp32, fused kernel) + "
                                                      "epsilon-greedy 0.05, dense benefits",
                    "envs_per_gpu": c4.envs, "n": c4.n, "m": c4.m,
                    "kernels_ms": {"fused_rollout_per_step": round(r5["fused_ms"], 4) if r5.get("fused_ms") else None,
@@ -693,7 +695,7 @@ def main():
         ra = agent_roofline(a, E, sel_ms - (res["lsa_ms"] or 0.0), f"{a.agent} forward")
     else:
         ra = agent_roofline(a, E, sel_ms, "asg::rnn_agent_h2_kernel (forward + eps-greedy)"
-                            if a.agent == "rnn_fused" else "torch RNNAgent + asg_epsilon_greedy")
+                            if a.agent in FUSED_AGENTS else "torch RNNAgent + asg_epsilon_greedy")
     if rank == 0:
         sel_name = {"eps": "epsilon-greedy", "sap": "SAP", "random": "random"}[a.selector]
         line = {

@@ -558,8 +558,9 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     // the kernel writes batch rows ts .. ts + steps of the [T + 1]-row time-major batch
     if (ts < 0 || ts + steps > st.T)
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: batch rows ts .. ts + steps must lie in the [T + 1]-row batch");
-    if (st.bids || st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED)
-        return fail(h, ASG_E_INVALID_ARG, "asg_rollout: Philox bump/dense benefits with integer actions only");
+    // every benefit source: Philox bumps in registers, or the handle's float64 table (MT19937
+    // compat / injected), whose reset is asg_reset (above: no asg_reset_rollout)
+    if (st.bids) return fail(h, ASG_E_INVALID_ARG, "asg_rollout: integer actions only (not bids_as_actions)");
     if (hidden != 64 || !asg::rollout_shape_ok(st.n, st.m, st.L, K))
         return fail(h, ASG_E_INVALID_ARG,
                     "asg_rollout: needs the RNNAgent (hidden 64) on the env's obs (K = m (L + 1), L >= 1), "

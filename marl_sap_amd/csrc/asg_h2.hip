@@ -994,6 +994,9 @@ struct RolloutArgs {
     float wmin, wmax;
     int k0, k1, select_first, select_last;
     int reset;  // the envs' reset (asg_reset) runs first, in this launch
+    // benefits: NULL = Philox bumps regenerated in registers; else the handle's float64 table
+    // [E][T][n][m] (MT19937 compat / injected sat_prox_mat), read for the L lookahead rows
+    const double *table;
     // agent
     const u32x4v *pk;
     const float *W1T, *Hin;
@@ -1085,7 +1088,7 @@ __device__ __forceinline__ void rollout_actions_from_batch(RA &ra, int64_t e, in
 // one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
 // terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
 // launch, or read from the batch by the env prologue)
-template <class RA>
+template <bool TAB, class RA>
 __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int ts, const EnvKey &key,
                                                    const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
                                                    uint16_t *s_prev, double *s_ret) {
@@ -1101,6 +1104,7 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
     for (int i = lane; i < n; i += 64) atomicAdd(&s_cnt[s_act[i]], 1);
     wave_lds_fence();
     const BumpShape bsh = bump_shape(ra.T, ra.wmin, ra.wmax);
+    (void)bsh;
     double sum = 0.0;  // Python's sum(rewards), left to right: lane order within each 64-agent chunk
     // two copies of the loop, with and without an injected T_trans: merged, the join after
     // the table load made every transition wait for the previous tile's stores (vmcnt)
@@ -1111,8 +1115,14 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
             double rr = 0.0;
             if (i < n) {
                 const int j = s_act[i], p = s_prev[i];
-                const Bump32 b = philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
-                const double beta = bump64_at(b, k);
+                double beta;
+                if constexpr (TAB) {
+                    beta = ra.table[(((int64_t)e * ra.T + k) * n + i) * m + j];
+                } else {
+                    const Bump32 b =
+                        philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
+                    beta = bump64_at(b, k);
+                }
                 const double tt = TT ? ra.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
                 const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
                 const double bh = beta - ra.lambda_ * pen;
@@ -1164,7 +1174,7 @@ struct HNext {
     int mode;
 };
 
-template <bool RNN, bool W2L, bool GEN, bool AGENT, class RA>
+template <bool RNN, bool W2L, bool GEN, bool TAB, bool AGENT, class RA>
 __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
                                              uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
@@ -1300,8 +1310,9 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
         }
         const bool st_now = stores && attempt == 0 && !(ASG_ROLLOUT_XSKIP & 1);
         for (int u = 0; u < Ub; ++u) {
-            // bump parameters of the lane's 16 (row, task) pairs of this chunk
+            // bump parameters of the lane's 16 (row, task) pairs of this chunk (Philox mode)
             Bump32 bp[2][4][NT];
+            if constexpr (!TAB) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const int jw = 32 * u + 16 * c + 4 * q;
@@ -1337,12 +1348,34 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                     }
                 }
             }
+            }
             for (int l = 1; l <= L; ++l) {
                 const int t = kk + l - 1;
                 // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
                 // past T are zeros)
                 float4 xv[2][NT];
-                if (t < T) {
+                if (TAB && t < T) {
+                    // the table's float64 benefits, rounded once to float32 (the batch's dtype,
+                    // as the separate step's rows): B[e][t][row][j0 .. j0 + 3]
+                    const double *trow = ra.table + ((int64_t)e * T + t) * n * m;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            const int j0 = 32 * u + 16 * c + 4 * q;
+                            const double *tp = trow + (int64_t)ia[nt] * m + j0;
+                            if (!GEN) {
+                                const double2 a = *reinterpret_cast<const double2 *>(tp);
+                                const double2 b = *reinterpret_cast<const double2 *>(tp + 2);
+                                xv[c][nt] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+                            } else {
+                                float v4[4];
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) v4[v] = (ok[nt] && j0 + v < m) ? (float)tp[v] : 0.f;
+                                xv[c][nt] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                            }
+                        }
+                } else if (!TAB && t < T) {
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -1465,7 +1498,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
     }
 }
 
-template <bool RNN, bool W2L, bool GEN>
+template <bool RNN, bool W2L, bool GEN, bool TAB>
 __global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
 rollout_kernel(RolloutArgs ra) {
     extern __shared__ u32x4v s_h2[];
@@ -1489,14 +1522,15 @@ rollout_kernel(RolloutArgs ra) {
         int64_t e = e0;
         asm volatile("" : "+s"(e));
         const EnvKey key = env_key(ra.seed, ra.env_base + e);
-        // task scales (choice([1, 1, 1, 10]) per task) as bits, the env's previous tasks
-        for (int c = 0; c < (mp + 63) / 64; ++c) {
+        // task scales (choice([1, 1, 1, 10]) per task) as bits (Philox mode), the env's
+        // previous tasks
+        for (int c = 0; c < (TAB ? 0 : (mp + 63) / 64); ++c) {
             const int j = 64 * c + lane;
             const bool ten = j < m && philox_task_scale(key, ra.episode, j) == 10.0f;
             const uint64_t bits = __ballot(ten);
             if (lane == 0) s_scl[c] = bits;
         }
-        if (ra.reset) {
+        if (!TAB && ra.reset) {
             // asg_reset (reset_kernel): prev_assigns = the first n of a Philox Fisher-Yates
             // permutation of the m tasks (choice(m, n, replace=False), mock :99-105), drawn
             // from the top; the draws are independent of the permutation, so the lanes make
@@ -1557,7 +1591,7 @@ rollout_kernel(RolloutArgs ra) {
             const int ts = ri.ts0 + (k - ri.k0);
             const bool first_sel = it < sf;
             if (!first_sel)
-                rollout_transition(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
+                rollout_transition<TAB>(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
             const int kk = k + 1;
             if (has_agent(ri, it)) {
                 const bool next_agent = has_agent(ri, it + 1);
@@ -1569,14 +1603,14 @@ rollout_kernel(RolloutArgs ra) {
                                                     (int64_t)(16 * kH2NT) * (sub + 1), 1};
                     else if (next_agent) nx = HNext{ri.Hout, kHid, 0, 1};
                     // the reset row (select_first) is stored here when the reset runs in this launch
-                    rollout_tile<RNN, W2L, GEN, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
+                    rollout_tile<RNN, W2L, GEN, TAB, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
                                                       key, s_scl, s_act, s_h2, sw, hN, hpf, nx);
                     hpf = nx.mode != 0;
                 }
                 ++pass;
             } else {
                 for (int sub = 0; sub < ntile; ++sub)
-                    rollout_tile<RNN, W2L, GEN, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
+                    rollout_tile<RNN, W2L, GEN, TAB, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
                                                        sw, hN, false, HNext{nullptr, kHid, 0, 0});
             }
 #undef RA_
@@ -1642,6 +1676,9 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.select_first = select_first;
     ra.select_last = select_last;
     ra.reset = reset;
+    const bool tab = st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
+    ra.table = tab ? st.table : nullptr;
+    if (tab && reset) return hipErrorInvalidValue;  // the table modes' reset is asg_reset (MT19937 stream)
     ra.W1T = reinterpret_cast<const float *>(packed);
     ra.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
     ra.Hin = Hin;
@@ -1665,8 +1702,15 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     const int ncu = stream_cus(s);
     const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
     const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
-#define LR_(RNN, W2L, GEN) \
-    hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN>), dim3(grid), dim3(64 * kH2Waves), plan.bytes, s, ra)
+#define LR_(RNN, W2L, GEN)                                                                                       \
+    do {                                                                                                         \
+        if (tab)                                                                                                 \
+            hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, true>), dim3(grid), dim3(64 * kH2Waves), plan.bytes, s, \
+                               ra);                                                                              \
+        else                                                                                                     \
+            hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, false>), dim3(grid), dim3(64 * kH2Waves), plan.bytes,   \
+                               s, ra);                                                                           \
+    } while (0)
 #define LR2_(RNN)                                                        \
     do {                                                                 \
         if (plan.w2l) {                                                  \

@@ -148,12 +148,20 @@ class AssignEnvBatch(MultiAgentEnv):
 
     def can_step_select(self, prefer=True, use_rnn=True):
         """Whether asg_rollout (env steps fused with the agent forward + epsilon-greedy
-        selections, up to a whole episode per launch) takes this env: Philox bump/dense
-        benefits, integer actions, 16 <= m <= 256, n <= 256, L >= 1 -- with the GRU or the
-        Linear RNNAgent.  `prefer` (kept for callers that ask whether it is also the faster
-        schedule): measured on MI355X it is wherever it applies."""
-        return (self.rng == "philox" and self.benefits in ("bump", "dense") and not self.bids_as_actions
+        selections, up to a whole episode per launch) takes this env: integer actions,
+        16 <= m <= 256, n <= 256, L >= 1 -- with the GRU or the Linear RNNAgent -- and any
+        benefit source: Philox bumps regenerated in the kernel, or the float64 table of the
+        MT19937-compat / injected modes read for the lookahead rows.  `prefer` (kept for
+        callers that ask whether it is also the faster schedule): measured on MI355X it is
+        wherever it applies."""
+        return (not self.bids_as_actions
                 and _lib.lib().asg_rollout_l2_slices(self.n, self.m, self.L, int(bool(use_rnn))) >= 0)
+
+    @property
+    def fused_reset_ok(self):
+        """asg_reset_rollout (the reset inside the episode's launch) takes the Philox modes; the
+        table modes reset with asg_reset (the MT19937 stream / the injected table)."""
+        return self.rng == "philox" and self.benefits in ("bump", "dense")
 
     def step_select(self, batch, ts, agent, hidden_state, epsilon, seed, counter, status):
         """asg_step at row ts and the fused agent forward + epsilon-greedy for row ts + 1 in
@@ -178,6 +186,9 @@ class AssignEnvBatch(MultiAgentEnv):
         h_out = args[-1]
         tail = (*args[:-1], ctypes.c_void_p(h_out.data_ptr()), float(epsilon), seed & 0xFFFFFFFFFFFFFFFF, int(counter),
                 ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(self.device))
+        if reset and not self.fused_reset_ok:
+            self.reset(batch, ts)  # table modes: asg_reset, then the episode from the reset row
+            reset, select_first = False, True
         if reset:
             self._call("asg_reset_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps),
                        int(bool(select_last)), *tail)

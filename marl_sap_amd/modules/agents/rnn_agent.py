@@ -44,8 +44,13 @@ class RNNFusedAgent(RNNAgent):
 
     def __init__(self, input_shape, args, n_out=None):
         super().__init__(input_shape, args, n_out)
-        if args.hidden_dim != 64 or not 1 <= self.n_out <= 512 or input_shape < 1:
-            raise ValueError("rnn_fused needs hidden_dim == 64 and 1 <= n_out <= 512; use agent 'rnn'")
+        if not self.supports(input_shape, args, self.n_out):
+            raise ValueError("rnn_fused needs hidden_dim == 64 and 1 <= n_out <= 512; use agent 'rnn_torch'")
+
+    @staticmethod
+    def supports(input_shape, args, n_out):
+        """Shapes the fused inference kernels take (hidden 64, 1 <= n_out <= 512, any input)."""
+        return args.hidden_dim == 64 and 1 <= int(n_out) <= 512 and int(input_shape) >= 1
 
     def _prep(self, inputs, hidden_state):
         x = inputs

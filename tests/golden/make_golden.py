@@ -25,8 +25,11 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   filtered_selectors.npz the filtered selectors' actions with their recorded random draws
   haal.npz            HAALSelector actions + every time-interval sequence's value
   replay_buffer.npz   ReplayBuffer ring inserts, counters and seeded samples
+  yaml_runner_dumps.npz  EpisodeRunner dumps of the unchanged mock_constellation_iql / _reda
+                      configs (20 x 25, agent "rnn", use_rnn False, jumpstart_mac), past both anneals
 
-  python tests/golden/make_golden.py round2   (only the last three)
+  python tests/golden/make_golden.py round2   (only the filtered / HAAL / buffer fixtures)
+  python tests/golden/make_golden.py yaml     (only yaml_runner_dumps.npz)
 """
 import os
 import sys
@@ -498,6 +501,80 @@ def gen_runner_dumps():
     np.savez_compressed(os.path.join(OUT, "runner_dumps.npz"), **out)
 
 
+def _ref_yaml_config(alg):
+    """default.yaml <- envs/mock_constellation_env.yaml <- algs/<alg>.yaml, merged as the
+    reference's main.py:59-65 / 92-104 merges them (read as data with yaml.safe_load)."""
+    import yaml
+
+    def load(rel):
+        with open(os.path.join(REF_SRC, "config", rel)) as f:
+            return yaml.safe_load(f)
+
+    def merge(d, u):
+        for k, v in u.items():
+            d[k] = merge(dict(d.get(k) or {}), v) if isinstance(v, dict) else v
+        return d
+
+    cfg = load("default.yaml")
+    merge(cfg, load("envs/mock_constellation_env.yaml"))
+    merge(cfg, load(f"algs/{alg}.yaml"))
+    return cfg
+
+
+def gen_yaml_runner_dumps():
+    """EpisodeRunner dumps of the reference's UNCHANGED mock algorithm configs
+    (mock_constellation_iql.yaml / mock_constellation_reda.yaml on
+    envs/mock_constellation_env.yaml: 20 agents x 25 tasks, T 20, L 3, agent "rnn", use_rnn
+    False, jumpstart_mac with the HAA jumpstart selector).  runner.t_env starts at 20,000, past
+    both epsilon anneals (1 -> 0 over 20,000 env steps): the jumpstart coin never picks HAA and
+    the RL selector is greedy (epsilon-greedy) / noise-free (SAP), so the episode is
+    deterministic given the seed and the agent weights recorded here."""
+    import torch as th
+    th.set_num_threads(1)
+    from runners.episode_runner import EpisodeRunner
+    from controllers import REGISTRY as mac_REGISTRY
+
+    out = {}
+    for ri, (tag, alg) in enumerate([("iql", "mock_constellation_iql"), ("reda", "mock_constellation_reda")]):
+        cfg = _ref_yaml_config(alg)
+        seed = 40 + ri
+        cfg["env_args"] = dict(cfg["env_args"], seed=seed)
+        cfg.update(batch_size_run=1, device="cpu", use_cuda=False, seed=seed, runner="episode")
+        args = SimpleNamespace(**cfg)
+        np.random.seed(seed)
+        th.manual_seed(seed)
+        logger = _Logger()
+        runner = EpisodeRunner(args, logger)
+        env = runner.get_env()
+        args.n, args.m, args.T = env.n, env.m, env.T
+        groups = {"agents": env.n}
+        mac = mac_REGISTRY[args.mac](env.scheme, groups, args)
+        g = th.Generator().manual_seed(2000 + ri)
+        with th.no_grad():
+            for p in mac.agent.parameters():
+                p.copy_(th.randn(p.shape, generator=g) * 0.3)
+        mac.update_action_selector_agent()
+        runner.setup(scheme=env.scheme, groups=groups, preprocess=env.preprocess, mac=mac)
+        runner.t_env = 20000
+        batch = runner.run(test_mode=False)
+        for k, v in batch.data.transition_data.items():
+            out[f"{tag}__{k}"] = v.numpy()
+        for k, v in mac.agent.state_dict().items():
+            out[f"{tag}__w__{k}"] = v.numpy()
+        # the runner logged (and cleared) its returns at this t_env: one env, so return_mean is it
+        rets = [v for k, v, t in logger.stats if k == "return_mean"] or list(runner.train_returns)
+        out[f"{tag}__returns"] = np.asarray(rets, dtype=np.float64)
+        out[f"{tag}__t_env"] = np.array(runner.t_env)
+        out[f"{tag}__cfg"] = np.array([env.n, env.m, env.T, int(args.env_args["L"]), seed, int(bool(args.use_rnn)),
+                                       20000])
+        out[f"{tag}__lambda"] = np.array(float(args.env_args["lambda_"]))
+        out[f"{tag}__names"] = np.array([args.mac, args.action_selector, args.agent, args.jumpstart_action_selector])
+        out[f"{tag}__sched"] = np.array([args.epsilon_start, args.epsilon_finish, args.epsilon_anneal_time,
+                                         args.jumpstart_epsilon_start, args.jumpstart_epsilon_finish,
+                                         args.jumpstart_epsilon_anneal_time], dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "yaml_runner_dumps.npz"), **out)
+
+
 def gen_real_runner_dumps():
     """EpisodeRunner + BasicMAC over RealConstellationEnv (constant benefits injected
     through env_args: sat_prox_mat + graphs), greedy epsilon-greedy and SAP selectors.
@@ -776,6 +853,9 @@ if __name__ == "__main__":
         gen_real_variants()
         gen_real_runner_dumps()
         sys.exit(0)
+    if sys.argv[1:] == ["yaml"]:  # the reference's unchanged mock algorithm configs (round 4)
+        gen_yaml_runner_dumps()
+        sys.exit(0)
     if sys.argv[1:] == ["round2"]:  # the selector / buffer fixtures added in round 2
         gen_filtered_selectors()
         gen_haal()
@@ -792,6 +872,7 @@ if __name__ == "__main__":
     gen_filtered_selectors()
     gen_haal()
     gen_replay_buffer()
+    gen_yaml_runner_dumps()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

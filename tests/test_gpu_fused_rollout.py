@@ -27,12 +27,21 @@ class _Logger:
         pass
 
 
+def _injected_table(n, m, T, seed=0):
+    """a sat_prox_mat-shaped [n, m, T] float64 table: sparse bumps plus exact zeros"""
+    r = np.random.RandomState(seed)
+    t = r.rand(n, m, T) * (r.rand(n, m, 1) > 0.6) * r.choice([1.0, 10.0], size=(1, m, 1))
+    return t
+
+
 def _rollout(n, m, T, L, E, eps, benefits, fused, episodes=2, quirks=(), protocol="episode", seed=7, use_rnn=True,
-             mac="basic_mac", **extra):
+             mac="basic_mac", rng="philox", **extra):
+    env_args = dict(n=n, m=m, T=T, L=L, lambda_=0.5, bids_as_actions=False, seed=seed, benefits=benefits)
+    if benefits == "injected":
+        env_args["sat_prox_mat"] = _injected_table(n, m, T)
     args = SimpleNamespace(
-        batch_size_run=E, env="mock_constellation_env",
-        env_args=dict(n=n, m=m, T=T, L=L, lambda_=0.5, bids_as_actions=False, seed=seed, benefits=benefits),
-        env_rng="philox", env_quirks=tuple(quirks), runner_protocol=protocol, test_nepisode=1,
+        batch_size_run=E, env="mock_constellation_env", env_args=env_args,
+        env_rng=rng, env_quirks=tuple(quirks), runner_protocol=protocol, test_nepisode=1,
         runner_log_interval=10 ** 12, n=n, m=m, T=T, hidden_dim=64, use_rnn=use_rnn, obs_last_action=False,
         obs_agent_id=False, agent_output_type="q", action_selector="epsilon_greedy", agent="rnn_fused",
         mac=mac, seed=3, epsilon_start=eps, epsilon_finish=eps, epsilon_anneal_time=1,
@@ -85,9 +94,29 @@ def test_fused_rollout_is_bit_identical(n, m, T, L, E, eps, benefits, use_rnn):
         _same(*a, *b)
 
 
+@pytest.mark.parametrize("n,m,T,L,E,eps,benefits,rng,use_rnn", [
+    (64, 64, 6, 3, 24, 0.05, "bump", "mt19937", True),     # the same-seed mode (numpy's stream per env)
+    (20, 25, 5, 3, 9, 0.2, "bump", "mt19937", False),      # the reference's default env, Linear agent
+    (64, 64, 5, 3, 10, 0.1, "injected", "philox", True),   # sat_prox_mat= (one table for every env)
+    (33, 41, 4, 2, 6, 0.3, "injected", "mt19937", False),  # odd m, injected table, MT19937 permutations
+])
+def test_fused_rollout_table_modes_bit_identical(n, m, T, L, E, eps, benefits, rng, use_rnn):
+    """The episode kernel on the handle's float64 table (MT19937 compat tables, injected
+    sat_prox_mat) instead of Philox bumps: the same batch, returns and hidden state as the
+    separate launches.  Reference: mock_constellation_env.py:22,32-37 (sat_prox_mat=), :94-114."""
+    b = _rollout(n, m, T, L, E, eps, benefits, fused=False, use_rnn=use_rnn, rng=rng)
+    for mode in ("always", "step"):
+        _same(*_rollout(n, m, T, L, E, eps, benefits, fused=mode, use_rnn=use_rnn, rng=rng), *b)
+
+
 def test_fused_rollout_quirks_and_parallel_protocol():
     kw = dict(n=32, m=32, T=5, L=3, E=6, eps=0.2, benefits="bump", quirks=("prev_assigns_zero", "parallel_terminated"),
               protocol="parallel")
+    b = _rollout(fused=False, **kw)
+    for mode in ("always", "step"):
+        _same(*_rollout(fused=mode, **kw), *b)
+    # the ParallelRunner's compat quirks: one replicated MT19937 stream (forked workers)
+    kw = dict(kw, rng="mt19937", quirks=("prev_assigns_zero", "parallel_terminated", "replicate_stream"))
     b = _rollout(fused=False, **kw)
     for mode in ("always", "step"):
         _same(*_rollout(fused=mode, **kw), *b)

@@ -40,7 +40,7 @@ def _args(n, m, T, B, seed, use_rnn, rname, sel, macname):
         jumpstart_epsilon_anneal_time=1000, jumpstart_evaluation_epsilon=1.0)
 
 
-@pytest.mark.parametrize("agent", ["rnn", "rnn_fused"])
+@pytest.mark.parametrize("agent", ["rnn", "rnn_fused", "rnn_torch"])
 @pytest.mark.parametrize("tag", TAGS)
 def test_runner_matches_reference_dump(golden, tag, agent):
     g = golden("runner_dumps")
@@ -66,3 +66,61 @@ def test_runner_matches_reference_dump(golden, tag, agent):
     np.testing.assert_allclose(td["rewards"], g[f"{tag}__rewards"], rtol=1e-5, atol=1e-6, err_msg=tag)
     np.testing.assert_allclose(np.array(runner.train_returns), g[f"{tag}__returns"], rtol=1e-5, atol=1e-6)
     assert runner.t_env == int(g[f"{tag}__t_env"])
+
+
+@pytest.mark.parametrize("tag", ["iql", "reda"])
+def test_reference_yaml_configs_land_on_the_fast_path(golden, tag):
+    """The reference's UNCHANGED mock algorithm configs -- mock_constellation_iql.yaml /
+    mock_constellation_reda.yaml on envs/mock_constellation_env.yaml (20 agents x 25 tasks,
+    T 20, L 3, agent "rnn", use_rnn False, jumpstart_mac with the HAA jumpstart selector, both
+    epsilons 1 -> 0 over 20,000 env steps) -- in the same-seed mode, with t_env past both
+    anneals: agent "rnn" resolves to the fused kernel module, the IQL episode runs as ONE
+    asg_rollout launch (fused_mode "episode"), and both batches equal the reference
+    EpisodeRunner's dumps (tests/golden/yaml_runner_dumps.npz, make_golden.py
+    gen_yaml_runner_dumps).  Reference: config/default.yaml:43, algs/mock_constellation_iql.yaml,
+    algs/mock_constellation_reda.yaml, runners/episode_runner.py:60-127."""
+    from marl_sap_amd.components import EpisodeBatch
+    from marl_sap_amd.modules.agents import RNNFusedAgent
+    g = golden("yaml_runner_dumps")
+    n, m, T, L, seed, use_rnn, t_env0 = [int(x) for x in g[f"{tag}__cfg"]]
+    macname, sel, agent, js = [str(x) for x in g[f"{tag}__names"]]
+    e0, e1, ea, j0, j1, ja = [float(x) for x in g[f"{tag}__sched"]]
+    args = SimpleNamespace(
+        batch_size_run=1, env="mock_constellation_env",
+        env_args=dict(n=n, m=m, T=T, L=L, lambda_=float(g[f"{tag}__lambda"]), bids_as_actions=False, seed=seed),
+        env_rng="mt19937", env_quirks=("prev_assigns_zero",), runner_protocol="episode", test_nepisode=50,
+        runner_log_interval=2500, n=n, m=m, T=T, agent=agent, hidden_dim=64, use_rnn=bool(use_rnn),
+        obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel, mac=macname,
+        epsilon_start=e0, epsilon_finish=e1, epsilon_anneal_time=ea, evaluation_epsilon=0.0,
+        jumpstart_action_selector=js, jumpstart_epsilon_start=j0, jumpstart_epsilon_finish=j1,
+        jumpstart_epsilon_anneal_time=ja, jumpstart_evaluation_epsilon=0.0)
+    assert agent == "rnn" and macname == "jumpstart_mac" and not use_rnn
+    runner = r_REGISTRY["gpu"](args, _Logger())
+    env = runner.get_env()
+    mac = mac_REGISTRY[macname](env.scheme, {"agents": n}, args)
+    assert isinstance(mac.agent, RNNFusedAgent)
+    sd = {k[len(tag) + 5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith(f"{tag}__w__")}
+    mac.agent.load_state_dict(sd)
+    mac.to(torch.device("cuda", 0))
+    runner.setup(env.scheme, {"agents": n}, env.preprocess, mac)
+    runner.t_env = t_env0
+    probe = EpisodeBatch(env.scheme, {"agents": n}, 1, T + 1, preprocess=env.preprocess, device=runner.device,
+                         time_major=True)
+    state = np.random.get_state()
+    with torch.no_grad():
+        mode = mac.fused_mode(env, probe, runner.t_env)
+    np.random.set_state(state)
+    assert mode == ("episode" if sel == "epsilon_greedy" else None), mode
+    batch = runner.run(test_mode=False)
+    td = {k: v.cpu().numpy() for k, v in batch.data.transition_data.items()}
+    for k in ["actions", "actions_onehot", "avail_actions", "terminated", "filled", "prev_assigns"]:
+        ref = g[f"{tag}__{k}"]
+        assert td[k].dtype == ref.dtype, k
+        np.testing.assert_array_equal(td[k], ref, err_msg=f"{tag}:{k}")
+    for k in ["obs", "beta"]:
+        np.testing.assert_allclose(td[k], g[f"{tag}__{k}"], rtol=1e-6, atol=1e-7, err_msg=f"{tag}:{k}")
+    np.testing.assert_allclose(td["rewards"], g[f"{tag}__rewards"], rtol=1e-5, atol=1e-6, err_msg=tag)
+    np.testing.assert_allclose(runner.last_returns.cpu().numpy(), g[f"{tag}__returns"], rtol=1e-5, atol=1e-6)
+    assert runner.t_env == int(g[f"{tag}__t_env"])
+    env.close()
+

@@ -47,11 +47,11 @@ DEV = torch.device("cuda", 0)
 GAP = 1e-4  # top-2 Q gap below which fp32 summation order may flip the greedy choice
 
 
-def _bench_runner(config, **over):
+def _bench_runner(config, args_over=None, **over):
     a = bench.parse(["--config", str(config)])
     for k, v in over.items():
         setattr(a, k, v)
-    args = bench.make_args(a, a.envs)
+    args = bench.make_args(a, a.envs, **(args_over or {}))
     runner = RUN["gpu"](args, bench.NullLogger())
     env = runner.get_env()
     torch.manual_seed(a.seed)
@@ -169,3 +169,45 @@ def _shape_probe(runner):
                         device=runner.device, time_major=True)
 
 
+def test_compat_mode_configs2_episode_vs_oracle():
+    """configs[2] (64 x 64, 16,384 envs, T = 20, the bench's GRU RNNAgent + epsilon-greedy 0.05)
+    in the same-seed mode: env e replays numpy's legacy MT19937 stream seeded with seed + e --
+    the throwaway __init__ table, the reset's table and its choice(m, n, False) permutation that
+    the reference draws after np.random.seed(seed + e) (mock_constellation_env.py:32-34, :99-105)
+    -- on the episode kernel (fused_mode "episode": asg_reset, then one asg_rollout launch).
+    Sampled envs are rebuilt by the C oracle from the seed alone and replayed row by row against
+    the batch (float64 table: obs / beta / rewards bit-exact); every env's invariants hold; the
+    actions are the PyTorch RNNAgent's."""
+    from oracle import oracle as ora
+    a, args, runner, env, mac = _bench_runner(2, args_over={"env_rng": "mt19937"})
+    E, n, m, T, L = a.envs, a.n, a.m, a.T, a.L
+    try:
+        with torch.no_grad():
+            assert mac.fused_mode(env, _shape_probe(runner)) == "episode"
+        b = runner.run(test_mode=False)
+        assert runner.t_env == E * T
+        prev0 = b["prev_assigns"][:, 0].reshape(E, n).clone()
+        env.sync()
+        r = _check_invariants(b, env, E, n, m, T, prev0)
+        idx = _sample(E)
+        tables, prevs = [], []
+        for e in idx:
+            oe = ora.OracleMockEnv(n, m, T, L, 0.5, mt=ora.MT(a.seed + int(e)))
+            oe.reset()
+            tables.append(oe.sat_prox_mat)
+            prevs.append(oe.prev_assigns.copy())
+        np.testing.assert_array_equal(prev0[idx].cpu().numpy(), np.stack(prevs))  # the seed's permutation
+        # the handle's tables are the seed's (the device's float64 exp vs libm's: within 1e-12
+        # relative, as tests/test_gpu_parity.py:test_mt_multi_env_streams), and the batch is
+        # their exact replay
+        dev_tab = env.export_benefits()[torch.as_tensor(idx, device=DEV)].cpu().numpy()
+        np.testing.assert_allclose(dev_tab, np.stack(tables), rtol=1e-12, atol=0)
+        td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
+        replay_and_compare(n, m, T, L, 0.5, dev_tab, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy())
+        sel = mac.action_selector
+        _check_actions(b, mac, idx, n, m, T, float(sel.epsilon), sel.seed, sel.calls - T)
+    finally:
+        env.close()
+        del runner, mac, env
+        gc.collect()
+        torch.cuda.empty_cache()
