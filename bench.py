@@ -682,6 +682,57 @@ def main():
             if r5.get("fused_ms"):
                 leg["roofline"] = fused_roofline(c4, c4.envs, r5["fused_ms"], resets_per_step=res_resets(r5))
             extra["config4"] = leg
+            # BASELINE configs[1]: 16 x 16, 4,096 envs, random policy (asg_random_actions + asg_step
+            # per step; SURVEY §8(d) B_env = 6,729 B per env-step, B_step with the fused one-hot 7,753)
+            c1 = argparse.Namespace(**vars(a))
+            for k in ("n", "m", "envs", "benefits", "selector"):
+                setattr(c1, k, CONFIGS[1][k])
+            c1.config = 1
+            r1 = run_leg(c1, dev, world, c1.envs, sk, sw)
+            sb = step_bytes(c1.n, c1.m, c1.L) * c1.envs
+            gbs = sb / (r1["kern_ms"] * 1e-3) / 1e9 if r1["kern_ms"] else None
+            pm1 = pmc_lookup("*pmc_step_kernel*.json", n=c1.n, m=c1.m, E=c1.envs, L=c1.L)
+            extra["config1"] = {
+                **leg_base(r1, sk, sw),
+                "workload": CONFIGS[1]["label"] + f"; T={a.T}, L={a.L}: asg_random_actions + asg_step per step",
+                "envs_per_gpu": c1.envs, "n": c1.n, "m": c1.m,
+                "kernels_ms": {"env_step": round(r1["kern_ms"], 4) if r1["kern_ms"] else None,
+                               "random_actions": round(r1["sel_ms"], 4) if r1["sel_ms"] else None},
+                "roofline": {"bound": "hbm", "kernel": "asg::step_kernel", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                             "achieved": round(gbs, 1) if gbs else None,
+                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                             "bytes_per_launch": sb, "b_env_survey_per_launch": (c1.n * c1.m * (4 * c1.L + 13)
+                                                                                 + 20 * c1.n + 9) * c1.envs,
+                             "traffic": pm1.get("hbm_bytes_per_launch") if pm1 else None,
+                             "note": "B_step = SURVEY §8(d)'s B_env + the fused int64 one-hot (8nm) - the table read "
+                                     "(bumps regenerated, 4nm); launch-bound at this size: 4,096 envs x 7.75 KB "
+                                     "= 32 MB per launch"}}
+            # the same-seed mode (rng="mt19937": env e replays numpy's legacy stream seeded with
+            # seed + e, the reference's draws) on the episode kernel: configs[2] with the handle's
+            # float64 tables read for the lookahead rows (and the reset's MT19937 table draws)
+            rc = run_leg(a, dev, world, E, sk, sw, env_rng="mt19937")
+            leg = {**leg_base(rc, sk, sw),
+                   "workload": "configs[2] in the same-seed mode: rng mt19937 (per env np.random.seed(seed + env)), "
+                               "float64 benefit tables; asg_reset (MT19937 table draws) + the episode kernel",
+                   "kernels_ms": {"fused_rollout_per_step": round(rc["fused_ms"], 4) if rc.get("fused_ms") else None,
+                                  "fused_note": "the episode launches of the window, their asg_reset (table draws) "
+                                                "included"}}
+            if rc.get("fused_ms"):
+                tb = 8 * a.n * a.m * E  # one float64 table slice read per env-step (+ its write at the reset)
+                roof = fused_roofline(a, E, rc["fused_ms"], resets_per_step=res_resets(rc))
+                per = roof["bytes_per_launch"] + 2 * tb
+                roof.update({"bytes_per_launch": per, "achieved": round(per / (rc["fused_ms"] * 1e-3) / 1e9, 1),
+                             "frac": round(per / (rc["fused_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "traffic": None, "kernel": "asg::rollout_kernel<TAB> (+ asg_reset's table draws)",
+                             "per_launch_note": "the Philox accounting + 8nm per env-step of table read (one new "
+                                                "float64 slice per step) + 8nm of table write (the reset's T slices "
+                                                "over T steps)"})
+                roof.pop("traffic_pmc", None)
+                roof.pop("traffic_over_algorithmic", None)
+                roof.pop("traffic_note", None)
+                roof.pop("issue", None)
+                leg["roofline"] = roof
+            extra["compat"] = leg
 
     if a.selector == "random":
         ra = None

@@ -215,12 +215,6 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
 int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                    double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
                    float *col_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
-/* Problems per wave of asg_sap_select's solver (process-wide; identical outputs for every
- * setting, only the schedule differs): 0 = one problem per wave over a static grid, 1..3 =
- * a persistent grid whose waves keep that many problems in flight with their augmenting-path
- * steps interleaved.  Default 2 (environment ASG_SAP_SLOTS overrides it at load).  A value
- * outside 0..3 only queries.  Returns the previous setting. */
-int asg_sap_slots(int slots);
 
 /* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
  * per row, with probability epsilon a uniformly random available action, else the first

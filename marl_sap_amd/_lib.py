@@ -34,7 +34,7 @@ _DTYPES = {torch.float32: ASG_F32, torch.float64: ASG_F64, torch.int64: ASG_I64,
 EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "asg_set_stream",
            "asg_reset", "asg_step", "asg_random_actions", "asg_sync_status", "asg_set_benefits",
            "asg_export_benefits", "asg_export_bump_params", "asg_export_prev_assigns", "asg_get_returns", "asg_get_step",
-           "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_sap_select", "asg_sap_slots", "asg_epsilon_greedy",
+           "asg_advance_stream", "asg_beta_hat", "asg_lsa_batched", "asg_haa_select", "asg_sap_select", "asg_epsilon_greedy",
            "asg_rnn_agent_packed_size", "asg_rnn_agent_mfma_mode", "asg_rnn_agent_mode", "asg_rnn_agent_pack", "asg_rnn_agent_forward",
            "asg_rnn_agent_select", "asg_real_create", "asg_real_destroy", "asg_real_set_stream",
            "asg_real_set_benefits", "asg_real_set_initial_assignments", "asg_real_reset", "asg_real_step", "asg_real_sync_status",
@@ -118,7 +118,6 @@ def lib():
         L.asg_haa_select.argtypes = [vp, i64p, vp, i64p, i64, i32, i32, vp, dbl, vp, vp, vp]
         L.asg_sap_select.argtypes = [vp, i64p, i64, i32, i32, dbl, ctypes.c_uint64, ctypes.c_uint64, i64, vp, vp, vp,
                                      vp]
-        L.asg_sap_slots.argtypes = [i32]
         L.asg_epsilon_greedy.argtypes = [vp, i64p, vp, i64p, i64, i32, i32, dbl, ctypes.c_uint64, ctypes.c_uint64,
                                          i64, vp, i64p, vp, vp]
         L.asg_rnn_agent_packed_size.argtypes = [i32, i32, i32, i32]

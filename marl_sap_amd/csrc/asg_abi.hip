@@ -371,8 +371,6 @@ int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n,
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select");
 }
 
-int asg_sap_slots(int slots) { return asg::sap_set_slots(slots); }
-
 int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
                        uint64_t counter, int64_t env_index_base, int64_t *out, const int64_t out_strides[2],

@@ -4,10 +4,6 @@
 // (L2-resident for the row sweeps).
 // Reference call sites: sap_selectors.py:32,90 (SAP selectors on Q-values),
 // non_rl_selectors.py:36-47 (HAA: beta_hat + LSA), mock_constellation_env.py:228-274.
-#include <stdlib.h>
-
-#include <atomic>
-#include <mutex>
 #include <type_traits>
 
 #include "asg_device.h"
@@ -273,6 +269,9 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
     if (lane == 0 && status_out) status_out[b] = status;
 }
 
+#ifndef ASG_SAP_PIN
+#define ASG_SAP_PIN 0
+#endif
 template <bool kCount>
 __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
@@ -280,214 +279,21 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
                                                         int32_t *steps_out, int64_t B) {
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
+#if ASG_SAP_PIN
+    RegColPin<32> rc;  // the column in v[32 .. 95]: one indexed move per row read
+#else
     RegCostF32 rc;
+#endif
     int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
     int c4r[1] = {-1};
     int nsteps = 0;
-    if (status == ASG_OK) status = lsa_solve_reg64<RegCostF32, kCount>(rc, n, m, c4r, &nsteps);
+    if (status == ASG_OK) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
     sap_emit<kCount>(b, status, c4r[0], nsteps, n, m, col_out, status_out, steps_out);
-}
-
-// ------------------------------------------------------------------------------------
-// The same selection with S problems per wave (lsa_wave.h "several problems per wave"): a
-// persistent grid whose waves keep S problems in flight, their augmenting-path steps
-// interleaved; a slot whose problem is solved takes the next one from a ticket counter
-// (problems gw + W s first, then W S + ticket).  Once the tickets run out the remaining
-// problems of a wave finish one at a time.  Decisions are lsa_solve_reg64's, problem by
-// problem: bit-identical outputs.
-// ------------------------------------------------------------------------------------
-#ifndef ASG_SAP_SLOTS
-#define ASG_SAP_SLOTS 2
-#endif
-template <int S>
-struct SapMultiWaves {
-    static constexpr int value = S == 1 ? 5 : (S == 2 ? 3 : 2);
-};
-struct SapArgs {
-    const float *q;
-    int64_t q0, q1, q2;
-    int n, m;
-    float epsilon;
-    uint64_t seed;
-    uint32_t counter;
-    int64_t env_base;
-    float *col_out;
-    int32_t *status_out, *steps_out;
-    int64_t B;
-    int *ticket;
-};
-// stage problem b into a slot: true when it is ready to solve; an invalid problem is emitted
-// at once (false)
-template <bool kCount, class RC>
-__device__ __forceinline__ bool sap_slot_stage(const SapArgs &a, RC &C, LsaLane &L, LsaScal &Sc, int64_t b) {
-    const int st = sap_stage(a.q, a.q0, a.q1, a.q2, a.n, a.m, a.epsilon, a.seed, a.counter, a.env_base, b, C);
-    if (st == ASG_OK) {
-        lsa_problem_begin(L, Sc, a.m);
-        return true;
-    }
-    sap_emit<kCount>(b, st, -1, 0, a.n, a.m, a.col_out, a.status_out, a.steps_out);
-    return false;
-}
-// the slot's problem to the end, alone
-template <bool kCount, class RC>
-__device__ __forceinline__ void sap_slot_finish(const SapArgs &a, RC &C, LsaLane &L, LsaScal &Sc, int64_t p) {
-    if (p >= a.B) return;
-    while (true) {
-        const float key = lsa_relax(C, L, Sc);
-        const float kmin = wave_min_f32_nonan(key);
-        lsa_pick(L, Sc, key, kmin);
-        if (Sc.ncand != 1) lsa_tie(L, Sc);
-        if (lsa_advance<kCount>(L, Sc)) continue;
-        const int r = lsa_row_end(L, Sc, a.n, a.m);
-        if (r == ASG_OK) continue;
-        sap_emit<kCount>(p, r == 1 ? ASG_OK : r, L.c4r, Sc.steps, a.n, a.m, a.col_out, a.status_out, a.steps_out);
-        return;
-    }
-}
-
-template <int S, bool kCount>
-__global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(SapMultiWaves<S>::value)))
-sap_multi_kernel(SapArgs a) {
-    const int64_t W = (int64_t)gridDim.x * kLsaWpb;
-    const int64_t gw = (int64_t)blockIdx.x * kLsaWpb + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // Rounds of S problems: the first round's problems are gw S .. gw S + S - 1, every later
-    // round's are S consecutive tickets (past the first W S).  Per round, the slots are
-    // staged, solved interleaved until one of them is done, and the rest finish one at a time.
-    // The slots are named variables declared inside the round, expanded per slot by SAP_SLOTS
-    // (no arrays of them, no lambdas capturing them, no column live across rounds: the
-    // dynamically indexed register columns must be promoted to registers).
-    int64_t base = gw * S;
-#define SAP_SLOTS(X) \
-    X(0)                 \
-    if constexpr (S > 1) { X(1) } \
-    if constexpr (S > 2) { X(2) }
-    while (base < a.B) {
-        // columns pinned to disjoint register ranges (RegColPin), the rest of the state below
-        RegColPin<S == 1 ? 32 : (S == 2 ? 40 : 64)> C0;
-        RegColPin<S == 2 ? 104 : 128> C1;
-        RegColPin<192> C2;
-        LsaLane L0, L1, L2;
-        LsaScal Sc0, Sc1, Sc2;
-        bool v0 = false, v1 = false, v2 = false;  // slot holds an unsolved problem
-#define SAP_STAGE(k) \
-    if (base + k < a.B) v##k = sap_slot_stage<kCount>(a, C##k, L##k, Sc##k, base + k);
-        SAP_SLOTS(SAP_STAGE)
-        bool all = v0;
-        if constexpr (S > 1) all = all && v1;
-        if constexpr (S > 2) all = all && v2;
-        while (all) {
-            float key[3], kmin[3];
-#define SAP_RELAX(k) key[k] = lsa_relax(C##k, L##k, Sc##k);
-            SAP_SLOTS(SAP_RELAX)
-            if constexpr (S == 1) {
-                kmin[0] = wave_min_f32_nonan(key[0]);
-            } else if constexpr (S == 2) {
-                const float k2[2] = {key[0], key[1]};
-                float m2[2];
-                wave_min_multi_f32<2>(k2, m2);
-                kmin[0] = m2[0];
-                kmin[1] = m2[1];
-            } else {
-                const float k3[3] = {key[0], key[1], key[2]};
-                float m3[3];
-                wave_min_multi_f32<3>(k3, m3);
-                kmin[0] = m3[0];
-                kmin[1] = m3[1];
-                kmin[2] = m3[2];
-            }
-#define SAP_PICK(k) lsa_pick(L##k, Sc##k, key[k], kmin[k]);
-            SAP_SLOTS(SAP_PICK)
-#define SAP_TIE(k) \
-    if (Sc##k.ncand != 1) lsa_tie(L##k, Sc##k);
-            SAP_SLOTS(SAP_TIE)
-            bool c0 = true, c1 = true, c2 = true;
-#define SAP_ADV(k) c##k = lsa_advance<kCount>(L##k, Sc##k);
-            SAP_SLOTS(SAP_ADV)
-            if (c0 && c1 && c2) continue;
-#define SAP_END(k)                                                                                               \
-    if (!c##k) {                                                                                                 \
-        const int r = lsa_row_end(L##k, Sc##k, a.n, a.m);                                                       \
-        if (r != ASG_OK) {                                                                                       \
-            sap_emit<kCount>(base + k, r == 1 ? ASG_OK : r, L##k.c4r, Sc##k.steps, a.n, a.m, a.col_out,           \
-                             a.status_out, a.steps_out);                                                         \
-            v##k = false;                                                                                        \
-            all = false;                                                                                         \
-        }                                                                                                        \
-    }
-            SAP_SLOTS(SAP_END)
-        }
-        // the round's unfinished problems, one at a time
-#define SAP_FIN(k) \
-    if (v##k) sap_slot_finish<kCount>(a, C##k, L##k, Sc##k, base + k);
-        SAP_SLOTS(SAP_FIN)
-        // the next round: S tickets in one atomic
-        int t = 0;
-        if ((threadIdx.x & (kWave - 1)) == 0) t = atomicAdd(a.ticket, S);
-        base = W * S + (int64_t)__builtin_amdgcn_readfirstlane(t);
-    }
-#undef SAP_FIN
-#undef SAP_END
-#undef SAP_ADV
-#undef SAP_TIE
-#undef SAP_PICK
-#undef SAP_RELAX
-#undef SAP_STAGE
-#undef SAP_SLOTS
-}
-
-// the ticket counter of sap_multi_kernel, one per device (zeroed on the stream before each
-// launch; calls on one device are stream-ordered through it)
-static int *sap_ticket_buffer() {
-    static std::mutex mu;
-    static int *bufs[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    if (!bufs[dev] && hipMalloc(reinterpret_cast<void **>(&bufs[dev]), 256) != hipSuccess) bufs[dev] = nullptr;
-    return bufs[dev];
-}
-
-// 0: the one-problem-per-wave kernel; 1..3: sap_multi_kernel with that many problems per wave
-static std::atomic<int> &sap_slots_var() {
-    static std::atomic<int> v([] {
-        const char *e = getenv("ASG_SAP_SLOTS");
-        const int x = e ? atoi(e) : ASG_SAP_SLOTS;
-        return x < 0 || x > 3 ? ASG_SAP_SLOTS : x;
-    }());
-    return v;
-}
-static int sap_slots() { return sap_slots_var().load(); }
-int sap_set_slots(int slots) {
-    if (slots < 0 || slots > 3) return sap_slots();
-    return sap_slots_var().exchange(slots);
 }
 
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
                              int32_t *steps_out, hipStream_t s) {
-    const int S = sap_slots();
-    if (S > 0) {
-        int *ticket = sap_ticket_buffer();
-        if (!ticket) return hipErrorOutOfMemory;
-        hipError_t e = hipMemsetAsync(ticket, 0, sizeof(int), s);
-        if (e != hipSuccess) return e;
-        const int wpc = 4 * (S == 1 ? 5 : (S == 2 ? 3 : 2)) / kLsaWpb;  // workgroups per CU
-        const int64_t need = (B + (int64_t)S * kLsaWpb - 1) / ((int64_t)S * kLsaWpb);
-        const int64_t cap = (int64_t)stream_cus(s) * wpc;
-        const dim3 grid((unsigned)(need < cap ? need : cap));
-        const SapArgs sa{q, qs[0], qs[1], qs[2], n, m, epsilon, seed, counter, env_base, col_out, status_out, steps_out,
-                         B, ticket};
-#define LM_(SS, KC) hipLaunchKernelGGL((sap_multi_kernel<SS, KC>), grid, dim3(64 * kLsaWpb), 0, s, sa)
-        if (S == 1) {
-            if (steps_out) LM_(1, true); else LM_(1, false);
-        } else if (S == 2) {
-            if (steps_out) LM_(2, true); else LM_(2, false);
-        } else {
-            if (steps_out) LM_(3, true); else LM_(3, false);
-        }
-#undef LM_
-        return hipGetLastError();
-    }
     if (steps_out)
         hipLaunchKernelGGL(sap_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n,
                            m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);

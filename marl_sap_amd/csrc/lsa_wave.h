@@ -433,219 +433,6 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 #endif
 }
 
-// ------------------------------------------------------------------------------------------
-// Several problems per wave, their augmenting-path steps interleaved (lsa_solve_reg64's
-// algorithm and decisions, problem by problem).  One augmenting-path step is a dependent
-// chain -- row read, three float64 adds, a float32 key, a six-step DPP minimum, ballot, bit
-// scan, readlanes, the owner row -- through which one problem per wave leaves most issue
-// cycles idle.  S problems per wave (each lane holds column l of every one) make S
-// independent chains in one instruction stream: the compiler interleaves their straight-line
-// steps, and one DPP block folds the S minima with the hazard gaps filled by the other
-// problems' steps instead of s_nops.  Per problem the state is LsaLane (per lane) + LsaScal
-// (wave-uniform).
-// ------------------------------------------------------------------------------------------
-// (the working column itself is kept beside it, as its own variable: inside a larger struct its
-// dynamically indexed reads would keep the struct in scratch)
-struct LsaLane {
-    double v, u, spc;
-    int r4c, path, c4r, pos;
-};
-struct LsaScal {
-    uint64_t rem, cm;  // columns still in `remaining`; the step's candidate ballot
-    uint32_t lo_lo, lo_hi;  // the step's minimum (lowest) as two words
-    uint32_t minv_lo, minv_hi;
-    int cur, i, nrem, jsel, psel, ncand, steps;
-};
-
-// S wave minima of never-NaN float32 keys in one interleaved DPP block (S = 1: the single
-// block of wave_min_f32_nonan); results wave-uniform
-template <int S>
-__device__ __forceinline__ void wave_min_multi_f32(const float (&x0)[S], float (&out)[S]) {
-    if constexpr (S == 1) {
-        out[0] = wave_min_f32_nonan(x0[0]);
-    } else if constexpr (S == 2) {
-        float a, b;
-        // VALU write -> DPP read needs 2 wait states: the other problem's op + s_nop 0
-        asm("s_nop 1\n\t"
-            "v_min_f32_dpp %0, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-            "s_nop 0\n\t"
-            "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-            "s_nop 0\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "s_nop 0\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "s_nop 0\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa\n\t"
-            "s_nop 0\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc"
-            : "=&v"(a), "=&v"(b)
-            : "v"(x0[0]), "v"(x0[1]));
-        out[0] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 63));
-        out[1] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b), 63));
-    } else {
-        static_assert(S == 3, "1 to 3 problems per wave");
-        float a, b, c;
-        // three independent chains: each op's source was written two instructions earlier
-        asm("s_nop 1\n\t"
-            "v_min_f32_dpp %0, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %2, %5, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %2, %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %2, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %2, %2, %2 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa\n\t"
-            "v_min_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa\n\t"
-            "v_min_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc\n\t"
-            "v_min_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc\n\t"
-            "v_min_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc"
-            : "=&v"(a), "=&v"(b), "=&v"(c)
-            : "v"(x0[0]), "v"(x0[1]), "v"(x0[2]));
-        out[0] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a), 63));
-        out[1] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, b), 63));
-        out[2] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, c), 63));
-    }
-}
-
-// the first row of the problem's current row loop (scipy: spc = inf, remaining = all columns
-// in reverse order, minv = 0, i = cur)
-__device__ __forceinline__ void lsa_row_begin(LsaLane &L, LsaScal &Sc, int nc) {
-    const int lane = threadIdx.x & (kWave - 1);
-    L.spc = __builtin_inf();
-    L.pos = (lane < nc) ? (nc - 1 - lane) : -1;  // remaining[it] = nc - it - 1
-    Sc.rem = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
-    Sc.nrem = nc;
-    Sc.minv_lo = 0u;
-    Sc.minv_hi = 0u;
-    Sc.i = Sc.cur;
-}
-__device__ __forceinline__ void lsa_problem_begin(LsaLane &L, LsaScal &Sc, int nc) {
-    L.v = 0.0;
-    L.u = 0.0;
-    L.r4c = -1;
-    L.path = -1;
-    L.c4r = -1;
-    Sc.cur = 0;
-    Sc.steps = 0;
-    lsa_row_begin(L, Sc, nc);
-}
-
-constexpr uint32_t kLsaKeyOut = 0x7fc00000u;  // key of a column out of `remaining`: a quiet NaN
-
-// step, part 1: relax the lane's column against row i, return its key
-template <class Acc>
-__device__ __forceinline__ float lsa_relax(const Acc &acc, LsaLane &L, LsaScal &Sc) {
-    const int i = __builtin_amdgcn_readfirstlane(Sc.i);
-    Sc.i = i;
-    const uint64_t ub = __builtin_bit_cast(uint64_t, L.u);
-    const double ui = dbl_of(__builtin_amdgcn_readlane((int)(uint32_t)ub, i),
-                             __builtin_amdgcn_readlane((int)(uint32_t)(ub >> 32), i));
-    const bool remb = __builtin_amdgcn_inverse_ballot_w64(Sc.rem);
-    const double r = ((dbl_of(Sc.minv_lo, Sc.minv_hi) + acc.col(i)) - ui) - L.v;
-    const bool upd = remb && r < L.spc;
-    L.spc = upd ? r : L.spc;
-    L.path = upd ? i : L.path;
-    return remb ? (float)L.spc : __builtin_bit_cast(float, kLsaKeyOut);
-}
-// step, part 2: the candidates at the minimum key; the first one is the selection when it is
-// the only one (cm == 0 -- a NaN cost mid-solve -- is given defined indices, then the step
-// ends the problem as invalid)
-__device__ __forceinline__ void lsa_pick(LsaLane &L, LsaScal &Sc, float key, float kmin) {
-    const uint64_t cm = __ballot(key == kmin);
-    int nc;
-    asm("s_bcnt1_i32_b64 %0, %1" : "=s"(nc) : "s"(cm));
-    Sc.cm = cm;
-    Sc.ncand = nc;
-    const int j = sff1(cm) & 63;  // cm == 0: lane 63, any lane would do
-    const uint64_t sb = __builtin_bit_cast(uint64_t, L.spc);
-    Sc.jsel = j;
-    Sc.lo_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, j);
-    Sc.lo_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), j);
-    Sc.psel = __builtin_amdgcn_readlane(L.pos, j);
-}
-// step, part 2b (several candidates): exact float64 ties checked against the first
-// candidate, else the exact minimum; scipy's tie rule by a max-reduced key
-__device__ __forceinline__ void lsa_tie(LsaLane &L, LsaScal &Sc) {
-    const bool remb = __builtin_amdgcn_inverse_ballot_w64(Sc.rem);
-    double lowest0 = dbl_of(Sc.lo_lo, Sc.lo_hi);
-    uint64_t cand = Sc.cm;
-    if ((__ballot(L.spc != lowest0) & Sc.cm) != 0) {
-        const double lo = remb ? L.spc : __builtin_inf();
-        const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));
-        Sc.lo_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
-        Sc.lo_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
-        lowest0 = dbl_of(Sc.lo_lo, Sc.lo_hi);
-        cand = __ballot(L.spc == lowest0) & Sc.rem;
-    }
-    const bool cb = __builtin_amdgcn_inverse_ballot_w64(cand);
-    const uint32_t k = (L.r4c == -1) ? (0x80000000u | (uint32_t)L.pos) : ((1u << 30) - (uint32_t)L.pos);
-    const uint32_t tk = wave_max_u32_bcast(cb ? k : 0u);
-    Sc.psel = (tk >> 31) ? (int)(tk & 0x7fffffffu) : (int)((1u << 30) - tk);
-    const uint64_t own = __ballot(L.pos == Sc.psel) & Sc.rem;  // positions are distinct
-    Sc.jsel = sff1(own) & 63;
-    if (Sc.ncand == 0) Sc.lo_hi = 0x7ff00000u;  // leaves the row loop; reported as invalid
-}
-// step, part 3: column jsel leaves `remaining` (swap-with-last positions), minv = lowest, the
-// next row is jsel's owner.  Returns whether the row's path continues (owner assigned and
-// lowest finite)
-template <bool kCount>
-__device__ __forceinline__ bool lsa_advance(LsaLane &L, LsaScal &Sc) {
-    if (kCount) ++Sc.steps;
-    const int last = Sc.nrem - 1;
-    L.pos = L.pos == last ? Sc.psel : L.pos;  // a removed column keeps a stale position
-    uint64_t rem = Sc.rem;
-    asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(__builtin_amdgcn_readfirstlane(Sc.jsel)) : "scc");
-    Sc.rem = rem;
-    --Sc.nrem;
-    Sc.minv_lo = Sc.lo_lo;
-    Sc.minv_hi = Sc.lo_hi;
-    Sc.i = __builtin_amdgcn_readlane(L.r4c, Sc.jsel);
-    return __builtin_elementwise_min((uint32_t)(Sc.i + 1), Sc.lo_hi ^ 0x7ff00000u) != 0u;
-}
-// the row's path has ended: status (invalid / infeasible), else the dual update and the
-// augmentation, then the next row.  Returns ASG_OK while rows remain, 1 once the problem is
-// solved, or the error status
-__device__ __forceinline__ int lsa_row_end(LsaLane &L, LsaScal &Sc, int nr, int nc) {
-    if (Sc.ncand == 0) return ASG_E_LSA_INVALID;
-    if (Sc.lo_hi == 0x7ff00000u) return ASG_E_LSA_INFEASIBLE;
-    const int lane = threadIdx.x & (kWave - 1);
-    const double minv = dbl_of(Sc.lo_lo, Sc.lo_hi);
-    const int cur = Sc.cur;
-    const int jm = L.c4r;
-    const double spc_j = __shfl(L.spc, jm & 63, kWave);
-    const bool sc_j = jm >= 0 && ((Sc.rem >> (jm & 63)) & 1ull) == 0;
-    if (lane < nr) {
-        if (lane == cur) L.u += minv;
-        else if (sc_j) L.u += minv - spc_j;
-    }
-    if (lane < nc && ((Sc.rem >> lane) & 1ull) == 0) L.v -= minv - L.spc;
-    int j = Sc.jsel;
-    while (true) {
-        const int pi = __builtin_amdgcn_readlane(L.path, j);
-        L.r4c = (lane == j) ? pi : L.r4c;
-        const int t = __builtin_amdgcn_readlane(L.c4r, pi);
-        L.c4r = (lane == pi) ? j : L.c4r;
-        j = t;
-        if (pi == cur) break;
-    }
-    Sc.cur = cur + 1;
-    if (Sc.cur == nr) return 1;
-    lsa_row_begin(L, Sc, nc);
-    return ASG_OK;
-}
-
 // Stage C (input [nr0][nc0], strides in elements) into dst as scipy's working matrix:
 // transposed when nr0 > nc0, negated for maximize.  Returns ASG_E_LSA_INVALID (wave
 // uniform) when an entry is NaN or -inf after the sign flip.

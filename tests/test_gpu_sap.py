@@ -114,32 +114,3 @@ def _sap_raw(q, eps, seed, counter, base=0):
                                          p(out), p(st), p(steps), _lib.stream_ptr(DEV)))
     torch.cuda.synchronize()
     return out, st, steps
-
-
-@pytest.mark.parametrize("B,n,m,eps", [(16384, 64, 64, 0.05), (3001, 64, 64, 0.3), (700, 20, 25, 0.5),
-                                       (5, 64, 64, 0.2), (2048, 33, 47, 0.0), (1024, 64, 64, 1.0)])
-def test_multi_problem_waves_equal_one_problem_waves(B, n, m, eps):
-    """asg_sap_slots 1..3 -- persistent waves keeping 1..3 problems in flight with their
-    augmenting-path steps interleaved, refilled from a ticket counter -- reproduce the
-    one-problem-per-wave kernel bit for bit: assignments, status and the per-env count of
-    augmenting-path steps (so every problem ran scipy's exact sequence of steps).  Also an
-    invalid env in the middle of a batch."""
-    from marl_sap_amd import _lib
-    rng = np.random.RandomState(B + n + m)
-    q = torch.as_tensor(sap_like_q(rng, B, n, m), device=DEV)
-    if B > 100:
-        q[B // 2, 3, 1] = float("nan")
-    L = _lib.lib()
-    prev = L.asg_sap_slots(0)
-    try:
-        ref = _sap_raw(q, eps, 5, 9)
-        assert int((ref[1] != 0).sum()) == (1 if B > 100 else 0)
-        assert int(ref[2].sum()) > 0
-        for s in (1, 2, 3):
-            L.asg_sap_slots(s)
-            got = _sap_raw(q, eps, 5, 9)
-            for a, b in zip(ref, got):
-                assert torch.equal(a, b), s
-    finally:
-        L.asg_sap_slots(prev)
-    assert L.asg_sap_slots(-1) == prev
