@@ -4,6 +4,8 @@
 // (L2-resident for the row sweeps).
 // Reference call sites: sap_selectors.py:32,90 (SAP selectors on Q-values),
 // non_rl_selectors.py:36-47 (HAA: beta_hat + LSA), mock_constellation_env.py:228-274.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "asg_device.h"
@@ -291,15 +293,27 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
     sap_emit<kCount>(b, status, c4r[0], nsteps, n, m, col_out, status_out, steps_out);
 }
 
+// occupancy experiments: ASG_SAP_LDS_PAD=<bytes> of unused dynamic LDS per 4-wave workgroup
+// caps the resident waves (e.g. 81920: 2 workgroups = 2 waves per SIMD) -- the rollout
+// kernel's residency, to price an LSA fused into it; 0 (default) = none
+static size_t sap_lds_pad() {
+    static const size_t v = [] {
+        const char *e = getenv("ASG_SAP_LDS_PAD");
+        return e ? (size_t)atol(e) : (size_t)0;
+    }();
+    return v;
+}
+
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
                              int32_t *steps_out, hipStream_t s) {
+    const size_t pad = sap_lds_pad();
     if (steps_out)
-        hipLaunchKernelGGL(sap_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n,
-                           m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
+        hipLaunchKernelGGL(sap_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2],
+                           n, m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
     else
-        hipLaunchKernelGGL(sap_select_kernel<false>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n,
-                           m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
+        hipLaunchKernelGGL(sap_select_kernel<false>, lsa_reg_grid(B), dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2],
+                           n, m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
     return hipGetLastError();
 }
 
