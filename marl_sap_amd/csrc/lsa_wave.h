@@ -315,10 +315,130 @@ __device__ __forceinline__ int sff1(uint64_t x) {
     return r;
 }
 
+// index of the highest set bit of a wave-uniform 64-bit mask (s_flbit counts from the MSB;
+// -1 for an empty mask)
+__device__ __forceinline__ int sfl1(uint64_t x) {
+    int r;
+    asm("s_flbit_i32_b64 %0, %1" : "=s"(r) : "s"(x));
+    return 63 - r;  // an empty mask: 64, lane 0 once masked
+}
+
+#ifndef ASG_LSA_COLAT
+#define ASG_LSA_COLAT 0
+#endif
+#if ASG_LSA_COLAT
+// lsa_solve_reg64 with scipy's `remaining` list held as it is -- lane `it` holds the column at
+// position it (colat), the swap-with-last removal one readlane + one writelane -- instead of
+// each column's position.  The tie rule then needs no reduction: the positions whose column is
+// a candidate are one ballot (a per-lane shift of the uniform candidate mask), and the largest
+// (an unassigned candidate exists) or smallest position is one s_flbit / s_ff1 of it; the
+// assigned columns are a scalar mask.  Same decisions as lsa_solve_reg64.
+template <class Acc, bool kCount = false>
+__device__ int lsa_solve_reg64_colat(const Acc &acc, int nr, int nc, int (&col4row)[1], int *steps) {
+    int nsteps = 0;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t colmask = nc >= 64 ? ~0ull : ((1ull << nc) - 1ull);
+    const float kOutF = __builtin_bit_cast(float, 0x7fc00000u);
+    double v = 0.0, u = 0.0;
+    int r4c = -1, path = -1, c4r = -1;
+    uint64_t asg = 0;  // columns assigned to a row (r4c != -1)
+    for (int cur = 0; cur < nr; ++cur) {
+        double spc = __builtin_inf();
+        int colat = (lane < nc) ? (nc - 1 - lane) : 0;  // remaining[it] = nc - it - 1
+        uint64_t rem = colmask;                          // columns still in `remaining`
+        uint64_t posmask = colmask;  // positions 0 .. nrem - 1 are `remaining`; past them stale copies
+        int nrem = nc;
+        double minv = 0.0;
+        int i = cur, jsel, ncand;
+        uint32_t lowest_hi;
+        do {
+            i = __builtin_amdgcn_readfirstlane(i);
+            if (kCount) ++nsteps;
+            const double ui = __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                                              (int)(uint32_t)__builtin_bit_cast(uint64_t, u), i)) |
+                                                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                                                  (int)(uint32_t)(__builtin_bit_cast(uint64_t, u) >> 32), i)
+                                                              << 32));
+            const bool remb = __builtin_amdgcn_inverse_ballot_w64(rem);
+            const double r = ((minv + acc.col(i)) - ui) - v;
+            const bool upd = remb && r < spc;
+            spc = upd ? r : spc;
+            path = upd ? i : path;
+            const float key = remb ? (float)spc : kOutF;
+            const float kmin = wave_min_f32_nonan(key);
+            const uint64_t cm = __ballot(key == kmin);
+            asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
+            const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
+            jsel = sff1(cm);
+            uint32_t lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
+            lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
+            // the first candidate's position (the selection when it is the only one); the tie
+            // branch below overrides it -- no else branch for the structurizer to flag
+            int psel = sff1(__ballot(colat == jsel) & posmask);
+            if (ncand != 1) {
+                double lowest0 = dbl_of(lowest_lo, lowest_hi);
+                uint64_t cand = cm;
+                if ((__ballot(spc != lowest0) & cm) != 0) {
+                    const double lo = remb ? spc : __builtin_inf();
+                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(lo));
+                    lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
+                    lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
+                    lowest0 = dbl_of(lowest_lo, lowest_hi);
+                    cand = __ballot(spc == lowest0) & rem;
+                }
+                // scipy's tie rule: the unassigned candidate of largest position, else the
+                // candidate of smallest position
+                const uint64_t un = cand & ~asg;
+                const uint64_t S = un ? un : cand;
+                const uint64_t at = __ballot(((S >> colat) & 1ull) != 0) & posmask;
+                psel = un ? sfl1(at) : sff1(at);
+                jsel = __builtin_amdgcn_readlane(colat, psel) & 63;
+                if (ncand == 0) lowest_hi = 0x7ff00000u;
+            }
+            // remaining[psel] = remaining[--num_remaining]
+            const int moved = __builtin_amdgcn_readlane(colat, nrem - 1);
+            // the lane select in M0 (an SGPR data operand takes gfx9's one constant-bus read)
+            asm("v_writelane_b32 %0, %1, m0" : "+v"(colat) : "s"(moved), "{m0}"(psel & 63));
+            asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(jsel) : "scc");
+            --nrem;
+            asm("s_bitset0_b64 %0, %1" : "+s"(posmask) : "s"(nrem) : "scc");
+            minv = dbl_of(lowest_lo, lowest_hi);
+            i = __builtin_amdgcn_readlane(r4c, jsel);
+        } while (__builtin_elementwise_min((uint32_t)(i + 1), lowest_hi ^ 0x7ff00000u) != 0u);
+        if (ncand == 0) return ASG_E_LSA_INVALID;
+        if (lowest_hi == 0x7ff00000u) return ASG_E_LSA_INFEASIBLE;
+        const int sink = jsel;
+        asm("s_bitset1_b64 %0, %1" : "+s"(asg) : "s"(sink) : "scc");  // the sink joins the assigned columns
+        const int jm = c4r;
+        const double spc_j = __shfl(spc, jm & 63, kWave);
+        const bool sc_j = jm >= 0 && ((rem >> (jm & 63)) & 1ull) == 0;
+        if (lane < nr) {
+            if (lane == cur) u += minv;
+            else if (sc_j) u += minv - spc_j;
+        }
+        if (lane < nc && ((rem >> lane) & 1ull) == 0) v -= minv - spc;
+        int j = sink;
+        while (true) {
+            const int pi = __builtin_amdgcn_readlane(path, j);
+            r4c = (lane == j) ? pi : r4c;
+            const int t = __builtin_amdgcn_readlane(c4r, pi);
+            c4r = (lane == pi) ? j : c4r;
+            j = t;
+            if (pi == cur) break;
+        }
+    }
+    col4row[0] = c4r;
+    if (kCount) *steps = nsteps;
+    return ASG_OK;
+}
+#endif
+
 template <class Acc, bool kCount = false>
 __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1], int *steps = nullptr) {
 #ifdef ASG_LSA_GENERIC_REG
     return lsa_solve_wave<1>(acc, nr, nc, col4row);
+#elif ASG_LSA_COLAT
+    return lsa_solve_reg64_colat<Acc, kCount>(acc, nr, nc, col4row, steps);
 #else
     int nsteps = 0;
     const int lane = threadIdx.x & (kWave - 1);

@@ -11,8 +11,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for lib in default "$@"; do
   if [ "$lib" = default ]; then unset ASG_LIB_PATH; else export ASG_LIB_PATH=$PWD/$lib; fi
   tag=$(basename "$lib" .so)
-  timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_sap.py \
-      -k "not multi_problem" > "$OUT/tests_$tag.log" 2>&1 || { echo "FAILED tests $lib"; tail -20 "$OUT/tests_$tag.log"; exit 1; }
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_sap.py tests/test_gpu_parity.py \
+      -k "sap or lsa or haa or eps0" > "$OUT/tests_$tag.log" 2>&1 || { echo "FAILED tests $lib"; tail -20 "$OUT/tests_$tag.log"; exit 1; }
   echo "tests ok $lib: $(tail -1 "$OUT/tests_$tag.log")"
 done
 for rep in $(seq 1 ${REPS:-2}); do
