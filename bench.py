@@ -191,7 +191,7 @@ def reset_bytes(n, m, L):
     return n * m * (4 * (L + 1) + 4 + 1) + 8 * n + 8
 
 
-def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
+def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=False):
     """Roofline of the fused rollout kernel (asg_rollout -> rollout_kernel), per env step: the
     env step's bytes plus the agent's h in / h out and the action written -- the observations
     it generates are consumed on chip, never read back -- per env, times E, over its HIP-event
@@ -199,16 +199,19 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
     `frac` is against HBM; `bound` names what binds, from the kernel's SQ counters when
     profiled (tools/round_profile.sh): "latency/store-ack" when neither VALU issue nor the
     MFMA pipe is at half its capacity and HBM is not near its roof (the waves wait on the
-    in-order vmcnt queue behind their own row stores)."""
+    in-order vmcnt queue behind their own row stores).  q_out: the
+    asg_step_forward instances (REDA's step_q schedule), which also write the Q rows (4 m per
+    agent) and read the actions row the SAP kernel wrote instead of writing one."""
     # the episode's reset runs in its first launch (asg_reset_rollout): its row counts too
-    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)
+    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8 + (4 * a.m if q_out else 0))
                   + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E
     per_launch = int(round(per_launch))
     achieved = per_launch / (fused_ms * 1e-3) / 1e9
     frac = achieved / HBM_PEAK_GBS
-    pm = pmc_lookup("*pmc_rollout_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
+    tag = "rollout_q" if q_out else "rollout"
+    pm = pmc_lookup(f"*pmc_{tag}_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     issue = None
-    pq = pmc_lookup("*pmc_rollout_sq*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
+    pq = pmc_lookup(f"*pmc_{tag}_sq*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     if pq:
         c, d = pq["counters"], pq["derived"]
         spl = pq.get("steps_per_launch", 1)  # the profiled launches ran spl steps each
@@ -235,7 +238,8 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0):
     out = {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(frac, 4),
            "traffic": traffic,
-           "kernel": "asg::rollout_kernel (env steps + agent/eps-greedy selections, per step)",
+           "kernel": ("asg::rollout_kernel Q-output instance (asg_step_forward: env step + agent forward)" if q_out
+                      else "asg::rollout_kernel (env steps + agent/eps-greedy selections, per step)"),
            "kernel_ms": round(fused_ms, 4), "bytes_per_launch": per_launch,
            "per_launch_note": "per env step of the launch (bytes_per_launch, kernel_ms: one step's share; "
                               "the fused resets' rows amortised over the timed steps)",
@@ -379,6 +383,20 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
 
     if selector == "sap":
         sel_obj.select_action = timed_select
+    fwd_pairs = []
+    inner_fwd = env.step_forward
+
+    def timed_forward(*args_, **kw):  # asg_step_forward alone (the step_q schedule's rollout kernel)
+        if not state["timing"]:
+            return inner_fwd(*args_, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = inner_fwd(*args_, **kw)
+        e1.record()
+        fwd_pairs.append((e0, e1, 1))
+        return out
+
+    env.step_forward = timed_forward
 
     # the runner's schedule (GpuVecRunner.rollout).  mode "episode" (the default with the fused
     # agent + epsilon-greedy): asg_rollout -- select(0); for t: env.step(t), select(t + 1) -- as one
@@ -441,7 +459,7 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     def one_step():
         t = state["t"]
         with torch.no_grad():
-            fused = state["mode"] == "step"
+            fused = state["mode"] in ("step", "step_q")
             if selector == "random":
                 timed(sel_pairs, lambda: env.random_actions(runner.batch, ts=t))
             elif not state["selected"]:
@@ -486,6 +504,7 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     res = {"elapsed": elapsed, "warmup_elapsed": warm_elapsed, "kern_ms": mean(ev_pairs), "sel_ms": mean(sel_pairs),
            "lsa_ms": mean(lsa_pairs) if lsa_pairs else None,
            "fused_ms": mean(fused_pairs) if fused_pairs else None, "mode": state.get("mode"),
+           "step_forward_ms": mean(fwd_pairs) if fwd_pairs else None,
            "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs),
            "fused_resets": state.get("fused_resets", 0),
            "gather_ms": mean(gather_pairs) if gather_pairs else None, "gathers": len(gather_pairs)}
@@ -526,6 +545,17 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
 def res_resets(res):
     """Fused resets per timed step of a leg (asg_reset_rollout launches in the timed window)."""
     return res.get("fused_resets", 0) / res["fused_steps"] if res.get("fused_steps") else 0.0
+
+
+def sap_kernels(r):
+    """HIP-event times per step of a SAP-selector leg: on the step_q schedule the fused env
+    step + agent forward (asg_step_forward), the SAP kernel, and the step as a whole (both
+    launches plus the selector's host-side work); the episode's first selection (agent kernel
+    + SAP) and last env step are separate launches."""
+    r4 = lambda v: round(v, 4) if v else None  # noqa: E731
+    return {"step_forward": r4(r.get("step_forward_ms")), "sap_select": r4(r.get("lsa_ms")),
+            "fused_step_total": r4(r.get("fused_ms")), "env_step": r4(r.get("kern_ms")),
+            "first_select": r4(r.get("sel_ms")), "schedule": r.get("mode") or "split"}
 
 
 def lsa_roofline(a, E, res):
@@ -583,7 +613,9 @@ def main():
     G = res["global_envs"]
     value = G * a.steps / res["elapsed"]
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
-    if res.get("fused_ms"):
+    if res.get("mode") == "step_q" and res.get("step_forward_ms"):
+        roof = fused_roofline(a, E, res["step_forward_ms"], use_rnn=a.use_rnn, q_out=True)
+    elif res.get("fused_ms"):
         roof = fused_roofline(a, E, res["fused_ms"], resets_per_step=res_resets(res))
     else:
         per_launch = step_bytes(a.n, a.m, a.L) * E
@@ -629,14 +661,17 @@ def main():
                         "kernel (rnn_agent_h2_kernel), one launch each per step"}
         if a.n <= a.m <= 64 and a.selector != "sap":
             r3 = run_leg(a, dev, world, E, sk, sw, selector="sap", agent="rnn", count_lsa=True)
-            agent_ms = r3["sel_ms"] - (r3["lsa_ms"] or 0.0)
             extra["sap"] = {
                 **leg_base(r3, sk, sw),
-                "what": "SequentialAssignmentProblemSelector (eps 0.05): fused RNNAgent forward kernel, then "
-                        "asg_sap_select (per-env Gaussian noise + scipy-exact LSA, one wave64 per env)",
-                "env_step_ms": round(r3["kern_ms"], 4), "agent_ms": round(agent_ms, 4),
-                "roofline_lsa": lsa_roofline(a, E, r3),
-                "roofline_agent": agent_roofline(a, E, agent_ms, "asg::rnn_agent_h2_kernel (forward only)")}
+                "what": "SequentialAssignmentProblemSelector (eps 0.05) on the step_q schedule: per step one "
+                        "asg_step_forward launch (env step t + the RNNAgent forward of t + 1, Q to HBM) and one "
+                        "asg_sap_select_into launch (per-env Gaussian noise + scipy-exact LSA, one wave64 per env, "
+                        "actions written into the batch row)",
+                "kernels_ms": sap_kernels(r3),
+                "roofline_lsa": lsa_roofline(a, E, r3)}
+            if r3.get("mode") == "step_q" and r3.get("step_forward_ms"):
+                extra["sap"]["roofline_step_forward"] = fused_roofline(a, E, r3["step_forward_ms"],
+                                                                       use_rnn=a.use_rnn, q_out=True)
         if a.config == 2 and world == 1 and a.selector == "eps":
             # the reference's own algorithms for this env (config/algs/mock_constellation_*.yaml):
             # jumpstart_mac with the HAA jumpstart selector, use_rnn: False (Linear + ReLU agent),
@@ -657,11 +692,13 @@ def main():
                             f"(Linear + ReLU, fused split-f16 kernel), both epsilons 1 -> 0 over 20,000 env steps; "
                             f"timed after one warmup episode (the jumpstart/HAA phase, t_env = 0)",
                     "jumpstart_phase_value": round(rj["global_envs"] * a.T / rj["warmup_elapsed"], 1),
-                    "kernels_ms": {"fused_rollout_per_step": round(rj["fused_ms"], 4) if rj["fused_ms"] else None,
-                                   "env_step": round(rj["kern_ms"], 4) if rj["kern_ms"] else None,
-                                   "select": round(rj["sel_ms"], 4) if rj["sel_ms"] else None,
-                                   "sap_select": round(rj["lsa_ms"], 4) if rj.get("lsa_ms") else None}}
-                if rj.get("fused_ms"):
+                    "kernels_ms": sap_kernels(rj) if sel_ == "sap" else {
+                        "fused_rollout_per_step": round(rj["fused_ms"], 4) if rj["fused_ms"] else None,
+                        "env_step": round(rj["kern_ms"], 4) if rj["kern_ms"] else None,
+                        "select": round(rj["sel_ms"], 4) if rj["sel_ms"] else None}}
+                if rj.get("mode") == "step_q" and rj.get("step_forward_ms"):
+                    extra[name]["roofline"] = fused_roofline(a, E, rj["step_forward_ms"], use_rnn=False, q_out=True)
+                elif rj.get("fused_ms"):
                     extra[name]["roofline"] = fused_roofline(a, E, rj["fused_ms"], use_rnn=False,
                                                              resets_per_step=res_resets(rj))
         if a.config == 2 and world == 1:
@@ -762,14 +799,17 @@ def main():
                        "envs_per_gpu": E, "global_envs": G, "n": a.n, "m": a.m, "T": a.T, "L": a.L,
                        "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
             "roofline": roof,
-            "kernels_ms": {"fused_rollout_per_step": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
-                           "env_step": round(kern_ms, 4) if kern_ms else None,
-                           "select": round(sel_ms, 4) if sel_ms else None,
+            "kernels_ms": {**(sap_kernels(res) if a.selector == "sap" else {
+                               "fused_rollout_per_step": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
+                               "env_step": round(kern_ms, 4) if kern_ms else None,
+                               "select": round(sel_ms, 4) if sel_ms else None}),
                            "schedule": res.get("mode") or "split",
                            "fused_launches": res.get("fused_launches"), "fused_steps": res.get("fused_steps"),
                            "note": {"episode": "asg_rollout: each launch runs a chunk of an episode's steps (the "
                                                "runner launches whole episodes); kernel time per step",
-                                    "step": "T-1 fused launches + 1 select + 1 step per episode"}.get(
+                                    "step": "T-1 fused launches + 1 select + 1 step per episode",
+                                    "step_q": "per episode: T-1 x (asg_step_forward + asg_sap_select_into), "
+                                              "1 select (agent kernel + SAP) + 1 step"}.get(
                                         res.get("mode"), "one select + one step per step")},
             "roofline_agent": ra,
             "cpu_baseline": cpu,

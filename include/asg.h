@@ -215,6 +215,15 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
 int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                    double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
                    float *col_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
+/* asg_sap_select writing the assignment as the int64 actions the runner's batch.update casts
+ * the selector's float picked_actions to (parallel_runner.py:150-152, episode_buffer.py:89-129):
+ * act_out [B][n] int64 contiguous (e.g. a time-major EpisodeBatch actions row), -1 rows for
+ * failed envs.  Same draws and assignments as asg_sap_select.  status_out [B] (may be NULL)
+ * ACCUMULATES: status_out[b] = min(status_out[b], status of env b) -- zero it once, read it
+ * once per episode (error codes are negative). */
+int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
+                        double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
+                        int64_t *act_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
 
 /* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
  * per row, with probability epsilon a uniformly random available action, else the first
@@ -348,6 +357,17 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
                     const float *b_ih, const float *b_hh, const float *b2, int K, int hidden, const float *h_in,
                     int64_t h_stride, float *h_out, double epsilon, uint64_t seed, uint64_t counter,
                     int32_t *status, void *hip_stream);
+/* asg_step at row ts then the agent forward (asg_rnn_agent_forward semantics) on row ts + 1,
+ * in one rollout-kernel launch: the runner loop's env.step(t) + mac.forward(t + 1) for a
+ * selector that acts on Q outside the kernel (SequentialAssignmentProblemSelector,
+ * mock_constellation_reda.yaml; sap_selectors.py:52-98).  Observation row ts + 1 is generated,
+ * stored and consumed on chip; q_out [E n][m] f32 contiguous (16-B aligned) receives the Q rows,
+ * h_out the hidden state.  Needs k + 1 < T; the actions of row ts are read from the batch.
+ * Every benefit source (Philox, MT19937-compat and injected tables); agent and batch
+ * requirements as asg_rollout. */
+int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                     const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                     const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream);
 /* Number of fc1 weight slices (32 inputs x 64 units) the rollout kernel reads through L2
  * instead of LDS for an (n, m, L) env and agent kind, or -1 when asg_rollout does not take
  * the shape (GRU: 64 x 64, L = 3: 1; 256 x 256: 19).  asg_step_select_l2_slices = the GRU

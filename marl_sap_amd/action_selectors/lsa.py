@@ -54,10 +54,13 @@ def raise_on_status(status):
 
 class DeferredStatus:
     """Accumulates LSA status on the device so the rollout loop never syncs per step;
-    `flush()` (called by the runner once per episode) raises the first error."""
+    `flush()` (called by the runner once per episode) raises the first error.  `sticky(B)`:
+    a zeroed per-env int32 word that kernels min-accumulate into themselves
+    (asg_sap_select_into) -- no reduction launches per call."""
 
     def __init__(self):
         self._acc = None
+        self._sticky = None
 
     def add(self, status):
         m = status.min() if status.numel() else None
@@ -65,7 +68,18 @@ class DeferredStatus:
             return
         self._acc = m if self._acc is None else torch.minimum(self._acc, m)
 
+    def sticky(self, B, device):
+        st = self._sticky
+        if st is None or st.numel() != B or st.device != device:
+            if st is not None:
+                self.add(st)  # keep what the old buffer holds
+            st = self._sticky = torch.zeros(B, dtype=torch.int32, device=device)
+        return st
+
     def flush(self):
+        if self._sticky is not None:
+            self.add(self._sticky)
+            self._sticky = None
         acc, self._acc = self._acc, None
         if acc is not None:
             raise_on_status(acc.reshape(1))

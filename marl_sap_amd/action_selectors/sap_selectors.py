@@ -41,7 +41,10 @@ class SequentialAssignmentProblemSelector:
     def _env_index_base(self):
         return env_index_base(self)
 
-    def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None):
+    def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, beta=None, out=None):
+        """Returns the float32 task ids (the reference's picked_actions); with `out` (an int64
+        [B, n] contiguous view, e.g. the EpisodeBatch actions row the runner would cast them
+        into) the ids are written there as int64 and `out` is returned."""
         self.epsilon = self.schedule.eval(t_env)
         if test_mode:
             self.epsilon = self.args.evaluation_epsilon
@@ -50,18 +53,26 @@ class SequentialAssignmentProblemSelector:
         if n <= m <= 64 and q.is_cuda:
             if q.dtype != torch.float32:
                 q = q.float()
-            out = torch.empty((B, n), dtype=torch.float32, device=q.device)
-            status = torch.empty((B,), dtype=torch.int32, device=q.device)
+            into = (out is not None and out.dtype == torch.int64 and tuple(out.shape) == (B, n)
+                    and out.is_contiguous() and out.device == q.device)
             self.calls += 1
+            steps = ctypes.c_void_p(self.count_steps.data_ptr()) if self.count_steps is not None else None
+            common = (ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), B, n, m, float(self.epsilon),
+                      self.seed & 0xFFFFFFFFFFFFFFFF, self.calls, self._env_index_base())
             with torch.cuda.device(q.device):
+                if into:
+                    status = self.status.sticky(B, q.device)  # min-accumulated by the kernel
+                    _lib.check(_lib.lib().asg_sap_select_into(
+                        *common, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), steps,
+                        _lib.stream_ptr(q.device)))
+                    return out
+                res = torch.empty((B, n), dtype=torch.float32, device=q.device)
+                status = torch.empty((B,), dtype=torch.int32, device=q.device)
                 _lib.check(_lib.lib().asg_sap_select(
-                    ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()), B, n, m, float(self.epsilon),
-                    self.seed & 0xFFFFFFFFFFFFFFFF, self.calls, self._env_index_base(),
-                    ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()),
-                    ctypes.c_void_p(self.count_steps.data_ptr()) if self.count_steps is not None else None,
+                    *common, ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(status.data_ptr()), steps,
                     _lib.stream_ptr(q.device)))
             self.status.add(status)
-            return out
+            return res
         if self.epsilon > 0:
             avg = q.abs().mean(dim=(1, 2), keepdim=True)
             q = q + torch.randn_like(q) * (avg * self.epsilon * 2)

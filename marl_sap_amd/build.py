@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmarl_sap_amd.so")
 SOURCES = ["asg_abi.hip", "asg_env.hip", "asg_lsa.hip", "asg_select.hip", "asg_agent.hip", "asg_real.hip",
-           "asg_filtered.hip", "asg_h2.hip"]
+           "asg_filtered.hip", "asg_h2.hip", "asg_rollout_tab.hip", "asg_rollout_q.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ASG_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",

@@ -55,30 +55,69 @@ class BasicMAC:
                 and isinstance(self.selector_agent, RNNFusedAgent)
                 and not getattr(self.args, "unfused_selection", False))
 
-    def fused_step_ok(self, env, ep_batch):
-        """The runner may fuse env.step(t) with select_actions(t + 1) (asg_rollout): the fused
-        agent (GRU or Linear RNNAgent) + epsilon-greedy selection on plain observation inputs, a
-        time-major batch and an env that takes it.  args.fused_rollout: True / "episode" /
-        "always" (default: a whole episode per launch), "step" (one launch per step), False
-        (separate env-step and agent launches)."""
+    def _fused_q_ok(self):
+        """The REDA selector (SequentialAssignmentProblemSelector, n <= m <= 64: its fused
+        noise + LSA kernel) acts on the agent's Q outside the rollout kernel: the env step and
+        the agent forward fuse (asg_step_forward), the selection stays a separate launch."""
+        from ..action_selectors.sap_selectors import SequentialAssignmentProblemSelector
+        from ..modules.agents.rnn_agent import RNNFusedAgent
+        return (not torch.is_grad_enabled() and self.agent_output_type == "q"
+                and type(self.action_selector) is SequentialAssignmentProblemSelector
+                and isinstance(self.selector_agent, RNNFusedAgent) and self.n <= self.selector_agent.n_out <= 64
+                and not getattr(self.args, "unfused_selection", False))
+
+    def _fused_kind(self, env, ep_batch):
+        """"select" (the selection runs in the rollout kernel: epsilon-greedy), "q" (the kernel
+        writes Q for the SAP selector) or None."""
         from ..modules.agents.rnn_agent import RNNFusedAgent
         mode = getattr(self.args, "fused_rollout", True)
-        return (bool(mode) and self._fused_select_ok(slice(None)) and hasattr(env, "can_step_select")
-                and env.can_step_select(prefer=(mode != "always"), use_rnn=bool(self.args.use_rnn))
-                and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
-                and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
-                and self.selector_agent.n_out == env.m)
+        if not mode:
+            return None
+        kind = "select" if self._fused_select_ok(slice(None)) else ("q" if self._fused_q_ok() else None)
+        ok = (kind is not None and hasattr(env, "can_step_select")
+              and env.can_step_select(prefer=(mode != "always"), use_rnn=bool(self.args.use_rnn))
+              and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
+              and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
+              and self.selector_agent.n_out == env.m)
+        return kind if ok else None
+
+    def fused_step_ok(self, env, ep_batch):
+        """The runner may fuse env.step(t) with select_actions(t + 1) (asg_rollout): the fused
+        agent (GRU or Linear RNNAgent) + epsilon-greedy selection -- or, for the SAP selector,
+        env.step(t) with the agent forward of t + 1 (asg_step_forward) -- on plain observation
+        inputs, a time-major batch and an env that takes it.  args.fused_rollout: True /
+        "episode" / "always" (default: a whole episode per launch), "step" (one launch per
+        step), False (separate env-step and agent launches)."""
+        return self._fused_kind(env, ep_batch) is not None
 
     def fused_mode(self, env, ep_batch, t_env=0, test_mode=False):
         """How the runner schedules this episode: "episode" (asg_rollout over all T steps),
-        "step" (asg_rollout per step) or None (separate launches)."""
-        if not self.fused_step_ok(env, ep_batch):
+        "step" (asg_rollout per step), "step_q" (asg_step_forward + the SAP selection per
+        step) or None (separate launches)."""
+        kind = self._fused_kind(env, ep_batch)
+        if kind is None:
             return None
+        if kind == "q":
+            return "step_q"
         return "step" if getattr(self.args, "fused_rollout", True) == "step" else "episode"
 
     def fused_step_select(self, env, ep_batch, t_ep, t_env, test_mode=False):
         """env.step at row t_ep and select_actions for row t_ep + 1 in one kernel; the
-        hidden state advances as select_actions would advance it."""
+        hidden state advances as select_actions would advance it.  SAP selector: the kernel
+        ends with the agent's Q (kept in one reused buffer), which the selector's kernel turns
+        into the actions of row t_ep + 1, written in place."""
+        if self._fused_q_ok():
+            q, self.hidden_states = env.step_forward(ep_batch, t_ep, self.selector_agent, self.hidden_states,
+                                                     q_out=getattr(self, "_q_buf", None))
+            self._q_buf = q
+            row = ep_batch["actions"][:, t_ep + 1, :, 0]
+            acts = self.action_selector.select_action(q.view(ep_batch.batch_size, self.n, -1),
+                                                      ep_batch["avail_actions"][:, t_ep + 1], t_env,
+                                                      test_mode=test_mode, beta=ep_batch["beta"][:, t_ep + 1],
+                                                      out=row)
+            if acts is not row:
+                ep_batch.update({"actions": acts}, ts=t_ep + 1, mark_filled=False, preprocess=False)
+            return
         eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device)
         self.hidden_states = env.step_select(ep_batch, t_ep, self.selector_agent, self.hidden_states, eps, seed,
                                              counter, status)

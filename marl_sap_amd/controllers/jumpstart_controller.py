@@ -2,13 +2,14 @@
 probability jumpstart_epsilon (one numpy coin flip per selection for the whole batch, drawn
 from numpy's global stream like the reference) the non-RL selector (HAA) acts.
 
-When the RL MAC fuses (the RNNAgent + epsilon-greedy: mock_constellation_iql.yaml) the GPU
-runner draws an episode's coin flips when it plans the episode (fused_mode), in the
+When the RL MAC fuses (the RNNAgent + epsilon-greedy: mock_constellation_iql.yaml; or
+the RNNAgent forward + the SAP selector: mock_constellation_reda.yaml) the GPU runner draws an episode's coin flips when it plans the episode (fused_mode), in the
 reference's order (one per select_actions call, t = 0, 1, ...): the epsilon-greedy selector
 draws nothing from numpy's global stream, so the stream is consumed exactly as the
 reference's per-step draws consume it.  When every flip picks the RL branch the episode is
 one asg_rollout kernel; otherwise the RL steps still fuse env.step(t) with
-select_actions(t + 1), and the HAA steps run env.step + the HAA selector.  Any other RL
+select_actions(t + 1) (SAP: with the agent forward of t + 1, the LSA kernel after it), and the
+HAA steps run env.step + the HAA selector.  Any other RL
 selector may draw from the same stream itself (EpsilonGreedySAPTestActionSelector,
 sap_selectors.py:36): then nothing is pre-drawn and each select_actions draws its flip when
 it runs, interleaved with the selector's draws as in the reference."""
@@ -47,8 +48,8 @@ class JumpstartMAC(BasicMAC):
         return super().select_actions(ep_batch, t_ep, t_env, bs=bs, test_mode=test_mode, out=out)
 
     def fused_mode(self, env, ep_batch, t_env=0, test_mode=False):
-        """When the RL MAC fuses (its selector is epsilon-greedy, which draws nothing from
-        numpy's global stream): draw the episode's T coin flips now (the reference's order);
+        """When the RL MAC fuses (its selector is epsilon-greedy or the fused SAP selector,
+        neither of which draws from numpy's global stream): draw the episode's T coin flips now (the reference's order);
         "episode" when every one picks the RL branch, else "step" (the RL steps' env.step +
         selection fused).  Otherwise None, and no flip is pre-drawn: each select_actions
         draws its own, interleaved with the RL selector's draws as in the reference."""
@@ -58,6 +59,8 @@ class JumpstartMAC(BasicMAC):
             return None
         eps = self._eps(t_env, test_mode)
         self._flips = list(np.random.rand(env.T) < eps)
+        if base == "step_q":
+            return base  # per step either way; the SAP selector's noise is Philox, not numpy
         return "episode" if base == "episode" and not any(self._flips) else "step"
 
     def fused_episode(self, env, ep_batch, t_env, test_mode=False, reset=False):

@@ -371,6 +371,20 @@ int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n,
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select");
 }
 
+int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, int n, int m, double epsilon,
+                        uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *act_out,
+                        int32_t *status_out, int32_t *path_steps_out, void *hip_stream) {
+    if (!q || !q_strides || !act_out || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_into: bad arguments");
+    if (n > m || m > 64) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_into: needs n <= m <= 64");
+    if (!(epsilon >= 0.0)) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_into: epsilon must be >= 0");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_sap_select(q, q_strides, B, n, m, (float)epsilon, seed, (uint32_t)counter,
+                                          env_index_base, nullptr, status_out, path_steps_out,
+                                          static_cast<hipStream_t>(hip_stream), act_out);
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select_into");
+}
+
 int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
                        uint64_t counter, int64_t env_index_base, int64_t *out, const int64_t out_strides[2],
@@ -537,11 +551,13 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
                         int reset, const void *packed, const float *b1, const float *b_r0, const float *b_r1,
                         const float *b2, int K, int hidden, int use_rnn, const float *h_in, int64_t h_stride,
                         float *h_out, double epsilon, uint64_t seed, uint64_t counter, int32_t *status,
-                        void *hip_stream) {
+                        void *hip_stream, float *q_out = nullptr) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (int rc = check_view(h, b, ts, true)) return rc;
-    if (!packed || !b1 || !b_r0 || (use_rnn && !b_r1) || !b2 || !h_out || !status)
+    if (!packed || !b1 || !b_r0 || (use_rnn && !b_r1) || !b2 || !h_out || (!status && !q_out))
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: NULL agent argument");
+    if (q_out && (reinterpret_cast<uintptr_t>(q_out) % 16) != 0)
+        return fail(h, ASG_E_INVALID_ARG, "asg_step_forward: q_out must be 16-B aligned");
     const asg::EnvState &st = h->st;
     if (!h->has_reset && !reset) return fail(h, ASG_E_STATE, "step called before reset");
     if (reset && (st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED))
@@ -589,7 +605,7 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     if (reset && h->has_reset) lst.episode += 1;
     hipError_t e = asg::launch_rollout(sl, lst, ts, k0, steps, select_first, select_last, reset,
                                        static_cast<const float4 *>(packed), b1, b_r0, b_r1, b2, use_rnn, h_in, h_stride,
-                                       h_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);
+                                       h_out, q_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);
     if (e != hipSuccess) return hip_fail(h, e, "asg_rollout");
     h->st.episode = lst.episode;
     if (reset) {
@@ -622,6 +638,14 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
                     int32_t *status, void *hip_stream) {
     return asg_rollout(h, b, ts, 1, 0, 1, packed, b1, b_ih, b_hh, b2, K, hidden, 1, h_in, h_stride, h_out, epsilon,
                        seed, counter, status, hip_stream);
+}
+
+int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                     const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                     const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream) {
+    if (!q_out) return fail(h, ASG_E_INVALID_ARG, "asg_step_forward: NULL q_out");
+    return rollout_impl(h, b, ts, 1, 0, 1, 0, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in, h_stride, h_out,
+                        0.0, 0, 0, nullptr, hip_stream, q_out);
 }
 
 }  // extern "C"

@@ -120,6 +120,7 @@ __device__ __forceinline__ float row_max4(float v) {
 __host__ __device__ inline int slice_k(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + j - 4; }
 
 // ---- geometry and packed layout -----------------------------------------------------------
+#if !ASG_H2_TU
 H2Geom h2_geom(int K, int nout) {
     H2Geom g;
     g.K = K;
@@ -134,6 +135,7 @@ H2Geom h2_geom(int K, int nout) {
     return g;
 }
 bool h2_ok(int K, int nout) { return K >= 1 && nout >= 1 && nout <= 256; }
+#endif
 
 // packed h2 section (u32x4v units): [header: int sw1, sw_r1, sw_r2, sw2]
 //   [W1 planes: slice Kp / 32][mt 4][plane 2][lane 64]
@@ -152,11 +154,13 @@ __device__ __forceinline__ int64_t w1_idx(int sl, int mt, int pl, int lane) {
     return (((int64_t)sl * 4 + mt) * 2 + pl) * 64 + lane;
 }
 __device__ __forceinline__ int w2_idx(int c, int sl, int pl, int lane) { return ((c * 2 + sl) * 2 + pl) * 64 + lane; }
-static int64_t w1t_f4(const H2Geom &g) { return g.prefix ? (int64_t)g.P * 16 : 0; }
+static inline int64_t w1t_f4(const H2Geom &g) { return g.prefix ? (int64_t)g.P * 16 : 0; }
+#if !ASG_H2_TU
 int64_t h2_packed_f4(int K, int nout, int use_rnn) {
     const H2Geom g = h2_geom(K, nout);
     return w1t_f4(g) + 1 + w1s_f4(g.Kp) + rec_f4(use_rnn != 0) + w2s_f4(g.nct);
 }
+#endif
 
 // LDS image (u32x4v units): [recurrent planes][biases][W2 planes (W2L)][W1 slices][scratch]
 // biases (floats): b1 [64] | GRU: b_ir + b_hr, b_iz + b_hz, b_in, b_hn [4 x 64]; Linear: b_rnn,
@@ -814,6 +818,7 @@ rnn_agent_h2_kernel(H2Args a) {
     }
 }
 
+#if !ASG_H2_TU
 // ---- packing: max|W| -> scale exponent, then the scaled f16 planes ------------------------
 __global__ void h2_exp_kernel(const float *W, int64_t n, int *out) {
     __shared__ float s_m[16];
@@ -889,6 +894,7 @@ hipError_t launch_h2_pack(const float *W1, const float *Wih, const float *Whh, c
     pack(W2, nout, kHid, kHid, kHid, g.nct, 2, 0, 3, o);
     return hipGetLastError();
 }
+#endif  // !ASG_H2_TU
 
 // LDS plan: recurrent planes, biases, W2 planes when they fit, then as many W1 slices (from
 // s0) as fit; `reserve` bytes per workgroup kept for a per-wave scratch
@@ -898,7 +904,7 @@ struct H2Lds {
     int64_t scratch_off;  // u32x4v units
     size_t bytes;
 };
-static H2Lds h2_lds_plan(const H2Geom &g, bool rnn, int s0, int64_t reserve_f4) {
+static inline H2Lds h2_lds_plan(const H2Geom &g, bool rnn, int s0, int64_t reserve_f4) {
     constexpr int64_t kCap = 160 * 1024 / 16;
     H2Lds p{};
     p.w2l = lds_w2_off(rnn, g.nct) + w2s_f4(g.nct) + reserve_f4 <= kCap;
@@ -911,6 +917,7 @@ static H2Lds h2_lds_plan(const H2Geom &g, bool rnn, int s0, int64_t reserve_f4) 
     return p;
 }
 
+#if !ASG_H2_TU
 hipError_t launch_h2_agent(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
                            const float4 *packed, const float *b1, const float *bih, const float *bhh, const float *b2,
                            int nout, int use_rnn, float *Hout, float *Q, const SelectArgs *sel, hipStream_t s) {
@@ -959,6 +966,7 @@ hipError_t launch_h2_agent(const float *X, int64_t xs, int64_t R, int K, const f
 #undef LH_
     return hipGetLastError();
 }
+#endif  // !ASG_H2_TU
 
 // =====================================================================================
 // Fused rollout (mock env, Philox bumps): for every env, transitions k0 .. k1 - 1 and the
@@ -997,6 +1005,9 @@ struct RolloutArgs {
     // benefits: NULL = Philox bumps regenerated in registers; else the handle's float64 table
     // [E][T][n][m] (MT19937 compat / injected sat_prox_mat), read for the L lookahead rows
     const double *table;
+    // QOUT instances: the agent's Q rows [E n][m] f32 (the forward of asg_rnn_agent_forward)
+    // instead of the epsilon-greedy selection -- a selector outside the kernel (SAP) acts on them
+    float *Q;
     // agent
     const u32x4v *pk;
     const float *W1T, *Hin;
@@ -1174,7 +1185,7 @@ struct HNext {
     int mode;
 };
 
-template <bool RNN, bool W2L, bool GEN, bool TAB, bool AGENT, class RA>
+template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, bool AGENT, class RA>
 __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
                                              uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
@@ -1460,6 +1471,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
         H2Args a = rollout_h2args(ra);
         a.sel.counter = ra.counter + (uint32_t)pass;
         a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
+        if constexpr (QOUT) a.Q = ra.Q;
         float4 hB[4][NT];
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1494,11 +1506,11 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                                        : f32x4{0.f, 0.f, 0.f, 0.f};
                 }
         };
-        h2_tail<NT, RNN, true, W2L, true, GEN>(a, Wl, sw, row0, rows, ok, hB, xB, s_act, RT * sub, prefetch);
+        h2_tail<NT, RNN, !QOUT, W2L, true, GEN>(a, Wl, sw, row0, rows, ok, hB, xB, s_act, RT * sub, prefetch);
     }
 }
 
-template <bool RNN, bool W2L, bool GEN, bool TAB>
+template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT>
 __global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
 rollout_kernel(RolloutArgs ra) {
     extern __shared__ u32x4v s_h2[];
@@ -1603,14 +1615,14 @@ rollout_kernel(RolloutArgs ra) {
                                                     (int64_t)(16 * kH2NT) * (sub + 1), 1};
                     else if (next_agent) nx = HNext{ri.Hout, kHid, 0, 1};
                     // the reset row (select_first) is stored here when the reset runs in this launch
-                    rollout_tile<RNN, W2L, GEN, TAB, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
+                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
                                                       key, s_scl, s_act, s_h2, sw, hN, hpf, nx);
                     hpf = nx.mode != 0;
                 }
                 ++pass;
             } else {
                 for (int sub = 0; sub < ntile; ++sub)
-                    rollout_tile<RNN, W2L, GEN, TAB, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
+                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
                                                        sw, hN, false, HNext{nullptr, kHid, 0, 0});
             }
 #undef RA_
@@ -1622,6 +1634,43 @@ rollout_kernel(RolloutArgs ra) {
     }
 }
 
+// The rollout kernel's instances, one launcher per translation unit (the instances dominate
+// the build: asg_h2.hip holds the Philox epsilon-greedy ones, asg_rollout_tab.hip the table
+// modes', asg_rollout_q.hip the Q-output ones of both benefit sources).
+struct RolloutLaunch {
+    unsigned grid;
+    size_t lds;
+    bool rnn, w2l, gen;
+};
+template <bool TAB, bool QOUT>
+static hipError_t launch_rollout_inst(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
+#define LR_(RNN, W2L, GEN) \
+    hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, TAB, QOUT>), dim3(lc.grid), dim3(64 * kH2Waves), lc.lds, s, ra)
+#define LR2_(RNN)                                                        \
+    do {                                                                 \
+        if (lc.w2l) {                                                    \
+            if (lc.gen) LR_(RNN, true, true); else LR_(RNN, true, false);   \
+        } else {                                                         \
+            if (lc.gen) LR_(RNN, false, true); else LR_(RNN, false, false); \
+        }                                                                \
+    } while (0)
+    if (lc.rnn) LR2_(true); else LR2_(false);
+#undef LR2_
+#undef LR_
+    return hipGetLastError();
+}
+hipError_t launch_rollout_tab(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s);
+hipError_t launch_rollout_q(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s);
+
+#if ASG_H2_TU == 1
+hipError_t launch_rollout_tab(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
+    return launch_rollout_inst<true, false>(ra, lc, s);
+}
+#elif ASG_H2_TU == 2
+hipError_t launch_rollout_q(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
+    return ra.table ? launch_rollout_inst<true, true>(ra, lc, s) : launch_rollout_inst<false, true>(ra, lc, s);
+}
+#else
 // shapes the rollout kernel takes: the split-f16 agent with the mock env's obs layout
 // (K = m (L + 1), one-hot prefix geometry), n, m <= 256
 bool rollout_shape_ok(int n, int m, int L, int K) {
@@ -1638,7 +1687,7 @@ int rollout_l2_slices(int n, int m, int L, int use_rnn) {
 
 hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
                           int select_last, int reset, const float4 *packed, const float *b1, const float *bi, const float *bh,
-                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
+                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float *Q, float epsilon,
                           uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s) {
     const int K = st.m * (st.L + 1), nout = st.m;
     const H2Geom g = h2_geom(K, nout);
@@ -1679,6 +1728,9 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     const bool tab = st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
     ra.table = tab ? st.table : nullptr;
     if (tab && reset) return hipErrorInvalidValue;  // the table modes' reset is asg_reset (MT19937 stream)
+    // Q output: one transition and the forward of the row after it (asg_step_forward)
+    if (Q && (steps != 1 || select_first || !select_last || reset)) return hipErrorInvalidValue;
+    ra.Q = Q;
     ra.W1T = reinterpret_cast<const float *>(packed);
     ra.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
     ra.Hin = Hin;
@@ -1698,31 +1750,18 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     const H2Lds plan = h2_lds_plan(g, rnn, g.Pp / 32, scr_f4);
     ra.w1_lds = plan.w1_lds;
     ra.scratch_off = plan.scratch_off;
-    const bool gen = st.m % 32 != 0 || st.n % 32 != 0;
     const int ncu = stream_cus(s);
     const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
-    const unsigned grid = (unsigned)(wgs < ncu ? wgs : ncu);
-#define LR_(RNN, W2L, GEN)                                                                                       \
-    do {                                                                                                         \
-        if (tab)                                                                                                 \
-            hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, true>), dim3(grid), dim3(64 * kH2Waves), plan.bytes, s, \
-                               ra);                                                                              \
-        else                                                                                                     \
-            hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, false>), dim3(grid), dim3(64 * kH2Waves), plan.bytes,   \
-                               s, ra);                                                                           \
-    } while (0)
-#define LR2_(RNN)                                                        \
-    do {                                                                 \
-        if (plan.w2l) {                                                  \
-            if (gen) LR_(RNN, true, true); else LR_(RNN, true, false);   \
-        } else {                                                         \
-            if (gen) LR_(RNN, false, true); else LR_(RNN, false, false); \
-        }                                                                \
-    } while (0)
-    if (rnn) LR2_(true); else LR2_(false);
-#undef LR2_
-#undef LR_
-    return hipGetLastError();
+    RolloutLaunch lc;
+    lc.grid = (unsigned)(wgs < ncu ? wgs : ncu);
+    lc.lds = plan.bytes;
+    lc.rnn = rnn;
+    lc.w2l = plan.w2l;
+    lc.gen = st.m % 32 != 0 || st.n % 32 != 0;
+    if (Q) return launch_rollout_q(ra, lc, s);
+    if (tab) return launch_rollout_tab(ra, lc, s);
+    return launch_rollout_inst<false, false>(ra, lc, s);
 }
+#endif  // ASG_H2_TU
 
 }  // namespace asg

@@ -67,7 +67,7 @@ hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], con
                            double *out, hipStream_t s);
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             int32_t *steps_out, hipStream_t s);
+                             int32_t *steps_out, hipStream_t s, int64_t *act_out = nullptr);
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s);
@@ -134,8 +134,8 @@ bool rollout_shape_ok(int n, int m, int L, int K);
 int rollout_l2_slices(int n, int m, int L, int use_rnn);
 hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, int k0, int steps, int select_first,
                           int select_last, int reset, const float4 *packed, const float *b1, const float *bi, const float *bh,
-                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float epsilon,
-                          uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
+                          const float *b2, int use_rnn, const float *Hin, int64_t hs, float *Hout, float *Q,
+                          float epsilon, uint64_t seed, uint32_t counter, int64_t row_base, int *err, hipStream_t s);
 hipError_t launch_rnn_agent_pack(const float *W1, const float *Wih, const float *Whh, const float *W2, int K, int nout,
                                  int use_rnn, float4 *packed, hipStream_t s);
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,

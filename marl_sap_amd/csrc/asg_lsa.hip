@@ -255,20 +255,28 @@ __device__ __forceinline__ int sap_stage(const float *q, int64_t q0, int64_t q1,
     return __builtin_amdgcn_readfirstlane(wave_or_i32(bad)) ? ASG_E_LSA_INVALID : ASG_OK;
 }
 
-// one problem's outputs: the assignment as float32 actions (sap_selectors.py:91-97), -1 on error
+// one problem's outputs: the assignment as float32 actions (sap_selectors.py:91-97), or as
+// the int64 the runner's batch.update casts them to (act_out: the EpisodeBatch actions row);
+// -1 on error
 template <bool kCount>
 __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int steps, int n, int m, float *col_out,
-                                         int32_t *status_out, int32_t *steps_out) {
+                                         int64_t *act_out, int32_t *status_out, int32_t *steps_out) {
     const int lane = threadIdx.x & (kWave - 1);
-    float *co = col_out + b * n;
+    float *co = act_out ? nullptr : col_out + b * n;
+    int64_t *ao = act_out ? act_out + b * n : nullptr;
     if (status == ASG_OK) {
         const int c[1] = {c4r};
-        lsa_emit_wave(c, n, m, nullptr, nullptr, nullptr, co);
+        lsa_emit_wave(c, n, m, nullptr, nullptr, ao, co);
     } else {
-        for (int i = lane; i < n; i += kWave) co[i] = -1.0f;
+        for (int i = lane; i < n; i += kWave) {
+            if (ao) ao[i] = -1;
+            else co[i] = -1.0f;
+        }
     }
     if (kCount && lane == 0) steps_out[b] = steps;
-    if (lane == 0 && status_out) status_out[b] = status;
+    // asg_sap_select_into accumulates: the env's status word keeps its minimum (the first error)
+    // over the episode's calls, read once per episode instead of reduced after every call
+    if (lane == 0 && status_out) status_out[b] = act_out ? min(status_out[b], status) : status;
 }
 
 #ifndef ASG_SAP_PIN
@@ -277,8 +285,8 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
 template <bool kCount>
 __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
-                                                        int64_t env_base, float *col_out, int32_t *status_out,
-                                                        int32_t *steps_out, int64_t B) {
+                                                        int64_t env_base, float *col_out, int64_t *act_out,
+                                                        int32_t *status_out, int32_t *steps_out, int64_t B) {
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
 #if ASG_SAP_PIN
@@ -290,7 +298,7 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
     int c4r[1] = {-1};
     int nsteps = 0;
     if (status == ASG_OK) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
-    sap_emit<kCount>(b, status, c4r[0], nsteps, n, m, col_out, status_out, steps_out);
+    sap_emit<kCount>(b, status, c4r[0], nsteps, n, m, col_out, act_out, status_out, steps_out);
 }
 
 // occupancy experiments: ASG_SAP_LDS_PAD=<bytes> of unused dynamic LDS per 4-wave workgroup
@@ -306,14 +314,14 @@ static size_t sap_lds_pad() {
 
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             int32_t *steps_out, hipStream_t s) {
+                             int32_t *steps_out, hipStream_t s, int64_t *act_out) {
     const size_t pad = sap_lds_pad();
     if (steps_out)
         hipLaunchKernelGGL(sap_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2],
-                           n, m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
+                           n, m, epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
     else
         hipLaunchKernelGGL(sap_select_kernel<false>, lsa_reg_grid(B), dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2],
-                           n, m, epsilon, seed, counter, env_base, col_out, status_out, steps_out, B);
+                           n, m, epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
     return hipGetLastError();
 }
 

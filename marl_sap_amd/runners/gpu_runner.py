@@ -98,9 +98,10 @@ class GpuVecRunner:
     def rollout(self, test_mode=False):
         """One episode of every env, fully asynchronous (no host sync).  When the MAC and env
         allow it the whole loop -- select(0); for t: env.step(t), select(t + 1) -- is ONE
-        kernel (asg_rollout, mode "episode"), or one kernel per step ("step"): the
-        observations are generated on chip and never re-read, and the batch is the separate
-        launches' bit for bit."""
+        kernel (asg_rollout, mode "episode"), or one kernel per step ("step"; "step_q": the
+        env step + agent forward kernel, then the SAP selection kernel): the observations are
+        generated on chip and never re-read, and the batch is the separate launches' bit for
+        bit."""
         self.reset(env_reset=False)
         self.mac.init_hidden(batch_size=self.batch_size)
         mode = self.mac.fused_mode(self.env, self.batch, self.t_env, test_mode) \
@@ -112,7 +113,7 @@ class GpuVecRunner:
             self.env.reset(self.batch, ts=0)
             self.select_into_batch(0, test_mode)
             for t in range(self.T):
-                if mode == "step" and t + 1 < self.T:
+                if mode in ("step", "step_q") and t + 1 < self.T:
                     self.mac.fused_step_select(self.env, self.batch, t, self.t_env, test_mode)
                     continue
                 self.env.step(self.batch, ts=t)

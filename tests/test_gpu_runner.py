@@ -75,7 +75,8 @@ def test_reference_yaml_configs_land_on_the_fast_path(golden, tag):
     T 20, L 3, agent "rnn", use_rnn False, jumpstart_mac with the HAA jumpstart selector, both
     epsilons 1 -> 0 over 20,000 env steps) -- in the same-seed mode, with t_env past both
     anneals: agent "rnn" resolves to the fused kernel module, the IQL episode runs as ONE
-    asg_rollout launch (fused_mode "episode"), and both batches equal the reference
+    asg_rollout launch (fused_mode "episode"), the REDA one as asg_step_forward + the SAP
+    kernel per step (fused_mode "step_q"), and both batches equal the reference
     EpisodeRunner's dumps (tests/golden/yaml_runner_dumps.npz, make_golden.py
     gen_yaml_runner_dumps).  Reference: config/default.yaml:43, algs/mock_constellation_iql.yaml,
     algs/mock_constellation_reda.yaml, runners/episode_runner.py:60-127."""
@@ -110,7 +111,7 @@ def test_reference_yaml_configs_land_on_the_fast_path(golden, tag):
     with torch.no_grad():
         mode = mac.fused_mode(env, probe, runner.t_env)
     np.random.set_state(state)
-    assert mode == ("episode" if sel == "epsilon_greedy" else None), mode
+    assert mode == ("episode" if sel == "epsilon_greedy" else "step_q"), mode
     batch = runner.run(test_mode=False)
     td = {k: v.cpu().numpy() for k, v in batch.data.transition_data.items()}
     for k in ["actions", "actions_onehot", "avail_actions", "terminated", "filled", "prev_assigns"]:

@@ -188,10 +188,10 @@ def test_continuous_selector_cpu():
 @pytest.mark.parametrize("selector", ["epsilon_greedy_sap_test", "sap"])
 def test_jumpstart_flips_keep_reference_stream_order(selector):
     """JumpstartMAC pre-draws an episode's coin flips only when its RL MAC fuses (the
-    epsilon-greedy selector draws nothing from numpy's global stream).  With an RL selector
-    that does draw (EpsilonGreedySAPTestActionSelector, reference sap_selectors.py:36) nothing
-    is pre-drawn: each step draws its flip, then the selector its own -- the reference's
-    order (jumpstart_controller.py:33)."""
+    epsilon-greedy selector and the fused SAP selector draw nothing from numpy's global
+    stream).  With an RL selector that does draw (EpsilonGreedySAPTestActionSelector,
+    reference sap_selectors.py:36) nothing is pre-drawn: each step draws its flip, then the
+    selector its own -- the reference's order (jumpstart_controller.py:33)."""
     from types import SimpleNamespace
     import numpy as np
     import torch
@@ -210,6 +210,13 @@ def test_jumpstart_flips_keep_reference_stream_order(selector):
     np.random.seed(123)
     with torch.no_grad():
         mode = mac.fused_mode(env, batch, 0)
+    if selector == "sap":
+        # the step_q schedule (asg_step_forward + the SAP kernel): the T flips are the stream's
+        # first T draws, consumed in step order
+        assert mode == "step_q"
+        np.random.seed(123)
+        assert mac._flips == list(np.random.rand(T) < 0.5)
+        return
     assert mode is None and mac._flips == []
     # nothing drawn yet: the next draw is the stream's first
     first = np.random.rand()
