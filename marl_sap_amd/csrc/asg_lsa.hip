@@ -289,8 +289,11 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
                                                         int32_t *status_out, int32_t *steps_out, int64_t B) {
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
+#ifndef ASG_SAP_PIN_BASE
+#define ASG_SAP_PIN_BASE 32
+#endif
 #if ASG_SAP_PIN
-    RegColPin<32> rc;  // the column in v[32 .. 95]: one indexed move per row read
+    RegColPin<ASG_SAP_PIN_BASE> rc;  // the column in v[BASE .. BASE + 63]: one indexed move per row read
 #else
     RegCostF32 rc;
 #endif

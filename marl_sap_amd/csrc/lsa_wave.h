@@ -65,6 +65,8 @@ struct RegColPin {
         const int ii = __builtin_amdgcn_readfirstlane(i);
         float x;
         if constexpr (BASE == 32) ASG_PIN_READ(32, 32:63, 64:95);
+        else if constexpr (BASE == 16) ASG_PIN_READ(16, 16:47, 48:79);
+        else if constexpr (BASE == 24) ASG_PIN_READ(24, 24:55, 56:87);
         else if constexpr (BASE == 40) ASG_PIN_READ(40, 40:71, 72:103);
         else if constexpr (BASE == 104) ASG_PIN_READ(104, 104:135, 136:167);
         else if constexpr (BASE == 64) ASG_PIN_READ(64, 64:95, 96:127);

@@ -28,6 +28,14 @@ for v in "rnn:--use-rnn 1:2" "lin:--use-rnn 0:2" "c4:--use-rnn 1:4"; do
   prof sq1_$tag 400 --pmc $SQ1 --output-format csv -d "$OUT/sq1_$tag" -o run -- python3 $B $args --config $cfg $E1
   prof sq2_$tag 400 --pmc $SQ2 --output-format csv -d "$OUT/sq2_$tag" -o run -- python3 $B $args --config $cfg $E1
 done
+# the REDA step schedule's rollout kernel (asg_step_forward, Q written; the Linear agent of
+# mock_constellation_reda.yaml): one launch per step
+for v in "q:--selector sap --use-rnn 0:2"; do
+  tag=${v%%:*}; rest=${v#*:}; args=${rest%:*}; cfg=${rest##*:}
+  prof fetch_$tag 400 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$tag" -o run -- python3 $B $args --config $cfg $E1
+  prof write_$tag 400 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$tag" -o run -- python3 $B $args --config $cfg $E1
+  prof sq1_$tag 400 --pmc $SQ1 --output-format csv -d "$OUT/sq1_$tag" -o run -- python3 $B $args --config $cfg $E1
+done
 prof kt_sap 400 --kernel-trace --stats --output-format csv -d "$OUT/kt_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5
 timeout -k 10 300 python bench.py --selector sap --cpu-baseline 0 --secondary 0 --steps 20 --warmup 5 > "$OUT/bench_sap.log" 2>&1 || exit 1
 prof sq_sap 400 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5
