@@ -371,6 +371,9 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     sel_obj = mac.action_selector
     inner = sel_obj.select_action
 
+    import functools
+
+    @functools.wraps(inner)  # keeps the selector's signature: mac.select_actions still passes `out`
     def timed_select(*args_, **kw):  # the selector call alone (SAP: noise + LSA kernel)
         if not state["timing"]:
             return inner(*args_, **kw)
@@ -517,7 +520,13 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
                 runner.reset()
                 mac.init_hidden(E)
             mac.select_actions(runner.batch, t_ep=t, t_env=runner.t_env)
-        res["path_steps_per_launch"] = int(sel_obj.count_steps.sum().item())
+        # fast-path steps in the low 16 bits, scipy-exact steps (uncertified or rectangular
+        # problems) above (asg_sap_select)
+        cs = sel_obj.count_steps.long()
+        res["path_steps_fast"] = int((cs & 0xFFFF).sum().item())
+        res["path_steps_exact"] = int((cs >> 16).sum().item())
+        res["exact_problems"] = int(((cs >> 16) > 0).sum().item())
+        res["path_steps_per_launch"] = res["path_steps_fast"] + res["path_steps_exact"]
         sel_obj.count_steps = None
     if world > 1:
         # every rank's figures (one all-gather): the job's time is the slowest rank's; the
@@ -574,6 +583,10 @@ def lsa_roofline(a, E, res):
     cyc = SIMDS * CLOCK_HZ * lsa_ms * 1e-3 / steps
     out = {"bound": None, "kernel": "asg::sap_select_kernel", "kernel_ms": round(lsa_ms, 4),
            "path_steps_per_launch": steps, "path_steps_per_s": round(per_s, 1),
+           "path_steps_fast": res.get("path_steps_fast"), "path_steps_exact": res.get("path_steps_exact"),
+           "problems_on_exact_solver": res.get("exact_problems"), "problems": E,
+           "steps_note": "augmenting-path steps of the certified fast path (column reduction + shortest augmenting "
+                         "paths, square problems) and of the scipy-exact solver (uncertified / rectangular problems)",
            "cycles_per_step_per_simd": round(cyc, 1), "achieved": None, "peak": None, "frac": None,
            "unit": "wave-VALU-instr/s", "traffic": None}
     pm = pmc_lookup("*pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
@@ -756,19 +769,19 @@ def main():
                                                 "included"}}
             if rc.get("fused_ms"):
                 tb = 8 * a.n * a.m * E  # one float64 table slice read per env-step (+ its write at the reset)
-                roof = fused_roofline(a, E, rc["fused_ms"], resets_per_step=res_resets(rc))
-                per = roof["bytes_per_launch"] + 2 * tb
-                roof.update({"bytes_per_launch": per, "achieved": round(per / (rc["fused_ms"] * 1e-3) / 1e9, 1),
+                croof = fused_roofline(a, E, rc["fused_ms"], resets_per_step=res_resets(rc))
+                per = croof["bytes_per_launch"] + 2 * tb
+                croof.update({"bytes_per_launch": per, "achieved": round(per / (rc["fused_ms"] * 1e-3) / 1e9, 1),
                              "frac": round(per / (rc["fused_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": None, "kernel": "asg::rollout_kernel<TAB> (+ asg_reset's table draws)",
                              "per_launch_note": "the Philox accounting + 8nm per env-step of table read (one new "
                                                 "float64 slice per step) + 8nm of table write (the reset's T slices "
                                                 "over T steps)"})
-                roof.pop("traffic_pmc", None)
-                roof.pop("traffic_over_algorithmic", None)
-                roof.pop("traffic_note", None)
-                roof.pop("issue", None)
-                leg["roofline"] = roof
+                croof.pop("traffic_pmc", None)
+                croof.pop("traffic_over_algorithmic", None)
+                croof.pop("traffic_note", None)
+                croof.pop("issue", None)
+                leg["roofline"] = croof
             extra["compat"] = leg
 
     if a.selector == "random":

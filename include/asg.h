@@ -209,9 +209,14 @@ int asg_haa_select(const float *beta, const int64_t beta_strides[3], const int64
  * float picked_actions).  Q [B][n][m] f32, any strides.  status_out [B] int32 (0,
  * ASG_E_LSA_INVALID for NaN / +inf entries, ASG_E_LSA_INFEASIBLE), may be NULL; failed envs
  * get -1 rows.  ASG_E_INVALID_ARG when n > m or m > 64 (the Python selector then adds the
- * noise with torch and calls asg_lsa_batched).  path_steps_out [B] int32 (may be NULL):
- * an instrumented instance also writes each env's count of augmenting-path steps (scipy's
- * inner-loop iterations), for the LSA efficiency figure; same assignments. */
+ * noise with torch and calls asg_lsa_batched).  Square problems (n == m) are solved by a
+ * certified fast path (column reduction + shortest augmenting paths, kept only when the
+ * final duals prove the optimum unique by a margin far above float64 rounding, so that
+ * scipy's assignment is the same one), the others and every uncertified problem by the
+ * scipy-exact solver.  path_steps_out [B] int32 (may be NULL): an instrumented instance also
+ * writes each env's count of augmenting-path steps, the fast path's in bits 0..15 and the
+ * scipy-exact solver's (scipy's inner-loop iterations) in bits 16..30, for the LSA
+ * efficiency figure; same assignments. */
 int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                    double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
                    float *col_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
@@ -224,6 +229,12 @@ int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n,
 int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                         double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
                         int64_t *act_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
+/* The matrix asg_sap_select solves for the same arguments: q_out [B][n][m] f32 contiguous =
+ * Q + the selector's noise (parity tooling: the selection at epsilon > 0 is checked against
+ * scipy on it).  status_out [B] (may be NULL): 0 or ASG_E_LSA_INVALID. */
+int asg_sap_noise(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
+                  double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
+                  float *q_out, int32_t *status_out, void *hip_stream);
 
 /* epsilon-greedy over Q [B][n][m] (f32) with availability mask avail [B][n][m] (bool):
  * per row, with probability epsilon a uniformly random available action, else the first

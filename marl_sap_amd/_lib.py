@@ -41,7 +41,8 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_real_get_returns", "asg_real_get_step", "asg_real_obs_size", "asg_filtered_topm",
            "asg_filtered_benefits", "asg_filtered_epsilon_greedy", "asg_filtered_soft_map", "asg_real_haal_select",
            "asg_real_haal_num_sequences", "asg_step_select", "asg_step_select_l2_slices", "asg_rollout",
-           "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward"]
+           "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward",
+           "asg_sap_noise"]
 
 
 class AsgField(ctypes.Structure):
@@ -159,6 +160,7 @@ def lib():
         L.asg_reset_rollout.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, i32, i32, vp, vp, vp, vp, vp, i32, i32,
                                         i32, vp, i64, vp, dbl, u64, u64, vp, vp]
         L.asg_sap_select_into.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp, vp]
+        L.asg_sap_noise.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp]
         L.asg_step_forward.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, vp, vp, vp, vp, vp, i32, i32, i32, vp,
                                        i64, vp, vp, vp]
         for f in EXPORTS:

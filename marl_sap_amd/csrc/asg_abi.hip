@@ -385,6 +385,19 @@ int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, i
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select_into");
 }
 
+int asg_sap_noise(const float *q, const int64_t q_strides[3], int64_t B, int n, int m, double epsilon,
+                  uint64_t seed, uint64_t counter, int64_t env_index_base, float *q_out, int32_t *status_out,
+                  void *hip_stream) {
+    if (!q || !q_strides || !q_out || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_noise: bad arguments");
+    if (n > m || m > 64) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_noise: needs n <= m <= 64");
+    if (!(epsilon >= 0.0)) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_noise: epsilon must be >= 0");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_sap_noise(q, q_strides, B, n, m, (float)epsilon, seed, (uint32_t)counter,
+                                         env_index_base, q_out, status_out, static_cast<hipStream_t>(hip_stream));
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_noise");
+}
+
 int asg_epsilon_greedy(const float *q, const int64_t q_strides[3], const uint8_t *avail,
                        const int64_t avail_strides[3], int64_t B, int n, int m, double epsilon, uint64_t seed,
                        uint64_t counter, int64_t env_index_base, int64_t *out, const int64_t out_strides[2],

@@ -555,6 +555,177 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 #endif
 }
 
+// ------------------------------------------------------------------------------------
+// Certified fast path for square register-resident problems (nr == nc <= 64).
+//
+// scipy's algorithm starts every row's Dijkstra from u = v = 0 and an empty matching; on
+// SAP Q-values (one shared task profile, small per-agent terms) that costs ~1,400
+// augmenting-path steps per 64 x 64 problem.  Here the SAME shortest-augmenting-path step
+// runs from a column reduction instead (v_j = min_i c_ij, u = 0: dual feasible; each row
+// keeps the column of smallest v among those whose minimum it holds: complementary slack),
+// so only the rows the reduction leaves free are augmented: ~0.5x the steps on SAP-like
+// matrices (tools/lsa_fastpath_sim.py).  Ties among equal path costs go to the lowest lane:
+// any shortest-path choice yields AN optimal assignment.
+//
+// Which optimum scipy returns only matters when the optimum is not unique, so the result is
+// used only under a uniqueness certificate computed from the final duals (u, v), with
+// S = max|c| + max|u| + max|v| and reduced costs rc_ij = (c_ij - u_i) - v_j:
+//   (1) rc_ij >= -S 2^-30 everywhere and rc <= S 2^-30 on the matching (dual feasibility
+//       and complementary slackness up to rounding);
+//   (2) the graph "column x_i -> column j" over the near-tight edges (rc_ij <= S 2^-20,
+//       j != x_i) is acyclic (peeled sink by sink).
+// Every other assignment differs from this one by alternating cycles, each of which
+// contains a non-tight edge by (2), so its cost exceeds this one's by more than S 2^-21
+// (exact arithmetic on the float64 working matrix; the rounding of rc and the slack of (1)
+// are a few S 2^-30).  scipy's float64 run ends at an assignment whose cost is within a few
+// thousand ulp(S) (< S 2^-40) of the optimum, so it is this one.  When (1) or (2) fails
+// (exact or near ties, NaN) the caller runs the scipy-exact solver from scratch.
+// Returns ASG_OK (col4row set), or kLsaUncertified.  `slot`: 64 uint64 of LDS scratch for
+// this wave.
+constexpr int kLsaUncertified = 1;
+
+__device__ __forceinline__ double lane_dbl(double x, int src) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    return dbl_of((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src),
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src));
+}
+
+template <class Acc, bool kCount = false>
+__device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *steps, uint64_t *slot) {
+    int nsteps = 0;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool live = lane < n;
+    const uint64_t colmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+    const float kOutF = __builtin_bit_cast(float, 0x7fc00000u);
+    // column reduction over the register-resident column (static register reads)
+    float cmin = __builtin_inff(), amax = 0.0f;
+    int imin = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const float x = acc.lo[k];
+        const bool t = k < n && x < cmin;
+        cmin = t ? x : cmin;
+        imin = t ? k : imin;
+        amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const float x = acc.hi[k];
+        const bool t = k + 32 < n && x < cmin;
+        cmin = t ? x : cmin;
+        imin = t ? k + 32 : imin;
+        amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+    }
+    // each row keeps the column of smallest v (then lowest index) among those whose minimum it
+    // holds: one 64-bit LDS minimum per column on (order-preserving v bits, column)
+    slot[lane] = ~0ull;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const uint32_t cb = __builtin_bit_cast(uint32_t, cmin);
+    const uint64_t key = ((uint64_t)((cb & 0x80000000u) ? ~cb : (cb | 0x80000000u)) << 32) | (uint32_t)lane;
+    if (live) atomicMin(reinterpret_cast<unsigned long long *>(&slot[imin]), (unsigned long long)key);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t won = slot[imin], mine = slot[lane];
+    int r4c = (live && won == key) ? imin : -1;
+    int c4r = (live && mine != ~0ull) ? (int)(uint32_t)mine : -1;
+    double v = live ? (double)cmin : 0.0, u = 0.0;
+    int path = -1;
+    uint64_t freerows = __ballot(live && c4r < 0);
+    int ncand = 1;
+    uint32_t lowest_hi = 0;
+    while (freerows != 0) {
+        const int cur = sff1(freerows);
+        asm("s_bitset0_b64 %0, %1" : "+s"(freerows) : "s"(cur) : "scc");
+        double spc = __builtin_inf();
+        uint64_t rem = colmask;
+        double minv = 0.0;
+        int i = cur, jsel;
+        do {
+            i = __builtin_amdgcn_readfirstlane(i);
+            if (kCount) ++nsteps;
+            const double ui = lane_dbl(u, i);
+            const bool remb = __builtin_amdgcn_inverse_ballot_w64(rem);
+            const double r = ((minv + acc.col(i)) - ui) - v;
+            const bool upd = remb && r < spc;
+            spc = upd ? r : spc;
+            path = upd ? i : path;
+            const float fkey = remb ? (float)spc : kOutF;
+            const float kmin = wave_min_f32_nonan(fkey);
+            const uint64_t cm = __ballot(fkey == kmin);
+            asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
+            const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
+            jsel = sff1(cm);
+            uint32_t lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
+            lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
+            if (ncand != 1) {
+                // equal keys: any column at the exact float64 minimum is a shortest-path choice
+                if ((__ballot(spc != dbl_of(lowest_lo, lowest_hi)) & cm) != 0) {
+                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(remb ? spc : __builtin_inf()));
+                    lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
+                    lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
+                    jsel = sff1(__ballot(spc == dbl_of(lowest_lo, lowest_hi)) & rem) & 63;
+                }
+                if (ncand == 0) lowest_hi = 0x7ff00000u;  // NaN mid-solve: leave, uncertified
+            }
+            asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(jsel) : "scc");
+            minv = dbl_of(lowest_lo, lowest_hi);
+            i = __builtin_amdgcn_readlane(r4c, jsel);
+        } while (__builtin_elementwise_min((uint32_t)(i + 1), lowest_hi ^ 0x7ff00000u) != 0u);
+        if (ncand == 0 || lowest_hi == 0x7ff00000u) {
+            if (kCount) *steps = nsteps;
+            return kLsaUncertified;
+        }
+        const int sink = jsel;
+        // scipy's dual update (u[cur] += minv; visited rows u[r] += minv - spc[col4row[r]];
+        // scanned columns v[j] -= minv - spc[j]) and augmentation, as lsa_solve_reg64
+        const int jm = c4r;
+        const double spc_j = __shfl(spc, jm & 63, kWave);
+        const bool sc_j = jm >= 0 && ((rem >> (jm & 63)) & 1ull) == 0;
+        if (live) {
+            if (lane == cur) u += minv;
+            else if (sc_j) u += minv - spc_j;
+        }
+        if (live && ((rem >> lane) & 1ull) == 0) v -= minv - spc;
+        int j = sink;
+        while (true) {
+            const int pi = __builtin_amdgcn_readlane(path, j);
+            r4c = (lane == j) ? pi : r4c;
+            const int t = __builtin_amdgcn_readlane(c4r, pi);
+            c4r = (lane == pi) ? j : c4r;
+            j = t;
+            if (pi == cur) break;
+        }
+    }
+    if (kCount) *steps = nsteps;
+    // the certificate
+    const float am = wave_max_f32_nonan(amax);
+    const double ua = wave_allreduce(live ? __builtin_fabs(u) : 0.0, [](double a, double b) { return fmax(a, b); });
+    const double va = wave_allreduce(live ? __builtin_fabs(v) : 0.0, [](double a, double b) { return fmax(a, b); });
+    const double S = ((double)am + ua) + va;
+    if (!(S < __builtin_inf())) return kLsaUncertified;
+    const double tight = S * 0x1p-20, slack = S * 0x1p-30;
+    uint64_t adj = 0;  // lane c (a column, matched to row r4c): the columns j != c with rc(r4c, j) <= tight
+    int bad = 0;
+    for (int i = 0; i < n; ++i) {
+        const double ui = lane_dbl(u, i);
+        const int xi = __builtin_amdgcn_readlane(c4r, i);
+        const double rc = ((double)acc.col(i) - ui) - v;
+        bad |= (live && !(rc >= -slack)) | (lane == xi && !(rc <= slack));
+        const uint64_t eq = __ballot(live && lane != xi && rc <= tight);
+        adj = lane == xi ? eq : adj;
+    }
+    if (wave_or_i32(bad)) return kLsaUncertified;
+    // peel the columns without an out-edge into the remaining set until none is left (acyclic)
+    // or none can go (a cycle: another optimum within S 2^-20)
+    uint64_t A = colmask;
+    while (A != 0) {
+        const uint64_t nA = __ballot(((A >> lane) & 1ull) != 0 && (adj & A) != 0);
+        if (nA == A) return kLsaUncertified;
+        A = nA;
+    }
+    col4row[0] = c4r;
+    return ASG_OK;
+}
+
 // Stage C (input [nr0][nc0], strides in elements) into dst as scipy's working matrix:
 // transposed when nr0 > nc0, negated for maximize.  Returns ASG_E_LSA_INVALID (wave
 // uniform) when an entry is NaN or -inf after the sign flip.

@@ -114,3 +114,75 @@ def _sap_raw(q, eps, seed, counter, base=0):
                                          p(out), p(st), p(steps), _lib.stream_ptr(DEV)))
     torch.cuda.synchronize()
     return out, st, steps
+
+
+def _noisy(q, eps, seed, counter, base=0):
+    """asg_sap_noise: the matrix the selector solves for these arguments"""
+    import ctypes
+    from marl_sap_amd import _lib
+    B, n, m = q.shape
+    out = torch.empty((B, n, m), dtype=torch.float32, device=DEV)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(_lib.lib().asg_sap_noise(p(q), _lib.i64arr(q.stride()), B, n, m, float(eps), seed, counter, base,
+                                        p(out), None, _lib.stream_ptr(DEV)))
+    return out
+
+
+@pytest.mark.parametrize("B,n,m,eps,kind", [
+    (2048, 64, 64, 0.05, "sap"),     # configs[2]'s SAP selection: the certified fast path
+    (2048, 64, 64, 0.0, "sap"),
+    (1024, 64, 64, 1.0, "sap"),
+    (1024, 64, 64, 0.05, "uniform"),
+    (1024, 16, 16, 0.3, "sap"),      # configs[1]'s shape
+    (1024, 33, 33, 0.2, "uniform"),  # odd square size (padding lanes)
+    (1024, 20, 25, 0.2, "sap"),      # rectangular: the scipy-exact solver alone
+])
+def test_sap_noisy_selection_is_scipy(B, n, m, eps, kind):
+    """At epsilon > 0 the selection equals scipy's LSA(maximize) of exactly the noisy matrix
+    the kernel formed (asg_sap_noise), env by env -- whichever solver ran (the certified fast
+    path for square problems, the scipy-exact one otherwise)."""
+    rng = np.random.RandomState(B + n + m)
+    q = sap_like_q(rng, B, n, m) if kind == "sap" else rng.rand(B, n, m).astype(np.float32)
+    qd = torch.as_tensor(q, device=DEV)
+    out, st, steps = _sap_raw(qd, eps, 5, 3, base=100)
+    noisy = _noisy(qd, eps, 5, 3, base=100).cpu().numpy()
+    out, st, steps = out.cpu().numpy(), st.cpu().numpy(), steps.cpu().numpy()
+    assert (st == 0).all()
+    for b in range(B):
+        assert np.array_equal(out[b], ora.lsa(noisy[b].astype(np.float64), maximize=True)[1].astype(np.float32)), b
+    fast, exact = steps & 0xFFFF, steps >> 16
+    if n == m:
+        assert (fast > 0).all()
+        assert (exact == 0).mean() > 0.95, (exact > 0).mean()  # almost every problem certified
+    else:
+        assert (fast == 0).all() and (exact > 0).all()
+
+
+def test_sap_fast_path_falls_back_on_ties():
+    """Square problems with exact ties (integer Q: several optimal assignments) fail the
+    uniqueness certificate and take the scipy-exact solver: scipy's tie rule is kept."""
+    rng = np.random.RandomState(9)
+    B, n = 512, 64
+    q = rng.randint(0, 4, size=(B, n, n)).astype(np.float32)
+    q[: B // 2] += rng.randint(0, 3, size=(B // 2, 1, n)).astype(np.float32)
+    out, st, steps = _sap_raw(torch.as_tensor(q, device=DEV), 0.0, 1, 1)
+    out, steps = out.cpu().numpy(), steps.cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(out[b], ora.lsa(q[b].astype(np.float64), maximize=True)[1].astype(np.float32)), b
+    assert ((steps >> 16) > 0).mean() > 0.9  # ties: the exact solver ran
+
+
+def test_sap_fast_path_full_size():
+    """configs[2]'s selection size, 16,384 envs of 64 x 64 at epsilon 0.05: every env equals
+    scipy on its noisy matrix (oracle, C), and the fast path's step count is reported."""
+    rng = np.random.RandomState(77)
+    B = 16384
+    q = torch.as_tensor(sap_like_q(rng, B, 64, 64), device=DEV)
+    out, st, steps = _sap_raw(q, 0.05, 2, 7)
+    noisy = _noisy(q, 0.05, 2, 7).cpu().numpy()
+    out, steps = out.cpu().numpy(), steps.cpu().numpy()
+    assert (st.cpu().numpy() == 0).all()
+    for b in range(B):
+        col = ora.lsa(noisy[b].astype(np.float64), maximize=True)[1]
+        assert np.array_equal(out[b], col.astype(np.float32)), b
+    assert ((steps >> 16) == 0).mean() > 0.99
