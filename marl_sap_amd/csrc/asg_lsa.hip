@@ -16,6 +16,14 @@ namespace asg {
 
 constexpr size_t kLdsCostBudget = 48 * 1024;
 
+// square SAP problems (sap_select_kernel, n == m) first take the certified fast path
+// (lsa_fast_reg64: column
+// reduction + shortest augmenting paths, used under a uniqueness certificate), the rest and
+// every uncertified problem the scipy-exact solver; -DASG_SAP_FAST=0: the exact solver only
+#ifndef ASG_SAP_FAST
+#define ASG_SAP_FAST 1
+#endif
+
 // working matrix read in place: transposed when nr0 > nc0, negated for maximize
 template <typename IT>
 struct GlobalCost {
@@ -280,58 +288,33 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
 }
 
 #ifndef ASG_SAP_PIN
-#define ASG_SAP_PIN 0
+#define ASG_SAP_PIN 1
 #endif
-// square problems (n == m) first take the certified fast path (lsa_fast_reg64: column
-// reduction + shortest augmenting paths, used under a uniqueness certificate), the rest and
-// every uncertified problem the scipy-exact solver; -DASG_SAP_FAST=0: the exact solver only
-#ifndef ASG_SAP_FAST
-#define ASG_SAP_FAST 1
-#endif
-// Persistent grid (one resident slot per wave) pulling problems from a ticket counter: path
-// lengths vary several-fold between problems, so a static problem-per-wave grid idles its
-// slots in the last round.  Every wave draws tickets until one is past the last problem; the
-// wave holding the last ticket of the launch (B + waves - 1) resets the counter for the next
-// launch that uses this slot.
 template <bool kCount>
 __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
                                                         int64_t env_base, float *col_out, int64_t *act_out,
-                                                        int32_t *status_out, int32_t *steps_out, int64_t B,
-                                                        unsigned *ticket) {
+                                                        int32_t *status_out, int32_t *steps_out, int64_t B) {
     __shared__ uint64_t s_slot[kLsaWpb][64];
-    const int lane = threadIdx.x & (kWave - 1);
-    const unsigned last = (unsigned)B + gridDim.x * kLsaWpb - 1u;
-    for (;;) {
-        unsigned tk = 0;
-        if (lane == 0) tk = atomicAdd(ticket, 1u);
-        tk = __builtin_amdgcn_readfirstlane(tk);
-        if (tk >= (unsigned)B) {
-            if (tk == last && lane == 0) atomicExch(ticket, 0u);
-            break;
-        }
-        const int64_t b = tk;
-        // nothing derived from the launch arguments stays live across problems (the loop would
-        // otherwise hoist it into registers the solver needs)
-        asm volatile("" : "+s"(q), "+s"(n), "+s"(m), "+s"(epsilon), "+s"(seed), "+s"(counter), "+s"(env_base));
+    const int64_t b = lsa_reg_problem();
+    if (b >= B) return;
 #ifndef ASG_SAP_PIN_BASE
 #define ASG_SAP_PIN_BASE 32
 #endif
 #if ASG_SAP_PIN
-        RegColPin<ASG_SAP_PIN_BASE> rc;  // the column in v[BASE .. BASE + 63]: one indexed move per row read
+    RegColPin<ASG_SAP_PIN_BASE> rc;  // the column in v[BASE .. BASE + 63]: one indexed move per row read
 #else
-        RegCostF32 rc;
+    RegCostF32 rc;
 #endif
-        int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
-        int c4r[1] = {-1};
-        int nsteps = 0, nfast = 0;
-        bool done = false;
-        if (ASG_SAP_FAST && status == ASG_OK && n == m)
-            done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
-        if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
-        // instrumented instance: fast-path steps in the low 16 bits, scipy-exact steps above
-        sap_emit<kCount>(b, status, c4r[0], nfast | (nsteps << 16), n, m, col_out, act_out, status_out, steps_out);
-    }
+    int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
+    int c4r[1] = {-1};
+    int nsteps = 0, nfast = 0;
+    bool done = false;
+    if (ASG_SAP_FAST && status == ASG_OK && n == m)
+        done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
+    if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
+    // instrumented instance: fast-path steps in the low 16 bits, scipy-exact steps above
+    sap_emit<kCount>(b, status, c4r[0], nfast | (nsteps << 16), n, m, col_out, act_out, status_out, steps_out);
 }
 
 // the noisy Q the selector solves (Q + its noise, as sap_stage forms it): parity tooling,
@@ -374,44 +357,17 @@ static size_t sap_lds_pad() {
     return v;
 }
 
-// ticket counters of the persistent SAP grid: a pool per device, one slot per launch in flight
-// (launches on different streams may overlap), each left at zero by the launch that used it
-constexpr int kSapTicketSlots = 64;
-static hipError_t sap_ticket(unsigned **out) {
-    static unsigned *pool[64] = {nullptr};
-    static unsigned next[64] = {0};
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (!pool[dev]) {
-        unsigned *p = nullptr;
-        if ((e = hipMalloc(&p, sizeof(unsigned) * kSapTicketSlots)) != hipSuccess) return e;
-        if ((e = hipMemset(p, 0, sizeof(unsigned) * kSapTicketSlots)) != hipSuccess) return e;
-        pool[dev] = p;
-    }
-    *out = pool[dev] + (next[dev]++ % kSapTicketSlots);
-    return hipSuccess;
-}
-
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
                              int32_t *steps_out, hipStream_t s, int64_t *act_out) {
-    if (B >= (1ll << 31)) return hipErrorInvalidValue;
-    unsigned *ticket = nullptr;
-    hipError_t e = sap_ticket(&ticket);
-    if (e != hipSuccess) return e;
-    // resident capacity: ASG_LSA_REG_WAVES waves per SIMD, kLsaWpb waves per workgroup
-    const int64_t cap = (int64_t)stream_cus(s) * 4 * ASG_LSA_REG_WAVES / kLsaWpb;
-    const int64_t need = (B + kLsaWpb - 1) / kLsaWpb;
-    const dim3 grid((unsigned)(need < cap ? need : cap));
+    const dim3 grid = lsa_reg_grid(B);
     const size_t pad = sap_lds_pad();
     if (steps_out)
         hipLaunchKernelGGL(sap_select_kernel<true>, grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m,
-                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B, ticket);
+                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
     else
         hipLaunchKernelGGL(sap_select_kernel<false>, grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m,
-                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B, ticket);
+                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
     return hipGetLastError();
 }
 

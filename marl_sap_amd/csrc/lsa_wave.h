@@ -570,16 +570,18 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 // Which optimum scipy returns only matters when the optimum is not unique, so the result is
 // used only under a uniqueness certificate computed from the final duals (u, v), with
 // S = max|c| + max|u| + max|v| and reduced costs rc_ij = (c_ij - u_i) - v_j:
-//   (1) rc_ij >= -S 2^-30 everywhere and rc <= S 2^-30 on the matching (dual feasibility
-//       and complementary slackness up to rounding);
-//   (2) the graph "column x_i -> column j" over the near-tight edges (rc_ij <= S 2^-20,
-//       j != x_i) is acyclic (peeled sink by sink).
+//   (1) rc_ij >= -S 2^-40 everywhere and rc <= S 2^-40 on the matching (dual feasibility and
+//       complementary slackness up to rounding: each dual carries at most ~2 roundings per
+//       augmentation, < S 2^-46 after 64 of them);
+//   (2) the graph "row i -> row owning column j" over the near-tight edges (rc_ij <= S 2^-30,
+//       j not i's column) is acyclic (peeled source by source).
 // Every other assignment differs from this one by alternating cycles, each of which
-// contains a non-tight edge by (2), so its cost exceeds this one's by more than S 2^-21
-// (exact arithmetic on the float64 working matrix; the rounding of rc and the slack of (1)
-// are a few S 2^-30).  scipy's float64 run ends at an assignment whose cost is within a few
-// thousand ulp(S) (< S 2^-40) of the optimum, so it is this one.  When (1) or (2) fails
-// (exact or near ties, NaN) the caller runs the scipy-exact solver from scratch.
+// contains a non-tight edge by (2), so its cost exceeds this one's by more than
+// S 2^-30 - 128 S 2^-40 > S 2^-31 (exact arithmetic on the float64 working matrix).  scipy's
+// float64 run makes the same kind of roundings (< S 2^-46 per reduced cost), so its result is
+// optimal to within 64 such errors (< S 2^-39) -- 2^8 below the margin: it is this
+// assignment.  When (1) or (2) fails (exact or near ties, NaN) the caller runs the
+// scipy-exact solver from scratch.
 // Returns ASG_OK (col4row set), or kLsaUncertified.  `slot`: 64 uint64 of LDS scratch for
 // this wave.
 constexpr int kLsaUncertified = 1;
@@ -696,31 +698,42 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
         }
     }
     if (kCount) *steps = nsteps;
+#ifdef ASG_LSA_FAST_NOCERT  // timing experiments only: what the certificate costs (wrong on ties)
+    col4row[0] = c4r;
+    return ASG_OK;
+#endif
     // the certificate
     const float am = wave_max_f32_nonan(amax);
     const double ua = wave_allreduce(live ? __builtin_fabs(u) : 0.0, [](double a, double b) { return fmax(a, b); });
     const double va = wave_allreduce(live ? __builtin_fabs(v) : 0.0, [](double a, double b) { return fmax(a, b); });
     const double S = ((double)am + ua) + va;
     if (!(S < __builtin_inf())) return kLsaUncertified;
-    const double tight = S * 0x1p-20, slack = S * 0x1p-30;
-    uint64_t adj = 0;  // lane c (a column, matched to row r4c): the columns j != c with rc(r4c, j) <= tight
-    int bad = 0;
-    for (int i = 0; i < n; ++i) {
-        const double ui = lane_dbl(u, i);
-        const int xi = __builtin_amdgcn_readlane(c4r, i);
-        const double rc = ((double)acc.col(i) - ui) - v;
-        bad |= (live && !(rc >= -slack)) | (lane == xi && !(rc <= slack));
-        const uint64_t eq = __ballot(live && lane != xi && rc <= tight);
-        adj = lane == xi ? eq : adj;
+    const double tight = S * 0x1p-30, slack = S * 0x1p-40;
+    // lane j (column j, matched to row r4c) collects tin: the rows i != r4c whose edge (i, j) is
+    // near-tight -- the in-edges of node r4c in the graph "row i -> row r4c(j)" -- from its own
+    // register column, four rows at a time
+    uint64_t tin = 0;
+    bool bad = false;
+    for (int k0 = 0; k0 < n; k0 += 4) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {  // four independent rows per iteration
+            const int k = __builtin_amdgcn_readfirstlane(k0 + kk);
+            const double rc = ((double)acc.col(k) - lane_dbl(u, k)) - v;
+            const bool row = live && k < n;
+            bad |= (row && !(rc >= -slack)) | (k == r4c && !(rc <= slack));
+            tin |= (row && k != r4c && rc <= tight) ? 1ull << k : 0ull;
+        }
     }
     if (wave_or_i32(bad)) return kLsaUncertified;
-    // peel the columns without an out-edge into the remaining set until none is left (acyclic)
-    // or none can go (a cycle: another optimum within S 2^-20)
+    // peel the sources (alive rows with no near-tight in-edge from an alive row) until none is
+    // left (acyclic) or none can go (a cycle: another optimum within S 2^-30).  Lane j speaks for
+    // row r4c; lane i learns whether its own row left through its column c4r.
     uint64_t A = colmask;
     while (A != 0) {
-        const uint64_t nA = __ballot(((A >> lane) & 1ull) != 0 && (adj & A) != 0);
-        if (nA == A) return kLsaUncertified;
-        A = nA;
+        const uint64_t srcc = __ballot(live && ((A >> (r4c & 63)) & 1ull) != 0 && (tin & A) == 0);
+        const uint64_t gone = __ballot(live && ((srcc >> (c4r & 63)) & 1ull) != 0);
+        if (gone == 0) return kLsaUncertified;
+        A &= ~gone;
     }
     col4row[0] = c4r;
     return ASG_OK;

@@ -6,7 +6,7 @@ set -o pipefail
 OUT=${1:-gpurun_out/sapfast}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sap.py \
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_sap.py tests/test_gpu_parity.py tests/test_gpu_learner.py \
     tests/test_gpu_step_q.py > "$OUT/tests.log" 2>&1 || { echo "FAILED tests"; grep -E "FAILED|Error|assert" "$OUT/tests.log" | head -20; tail -5 "$OUT/tests.log"; exit 1; }
 tail -1 "$OUT/tests.log"
 for rep in 1 2; do

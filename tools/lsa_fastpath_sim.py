@@ -9,7 +9,7 @@ matrices, it counts the augmenting-path steps of
   * the certified fast path (csrc/lsa_wave.h lsa_fast_reg64): column reduction, then the same
     shortest-augmenting-path step for the rows it leaves free only,
 checks both assignments against scipy, and evaluates the fast path's uniqueness certificate
-(dual feasibility within S 2^-30, acyclic near-tight graph at S 2^-20).  The kernel's steps
+(dual feasibility within S 2^-40, acyclic near-tight graph at S 2^-30).  The kernel's steps
 and certificate are this model's; the GPU figures are bench.py's roofline_lsa.
 """
 import argparse
@@ -117,7 +117,7 @@ def fast_path(C):
                 break
     rc = (C - u[:, None]) - v[None, :]
     S = np.abs(C).max() + np.abs(u).max() + np.abs(v).max()
-    tight, slack = S * 2.0 ** -20, S * 2.0 ** -30
+    tight, slack = S * 2.0 ** -30, S * 2.0 ** -40
     ok = rc.min() >= -slack and np.abs(rc[np.arange(n), x]).max() <= slack
     adj = np.zeros((n, n), bool)  # column x_i -> column j over near-tight edges
     for i in range(n):
