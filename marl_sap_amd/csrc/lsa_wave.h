@@ -561,10 +561,10 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 // scipy's algorithm starts every row's Dijkstra from u = v = 0 and an empty matching; on
 // SAP Q-values (one shared task profile, small per-agent terms) that costs ~1,400
 // augmenting-path steps per 64 x 64 problem.  Here the SAME shortest-augmenting-path step
-// runs from a column reduction instead (v_j = min_i c_ij, u = 0: dual feasible; each row
-// keeps the column of smallest v among those whose minimum it holds: complementary slack),
-// so only the rows the reduction leaves free are augmented: ~0.5x the steps on SAP-like
-// matrices (tools/lsa_fastpath_sim.py).  Ties among equal path costs go to the lowest lane:
+// runs from a row + column reduction instead (u_i = min_j c_ij, v_j = min_i (c_ij - u_i): dual
+// feasible; each row keeps a column whose minimum it holds: complementary slack), so only the
+// rows the reduction leaves free are augmented: ~0.4x the steps on SAP-like matrices
+// (tools/lsa_fastpath_sim.py).  Ties among equal path costs go to the lowest lane:
 // any shortest-path choice yields AN optimal assignment.
 //
 // Which optimum scipy returns only matters when the optimum is not unique, so the result is
@@ -599,37 +599,37 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
     const bool live = lane < n;
     const uint64_t colmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
     const float kOutF = __builtin_bit_cast(float, 0x7fc00000u);
-    // column reduction over the register-resident column (static register reads)
-    float cmin = __builtin_inff(), amax = 0.0f;
+    // row reduction (u_k = min_j c_kj, float32: exact) then column reduction of the rest
+    // (v_j = min_k (c_kj - u_k), float64: exact for float32 operands): both the agents' and the
+    // tasks' common offsets come out, so the column minima spread over more rows than a column
+    // reduction alone leaves them (SAP Q: -16..28 % augmenting-path steps in the host model)
+    float amax = 0.0f;
+    double vmin = __builtin_inf(), u = 0.0;
     int imin = 0;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const float x = acc.lo[k];
-        const bool t = k < n && x < cmin;
-        cmin = t ? x : cmin;
-        imin = t ? k : imin;
-        amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+    for (int k = 0; k < 64; ++k) {
+        if (k < n) {
+            const float x = k < 32 ? acc.lo[k] : acc.hi[k - 32];
+            const float uk = wave_min_f32_nonan(live ? x : __builtin_inff());
+            u = lane == k ? (double)uk : u;
+            const double r = (double)x - (double)uk;
+            const bool t = r < vmin;
+            vmin = t ? r : vmin;
+            imin = t ? k : imin;
+            amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+        }
     }
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const float x = acc.hi[k];
-        const bool t = k + 32 < n && x < cmin;
-        cmin = t ? x : cmin;
-        imin = t ? k + 32 : imin;
-        amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
-    }
-    // each row keeps the column of smallest v (then lowest index) among those whose minimum it
-    // holds: one 64-bit LDS minimum per column on (order-preserving v bits, column)
-    slot[lane] = ~0ull;
+    // each row keeps one of the columns whose minimum it holds (the lowest: any keeps
+    // complementary slackness, rc = 0 there): one LDS minimum per column
+    uint32_t *slot32 = reinterpret_cast<uint32_t *>(slot);
+    slot32[lane] = 0xffffffffu;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const uint32_t cb = __builtin_bit_cast(uint32_t, cmin);
-    const uint64_t key = ((uint64_t)((cb & 0x80000000u) ? ~cb : (cb | 0x80000000u)) << 32) | (uint32_t)lane;
-    if (live) atomicMin(reinterpret_cast<unsigned long long *>(&slot[imin]), (unsigned long long)key);
+    if (live) atomicMin(&slot32[imin], (uint32_t)lane);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t won = slot[imin], mine = slot[lane];
-    int r4c = (live && won == key) ? imin : -1;
-    int c4r = (live && mine != ~0ull) ? (int)(uint32_t)mine : -1;
-    double v = live ? (double)cmin : 0.0, u = 0.0;
+    const uint32_t won = slot32[imin], mine = slot32[lane];
+    int r4c = (live && won == (uint32_t)lane) ? imin : -1;
+    int c4r = (live && mine != 0xffffffffu) ? (int)mine : -1;
+    double v = live ? vmin : 0.0;
     int path = -1;
     uint64_t freerows = __ballot(live && c4r < 0);
     int ncand = 1;

@@ -6,8 +6,8 @@ For SAP-selector matrices (Q of a random-init RNNAgent on the mock env's observa
 the C oracle env, plus the selector's Gaussian noise of std 2 eps mean|Q|) and for uniform
 matrices, it counts the augmenting-path steps of
   * scipy's algorithm (every row's Dijkstra from u = v = 0; csrc/lsa_wave.h lsa_solve_reg64),
-  * the certified fast path (csrc/lsa_wave.h lsa_fast_reg64): column reduction, then the same
-    shortest-augmenting-path step for the rows it leaves free only,
+  * the certified fast path (csrc/lsa_wave.h lsa_fast_reg64): row + column reduction, then the
+    same shortest-augmenting-path step for the rows it leaves free only,
 checks both assignments against scipy, and evaluates the fast path's uniqueness certificate
 (dual feasibility within S 2^-40, acyclic near-tight graph at S 2^-30).  The kernel's steps
 and certificate are this model's; the GPU figures are bench.py's roofline_lsa.
@@ -72,15 +72,15 @@ def scipy_steps(C):
 def fast_path(C):
     """lsa_fast_reg64: (assignment, steps, certified)."""
     n = C.shape[0]
-    v = C.min(0).copy()
-    imin = C.argmin(0)
+    u = C.min(1).copy()  # row reduction
+    R = C - u[:, None]
+    v = R.min(0).copy()  # column reduction of the rest
+    imin = R.argmin(0)
     x, y = -np.ones(n, int), -np.ones(n, int)
-    for i in range(n):  # each row keeps the column of smallest v (then lowest index) it is the minimum of
+    for i in range(n):  # each row keeps the lowest column whose minimum it holds
         js = np.where(imin == i)[0]
         if len(js):
-            j = js[np.argmin(v[js])]
-            x[i], y[j] = j, i
-    u = np.zeros(n)
+            x[i], y[js[0]] = js[0], i
     path = -np.ones(n, int)
     steps = 0
     for cur in [i for i in range(n) if x[i] < 0]:
