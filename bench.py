@@ -191,6 +191,23 @@ def reset_bytes(n, m, L):
     return n * m * (4 * (L + 1) + 4 + 1) + 8 * n + 8
 
 
+def store_ceiling():
+    """The measured HBM store ceiling (GB/s): the best shape of the newest tools/store_bw.hip
+    record under profiles/ (store-only streams over a 4 GiB buffer), with the file name."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*store_bw*.txt")), key=profile_order, reverse=True)
+    for f in files:
+        best = 0.0
+        for line in open(f):
+            if line.startswith("{"):
+                try:
+                    best = max(best, float(json.loads(line)["GBps"]))
+                except (ValueError, KeyError):
+                    pass
+        if best > 0:
+            return best, os.path.basename(f)
+    return None, None
+
+
 def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=False):
     """Roofline of the fused rollout kernel (asg_rollout -> rollout_kernel), per env step: the
     env step's bytes plus the agent's h in / h out and the action written -- the observations
@@ -245,6 +262,16 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
                               "the fused resets' rows amortised over the timed steps)",
            "resets_per_step": round(resets_per_step, 4),
            "frac_note": "frac is against the 8 TB/s HBM peak"}
+    # the kernel writes almost all of its bytes: against the measured store ceiling too (writes
+    # = the rows, h out, the action, Q; reads = h in)
+    ceil, ceil_src = store_ceiling()
+    if ceil:
+        reads = (a.n * 4 * 64 if use_rnn else 0) * E
+        writes = per_launch - reads - 8 * a.n * E  # B_step counts the actions row as a read: it stays in LDS
+        wgbs = writes / (fused_ms * 1e-3) / 1e9
+        out["store_ceiling"] = {"write_bytes_per_launch": int(writes), "achieved_write_GBps": round(wgbs, 1),
+                                "ceiling_GBps": ceil, "frac": round(wgbs / ceil, 4), "source": ceil_src,
+                                "note": "HBM store-only ceiling measured by tools/store_bw.hip on MI355X"}
     if pm:
         out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
         out["traffic_over_algorithmic"] = round(traffic / per_launch, 4)
