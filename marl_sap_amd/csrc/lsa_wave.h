@@ -639,37 +639,50 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
         asm("s_bitset0_b64 %0, %1" : "+s"(freerows) : "s"(cur) : "scc");
         double spc = __builtin_inf();
         uint64_t rem = colmask;
-        double minv = 0.0;
+        // the distance of the last scanned column (minv), kept as its two words
+        uint32_t lowest_lo = 0;
+        lowest_hi = 0;
+        const uint64_t freec = __ballot(live && r4c < 0);  // unassigned columns: a tie among them ends the search
         int i = cur, jsel;
         do {
             i = __builtin_amdgcn_readfirstlane(i);
             if (kCount) ++nsteps;
+            const double minv = dbl_of(lowest_lo, lowest_hi);
             const double ui = lane_dbl(u, i);
             const bool remb = __builtin_amdgcn_inverse_ballot_w64(rem);
             const double r = ((minv + acc.col(i)) - ui) - v;
             const bool upd = remb && r < spc;
             spc = upd ? r : spc;
             path = upd ? i : path;
-            const float fkey = remb ? (float)spc : kOutF;
-            const float kmin = wave_min_f32_nonan(fkey);
-            const uint64_t cm = __ballot(fkey == kmin);
-            asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
-            const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
-            jsel = sff1(cm);
-            uint32_t lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
-            lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
-            if (ncand != 1) {
-                // equal keys: any column at the exact float64 minimum is a shortest-path choice
-                if ((__ballot(spc != dbl_of(lowest_lo, lowest_hi)) & cm) != 0) {
-                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(remb ? spc : __builtin_inf()));
-                    lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
-                    lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
-                    jsel = sff1(__ballot(spc == dbl_of(lowest_lo, lowest_hi)) & rem) & 63;
+            // columns still at exactly the current distance (zero reduced costs, two thirds of
+            // the steps on SAP Q): one of them is next -- every remaining distance is >= minv --
+            // so no reduction; an unassigned one ends the search
+            const uint64_t tie = __ballot(remb && spc == minv);
+            if (tie != 0) {
+                const uint64_t tf = tie & freec;
+                jsel = sff1(tf != 0 ? tf : tie);
+                ncand = 1;
+            } else {
+                const float fkey = remb ? (float)spc : kOutF;
+                const float kmin = wave_min_f32_nonan(fkey);
+                const uint64_t cm = __ballot(fkey == kmin);
+                asm("s_bcnt1_i32_b64 %0, %1" : "=s"(ncand) : "s"(cm));
+                const uint64_t sb = __builtin_bit_cast(uint64_t, spc);
+                jsel = sff1(cm);
+                lowest_lo = __builtin_amdgcn_readlane((int)(uint32_t)sb, jsel);
+                lowest_hi = __builtin_amdgcn_readlane((int)(uint32_t)(sb >> 32), jsel);
+                if (ncand != 1) {
+                    // equal keys: any column at the exact float64 minimum is a shortest-path choice
+                    if ((__ballot(spc != dbl_of(lowest_lo, lowest_hi)) & cm) != 0) {
+                        const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(remb ? spc : __builtin_inf()));
+                        lowest_lo = __builtin_amdgcn_readfirstlane((uint32_t)lb);
+                        lowest_hi = __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32));
+                        jsel = sff1(__ballot(spc == dbl_of(lowest_lo, lowest_hi)) & rem) & 63;
+                    }
+                    if (ncand == 0) lowest_hi = 0x7ff00000u;  // NaN mid-solve: leave, uncertified
                 }
-                if (ncand == 0) lowest_hi = 0x7ff00000u;  // NaN mid-solve: leave, uncertified
             }
             asm("s_bitset0_b64 %0, %1" : "+s"(rem) : "s"(jsel) : "scc");
-            minv = dbl_of(lowest_lo, lowest_hi);
             i = __builtin_amdgcn_readlane(r4c, jsel);
         } while (__builtin_elementwise_min((uint32_t)(i + 1), lowest_hi ^ 0x7ff00000u) != 0u);
         if (ncand == 0 || lowest_hi == 0x7ff00000u) {
@@ -677,6 +690,7 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
             return kLsaUncertified;
         }
         const int sink = jsel;
+        const double minv = dbl_of(lowest_lo, lowest_hi);
         // scipy's dual update (u[cur] += minv; visited rows u[r] += minv - spc[col4row[r]];
         // scanned columns v[j] -= minv - spc[j]) and augmentation, as lsa_solve_reg64
         const int jm = c4r;

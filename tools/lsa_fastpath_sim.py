@@ -92,9 +92,15 @@ def fast_path(C):
             r = ((minv + C[i]) - u[i]) - v
             upd = rem & (r < spc)
             spc[upd], path[upd] = r[upd], i
-            key = np.where(rem, spc, INF)
-            lowest = key.min()
-            j = int(np.argmax(key == lowest))  # lowest column at the minimum
+            tie = np.where(rem & (spc == minv))[0]  # still at the current distance: no reduction
+            if len(tie):
+                cand, lowest = tie, minv
+            else:
+                key = np.where(rem, spc, INF)
+                lowest = key.min()
+                cand = np.where(key == lowest)[0]
+            free = [c for c in cand if y[c] == -1] if len(tie) else []
+            j = int(free[0]) if free else int(cand[0])  # an unassigned tied column ends the search
             minv = lowest
             rem[j] = False
             if y[j] == -1:
