@@ -295,6 +295,9 @@ def parse(argv=None):
     p.add_argument("--L", type=int, default=3)
     p.add_argument("--selector", default=None, choices=["eps", "sap", "random"])
     p.add_argument("--benefits", default=None, choices=["bump", "dense"])
+    p.add_argument("--rng", default="philox", choices=["philox", "mt19937"],
+                   help="mt19937: the same-seed mode (env e replays numpy's legacy stream seeded with seed + e; "
+                        "float64 benefit tables)")
     p.add_argument("--agent", default=None, choices=["rnn", "rnn_fused", "rnn_torch"],
                    help="rnn (the reference's name; default): the RNNAgent with its inference forward as one HIP "
                         "kernel wherever the shape allows (= rnn_fused); rnn_torch: the plain PyTorch module")
@@ -329,7 +332,7 @@ def make_args(a, E, selector=None, agent=None, fused=None, mac="basic_mac", use_
         batch_size_run=E, env="mock_constellation_env",
         env_args=dict(n=a.n, m=a.m, T=a.T, L=a.L, lambda_=0.5, bids_as_actions=False, seed=a.seed,
                       benefits=a.benefits),
-        env_rng="philox", env_quirks=(), runner_protocol="episode", test_nepisode=1,
+        env_rng=a.rng, env_quirks=(), runner_protocol="episode", test_nepisode=1,
         runner_log_interval=10 ** 12, n=a.n, m=a.m, T=a.T, hidden_dim=64,
         use_rnn=bool(a.use_rnn if use_rnn is None else use_rnn),
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
