@@ -146,6 +146,9 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
     }
     if (st.rng_mode == ASG_RNG_MT19937) {
         if ((e = hipMalloc(&st.mt, sizeof(uint32_t) * E * 625)) != hipSuccess) goto oom;
+        if (st.benefit_mode != ASG_BENEFIT_INJECTED &&
+            (e = hipMalloc(&st.mtpar, sizeof(double2) * E * n * m)) != hipSuccess)
+            goto oom;
         if ((e = asg::launch_mt_seed(st, h->stream)) != hipSuccess) goto oom;
     }
     *out = h;
@@ -170,6 +173,7 @@ int asg_destroy(asg_handle *h) {
     (void)hipFree(const_cast<double *>(st.T_trans));
     (void)hipFree(st.table);
     (void)hipFree(st.mt);
+    (void)hipFree(st.mtpar);
     (void)hipFree(st.assign);
     delete h;
     return ASG_OK;

@@ -470,43 +470,145 @@ struct MtWave {
     }
 };
 
-// generate_benefits_over_time + permutation in MT compat mode.  construct: also replay
-// the throwaway __init__ table draw (mock :34) first.  tab: [E][T][n][m].
-__global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvState st, double *tab, bool construct,
+// MT19937 over two LDS blocks: `out` holds the tempered words of the current block (numpy's
+// state `key`, position `pos`) and of the next one (`key2`, twisted ahead), so any word up to
+// 624 ahead of pos is readable without a twist in between -- what the speculative reads of
+// mt_reset_kernel need.  The state handed back is (key, pos): numpy's.
+__device__ __forceinline__ void mt_twist_inplace(uint32_t *k) {
+    const int lane = threadIdx.x & (kWave - 1);
+    auto gen = [&](uint32_t ki, uint32_t ki1, uint32_t kim) {
+        const uint32_t y = (ki & 0x80000000u) | (ki1 & 0x7fffffffu);
+        return kim ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    };
+    const int phase_lo[3] = {0, kMtN - kMtM, 2 * (kMtN - kMtM)};
+    const int phase_hi[3] = {kMtN - kMtM, 2 * (kMtN - kMtM), kMtN - 1};
+    for (int ph = 0; ph < 3; ++ph) {
+        uint32_t nv[4];
+        int cnt = 0;
+        for (int i = phase_lo[ph] + lane; i < phase_hi[ph]; i += kWave, ++cnt)
+            nv[cnt] = gen(k[i], k[i + 1], k[(i + kMtM) % kMtN]);
+        wave_sync();
+        cnt = 0;
+        for (int i = phase_lo[ph] + lane; i < phase_hi[ph]; i += kWave, ++cnt) k[i] = nv[cnt];
+        wave_sync();
+    }
+    if (lane == 0) k[kMtN - 1] = gen(k[kMtN - 1], k[0], k[kMtM - 1]);
+    wave_sync();
+}
+__device__ __forceinline__ void mt_temper(const uint32_t *k, uint32_t *o) {
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int i = lane; i < kMtN; i += kWave) {
+        uint32_t y = k[i];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        o[i] = y;
+    }
+    wave_sync();
+}
+struct MtWave2 {
+    uint32_t *key, *key2;  // [624] raw states of the current and the next block (LDS)
+    uint32_t *out;         // [1248] tempered words of both
+    int pos;               // wave-uniform, < 624 between calls
+    __device__ void init(int pos0) {
+        const int lane = threadIdx.x & (kWave - 1);
+        mt_temper(key, out);
+        for (int i = lane; i < kMtN; i += kWave) key2[i] = key[i];
+        wave_sync();
+        mt_twist_inplace(key2);
+        mt_temper(key2, out + kMtN);
+        pos = pos0;
+        if (pos >= kMtN) shift();
+    }
+    __device__ void shift() {  // the next block becomes the current one
+        const int lane = threadIdx.x & (kWave - 1);
+        for (int i = lane; i < kMtN; i += kWave) {
+            key[i] = key2[i];
+            out[i] = out[kMtN + i];
+        }
+        wave_sync();
+        mt_twist_inplace(key2);
+        mt_temper(key2, out + kMtN);
+        pos -= kMtN;
+    }
+    __device__ uint32_t word(int k) const { return out[pos + k]; }  // k < 624, uniform
+    __device__ void advance(int c) {
+        pos += c;
+        if (pos >= kMtN) shift();
+    }
+    __device__ uint32_t next() {
+        const uint32_t w = word(0);
+        advance(1);
+        return w;
+    }
+    __device__ static double dbl(uint32_t a, uint32_t b) {  // numpy's random_sample from two words
+        return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+    }
+    __device__ double next_double() {
+        const double d = dbl(word(0), word(1));
+        advance(2);
+        return d;
+    }
+    __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * next_double(); }
+    __device__ uint32_t interval(uint32_t max) {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+        uint32_t v;
+        while ((v = (next() & mask)) > max) {}
+        return v;
+    }
+};
+
+// generate_benefits_over_time + permutation in MT compat mode, the draws half: one wave per
+// env consumes its MT19937 stream in the reference's order (mock :276-299, :105) and records
+// each (agent, task) bump of the reset's table -- center and spread, the scale as the sign of spread,
+// (0, 0) for no bump -- in par [E][m][n] (draw order: one coalesced 1 KiB store per 64 agents
+// of a task); mt_table_kernel then writes the table from them with whole-row stores.
+// construct: also replay the throwaway __init__ table draw (mock :34) first.
+__global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvState st, double2 *par, bool construct,
                                                        bool generate) {
-    const bool write_table = generate;
     extern __shared__ uint32_t s_mt[];
-    uint32_t *key = s_mt;
-    uint32_t *out = s_mt + kMtN;
-    int *perm = reinterpret_cast<int *>(out + kMtN);
+    uint32_t *key = s_mt, *key2 = s_mt + kMtN, *out = s_mt + 2 * kMtN;
+    int *perm = reinterpret_cast<int *>(out + 2 * kMtN);
     const int64_t e = blockIdx.x;
     const int lane = threadIdx.x;
     const int n = st.n, m = st.m, T = st.T;
     uint32_t *g = mtstate + e * (kMtN + 1);
     for (int i = lane; i < kMtN; i += kWave) key[i] = g[i];
     wave_sync();
-    MtWave mt{key, out, (int)g[kMtN]};
-    mt.temper_all();
-    const int64_t nm = (int64_t)n * m;
-    double *te = tab + e * T * nm;
-    if (write_table)
-        for (int64_t p = lane; p < T * nm; p += kWave) te[p] = 0.0;
-    wave_sync();
+    MtWave2 mt{key, key2, out, 0};
+    mt.init((int)g[kMtN]);
+    double2 *pe = par ? par + e * (int64_t)n * m : nullptr;
     for (int pass = construct ? 0 : 1; generate && pass < 2; ++pass) {
         const double wmin = pass == 0 ? st.wmin_init : st.wmin;
         const double wmax = pass == 0 ? st.wmax_init : st.wmax;
         for (int j = 0; j < m; ++j) {
             const double scale = (mt.next() & 3u) == 3u ? 10.0 : 1.0;
-            for (int i = 0; i < n; ++i) {
-                const double r = mt.next_double();
-                if (!(r > 0.75)) continue;
-                const double center = mt.uniform(0.0, (double)T);
-                const double spread = mt.uniform(wmin, wmax);
-                if (pass == 1 && write_table) {
-                    const double s2 = bump_s2(spread);
-                    for (int t = lane; t < T; t += kWave)
-                        te[(int64_t)t * nm + (int64_t)i * m + j] = bump_value(scale, center, s2, t);
+            for (int c0 = 0; c0 < n; c0 += kWave) {
+                const int cend = min(n, c0 + kWave);
+                double2 mine = make_double2(0.0, 0.0);  // lane i - c0: agent i's bump on task j
+                // speculative reads: every remaining agent of the chunk tests its r as if no bump
+                // came before it (two words each); the first agent with r > 0.75 is exact, it
+                // consumes four more words, and the agents after it test again from there
+                for (int i = c0; i < cend;) {
+                    const int rows = cend - i;
+                    const int w = 2 * lane;  // < 128 words ahead: inside the two blocks
+                    const double r = lane < rows ? MtWave2::dbl(mt.word(w), mt.word(w + 1)) : 0.0;
+                    const uint64_t act = __ballot(lane < rows && r > 0.75);
+                    if (act == 0) {
+                        mt.advance(2 * rows);
+                        break;
+                    }
+                    const int k = __builtin_amdgcn_readfirstlane(__builtin_ctzll(act));
+                    mt.advance(2 * k + 2);
+                    const double center = mt.uniform(0.0, (double)T);
+                    const double spread = mt.uniform(wmin, wmax);  // s2 = bump_s2(spread) in mt_table_kernel
+                    if (lane == i + k - c0) mine = make_double2(center, scale == 10.0 ? -spread : spread);
+                    i += k + 1;
                 }
+                if (pass == 1 && pe && c0 + lane < n) pe[(int64_t)j * n + c0 + lane] = mine;
             }
         }
     }
@@ -525,6 +627,39 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
     for (int i = lane; i < n; i += kWave) st.prev[e * n + i] = perm[i];
     for (int i = lane; i < kMtN; i += kWave) g[i] = key[i];
     if (lane == 0) g[kMtN] = (uint32_t)mt.pos;
+}
+
+// the reset's float64 table B[e][t][i][j] = bump_value(scale, center, s2, t) for a recorded
+// bump, else 0 (the reference's zeros + bumps, mock :276-299): the draws of `rows` agents
+// (rows * m <= 1024: 16 KiB) staged transposed in LDS, then all T rows of those agents written
+// as whole rows
+static int mt_table_rows(int m) { return m >= 1024 ? 1 : (1024 / m < 16 ? 1024 / m : 16); }
+__global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, double *tab, int R) {
+    extern __shared__ double2 s_par[];  // [R agents][m tasks]
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, T = st.T;
+    const int64_t nm = (int64_t)n * m;
+    const double2 *pe = par + e * nm;
+    double *te = tab + e * T * nm;
+    for (int i0 = 0; i0 < n; i0 += R) {
+        const int rows = min(R, n - i0);
+        __syncthreads();
+        // par is [task][agent]: `rows` consecutive agents of a task are contiguous
+        for (int idx = threadIdx.x; idx < rows * m; idx += blockDim.x) {
+            const int ii = idx % rows, j = idx / rows;
+            s_par[ii * m + j] = pe[(int64_t)j * n + i0 + ii];
+        }
+        __syncthreads();
+        // each thread owns elements (ii, j) of the chunk and writes them for every t: per t the
+        // block's stores cover the chunk's rows whole (rows * m contiguous doubles)
+        for (int idx = threadIdx.x; idx < rows * m; idx += blockDim.x) {
+            const double2 p = s_par[idx];
+            const bool on = p.y != 0.0;
+            const double sc = p.y < 0.0 ? 10.0 : 1.0, s2 = on ? bump_s2(__builtin_fabs(p.y)) : 1.0;
+            double *o = te + (int64_t)i0 * m + idx;
+            for (int t = 0; t < T; ++t) o[(int64_t)t * nm] = on ? bump_value(sc, p.x, s2, t) : 0.0;
+        }
+    }
 }
 
 // skip `words` draws of every stream (other consumers of numpy's global stream)
@@ -617,14 +752,20 @@ static bool uses_table(const EnvState &st) {
 
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s) {
     if (st.rng_mode == ASG_RNG_MT19937) {
-        const size_t lds = sizeof(uint32_t) * 2 * kMtN + sizeof(int) * st.m + 16;
+        const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m + 16;
         const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
         // with an injected table (sat_prox_mat=) neither __init__ nor reset draw a
         // table: only the permutation consumes the stream (mock :32-37, :99-105)
-        hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.table, construct && gen,
+        hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen,
                            gen);
         hipError_t err = hipGetLastError();
         if (err != hipSuccess) return err;
+        if (gen) {
+            const int R = mt_table_rows(st.m);
+            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), sizeof(double2) * R * st.m, s, st.mtpar, st,
+                               st.table, R);
+            if ((err = hipGetLastError()) != hipSuccess) return err;
+        }
         return launch_reset_src(table_src(st), bv, st, ts, false, s);
     }
     if (uses_table(st)) return launch_reset_src(table_src(st), bv, st, ts, true, s);
