@@ -309,6 +309,14 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
     int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
     int c4r[1] = {-1};
     int nsteps = 0, nfast = 0;
+#ifdef ASG_SAP_STAGE_ONLY  // timing experiments only: the staging and noise alone (wrong results)
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) sum += rc.lo[k] + rc.hi[k];
+    if (__builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sum)) == 0x7fffffff) status = 1;
+    sap_emit<kCount>(b, status, (int)(threadIdx.x & 63), 0, n, m, col_out, act_out, status_out, steps_out);
+    return;
+#endif
     bool done = false;
     if (ASG_SAP_FAST && status == ASG_OK && n == m)
         done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
