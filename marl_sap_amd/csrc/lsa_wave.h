@@ -657,7 +657,7 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
             // columns still at exactly the current distance (zero reduced costs, two thirds of
             // the steps on SAP Q): one of them is next -- every remaining distance is >= minv --
             // so no reduction; an unassigned one ends the search
-            const uint64_t tie = __ballot(remb && spc == minv);
+            const uint64_t tie = __builtin_amdgcn_ballot_w64(spc == minv) & rem;  // compare straight into an SGPR pair
             if (tie != 0) {
                 const uint64_t tf = tie & freec;
                 jsel = sff1(tf != 0 ? tf : tie);
