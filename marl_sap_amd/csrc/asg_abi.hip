@@ -140,6 +140,8 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
     if (st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED) {
         if ((e = hipMalloc(&st.table, sizeof(double) * E * T * n * m)) != hipSuccess) goto oom;
         if ((e = hipMemsetAsync(st.table, 0, sizeof(double) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
+        if ((e = hipMalloc(&st.table32, sizeof(float) * E * T * n * m)) != hipSuccess) goto oom;
+        if ((e = hipMemsetAsync(st.table32, 0, sizeof(float) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
     }
     if (st.bids) {
         if ((e = hipMalloc(&st.assign, sizeof(int) * E * n)) != hipSuccess) goto oom;
@@ -172,6 +174,7 @@ int asg_destroy(asg_handle *h) {
     (void)hipFree(st.err);
     (void)hipFree(const_cast<double *>(st.T_trans));
     (void)hipFree(st.table);
+    (void)hipFree(st.table32);
     (void)hipFree(st.mt);
     (void)hipFree(st.mtpar);
     (void)hipFree(st.assign);

@@ -382,7 +382,9 @@ __global__ void import_table_kernel(const double *in, EnvState st, double *tab, 
     for (int64_t p = threadIdx.x; p < (int64_t)n * m * T; p += blockDim.x) {
         const int t = (int)(p % T);
         const int64_t ij = p / T;
-        tab[(e * T + t) * (int64_t)n * m + ij] = in[se * (int64_t)n * m * T + p];
+        const double x = in[se * (int64_t)n * m * T + p];
+        tab[(e * T + t) * (int64_t)n * m + ij] = x;
+        st.table32[(e * T + t) * (int64_t)n * m + ij] = (float)x;
     }
 }
 
@@ -657,7 +659,12 @@ __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvSt
             const bool on = p.y != 0.0;
             const double sc = p.y < 0.0 ? 10.0 : 1.0, s2 = on ? bump_s2(__builtin_fabs(p.y)) : 1.0;
             double *o = te + (int64_t)i0 * m + idx;
-            for (int t = 0; t < T; ++t) o[(int64_t)t * nm] = on ? bump_value(sc, p.x, s2, t) : 0.0;
+            float *o32 = st.table32 + e * T * nm + (int64_t)i0 * m + idx;
+            for (int t = 0; t < T; ++t) {
+                const double x = on ? bump_value(sc, p.x, s2, t) : 0.0;
+                o[(int64_t)t * nm] = x;
+                o32[(int64_t)t * nm] = (float)x;
+            }
         }
     }
 }

@@ -1005,6 +1005,7 @@ struct RolloutArgs {
     // benefits: NULL = Philox bumps regenerated in registers; else the handle's float64 table
     // [E][T][n][m] (MT19937 compat / injected sat_prox_mat), read for the L lookahead rows
     const double *table;
+    const float *table32;  // the table rounded to float32: the lookahead rows' reads
     // QOUT instances: the agent's Q rows [E n][m] f32 (the forward of asg_rnn_agent_forward)
     // instead of the epsilon-greedy selection -- a selector outside the kernel (SAP) acts on them
     float *Q;
@@ -1366,23 +1367,22 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 // past T are zeros)
                 float4 xv[2][NT];
                 if (TAB && t < T) {
-                    // the table's float64 benefits, rounded once to float32 (the batch's dtype,
-                    // as the separate step's rows): B[e][t][row][j0 .. j0 + 3]
-                    const double *trow = ra.table + ((int64_t)e * T + t) * n * m;
+                    // the table's benefits rounded to float32 (the batch's dtype, as the separate
+                    // step's rows), from its float32 copy: B[e][t][row][j0 .. j0 + 3], one 16-byte
+                    // load (the float64 table would take two behind the tile's stores)
+                    const float *trow = ra.table32 + ((int64_t)e * T + t) * n * m;
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt) {
                             const int j0 = 32 * u + 16 * c + 4 * q;
-                            const double *tp = trow + (int64_t)ia[nt] * m + j0;
+                            const float *tp = trow + (int64_t)ia[nt] * m + j0;
                             if (!GEN) {
-                                const double2 a = *reinterpret_cast<const double2 *>(tp);
-                                const double2 b = *reinterpret_cast<const double2 *>(tp + 2);
-                                xv[c][nt] = make_float4((float)a.x, (float)a.y, (float)b.x, (float)b.y);
+                                xv[c][nt] = *reinterpret_cast<const float4 *>(tp);
                             } else {
                                 float v4[4];
 #pragma unroll
-                                for (int v = 0; v < 4; ++v) v4[v] = (ok[nt] && j0 + v < m) ? (float)tp[v] : 0.f;
+                                for (int v = 0; v < 4; ++v) v4[v] = (ok[nt] && j0 + v < m) ? tp[v] : 0.f;
                                 xv[c][nt] = make_float4(v4[0], v4[1], v4[2], v4[3]);
                             }
                         }
@@ -1727,6 +1727,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.reset = reset;
     const bool tab = st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
     ra.table = tab ? st.table : nullptr;
+    ra.table32 = tab ? st.table32 : nullptr;
     if (tab && reset) return hipErrorInvalidValue;  // the table modes' reset is asg_reset (MT19937 stream)
     // Q output: one transition and the forward of the row after it (asg_step_forward)
     if (Q && (steps != 1 || select_first || !select_last || reset)) return hipErrorInvalidValue;

@@ -30,6 +30,7 @@ struct EnvState {
     int *prev;             // [E][n] previous assignment (state for beta_hat)
     double *returns;       // [E] float64 episode returns
     double *table;         // [E][T][n][m] float64 (MT19937 / injected modes)
+    float *table32;        // the same rounded to float32 (the rows' dtype): the episode kernel's lookahead reads
     uint32_t *mt;          // [E][625] MT19937 key + pos (compat mode)
     double2 *mtpar;        // [E][m][n] the reset's bump draws (center, +-spread; 0: no bump) (compat mode)
     int *assign;           // [E][n] LSA assignments of the bids (bids_as_actions)
