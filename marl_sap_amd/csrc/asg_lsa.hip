@@ -202,27 +202,39 @@ hipError_t launch_lsa_batched(const void *C, int dtype, const int64_t strides[3]
 // problem b's working column: Q column `lane` of env b plus its noise (std mean|Q| * eps * 2),
 // negated (maximize) -- ASG_E_LSA_INVALID (wave uniform) when the noisy matrix holds NaN or
 // +inf
-template <class RC>
+template <bool kDense64, class RC>
 __device__ __forceinline__ int sap_stage(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, int m,
                                          float epsilon, uint64_t seed, uint32_t counter, int64_t env_base, int64_t b,
                                          RC &rc) {
-    // opaque strides: in a persistent loop the 64 row offsets i * q1 would otherwise be hoisted
-    // out of it, 128 SGPRs live across the whole solve
-    asm volatile("" : "+s"(q0), "+s"(q1), "+s"(q2));
     const int lane = threadIdx.x & (kWave - 1);
-    const float *col = q + b * q0 + (int64_t)lane * q2;
     float asum = 0.0f;
-    // in place in the column's registers (a second 64-register copy would spill beside the
-    // other problems of the wave)
+    if constexpr (kDense64) {
+        // 64 x 64 rows of 64 contiguous floats (the rollout's Q rows): every lane and row valid,
+        // the rows at compile-time offsets -- 64 loads off four base addresses, no guards
+        const float *col = q + b * q0 + lane;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        float x = 0.0f, y = 0.0f;
-        if (lane < m && i < n) x = col[i * q1];
-        if (lane < m && i + 32 < n) y = col[(i + 32) * q1];
-        asum += __builtin_fabsf(x);
-        asum += __builtin_fabsf(y);
-        rc.lo[i] = x;
-        rc.hi[i] = y;
+        for (int i = 0; i < 32; ++i) {
+            const float x = col[i * 64], y = col[(i + 32) * 64];
+            asum += __builtin_fabsf(x);
+            asum += __builtin_fabsf(y);
+            rc.lo[i] = x;
+            rc.hi[i] = y;
+        }
+    } else {
+        // opaque strides: the 64 row offsets i * q1 are formed where used, not kept live
+        asm volatile("" : "+s"(q0), "+s"(q1), "+s"(q2));
+        const float *col = q + b * q0 + (int64_t)lane * q2;
+        // in place in the column's registers
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            float x = 0.0f, y = 0.0f;
+            if (lane < m && i < n) x = col[i * q1];
+            if (lane < m && i + 32 < n) y = col[(i + 32) * q1];
+            asum += __builtin_fabsf(x);
+            asum += __builtin_fabsf(y);
+            rc.lo[i] = x;
+            rc.hi[i] = y;
+        }
     }
     // th.mean(th.abs(Q)) (float32; summation order differs from torch's, the noise is
     // random either way), stds = avg * eps * 2
@@ -290,7 +302,7 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
 #ifndef ASG_SAP_PIN
 #define ASG_SAP_PIN 1
 #endif
-template <bool kCount>
+template <bool kCount, bool kDense64>
 __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
                                                         int64_t env_base, float *col_out, int64_t *act_out,
@@ -306,7 +318,7 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
 #else
     RegCostF32 rc;
 #endif
-    int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
+    int status = sap_stage<kDense64>(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
     int c4r[1] = {-1};
     int nsteps = 0, nfast = 0;
 #ifdef ASG_SAP_STAGE_ONLY  // timing experiments only: the staging and noise alone (wrong results)
@@ -334,7 +346,7 @@ __global__ void __launch_bounds__(64 * kLsaWpb) sap_noise_kernel(const float *q,
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
     RegCostF32 rc;
-    const int status = sap_stage(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
+    const int status = sap_stage<false>(q, q0, q1, q2, n, m, epsilon, seed, counter, env_base, b, rc);
     const int lane = threadIdx.x & (kWave - 1);
     float *o = q_out + b * n * m + lane;
     if (lane < m) {
@@ -370,12 +382,19 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
                              int32_t *steps_out, hipStream_t s, int64_t *act_out) {
     const dim3 grid = lsa_reg_grid(B);
     const size_t pad = sap_lds_pad();
-    if (steps_out)
-        hipLaunchKernelGGL(sap_select_kernel<true>, grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m,
-                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
-    else
-        hipLaunchKernelGGL(sap_select_kernel<false>, grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m,
-                           epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B);
+    // the rollout's Q rows ([B][64][64] contiguous): the unguarded staging instance
+    const bool d64 = n == 64 && m == 64 && qs[2] == 1 && qs[1] == 64 && (reinterpret_cast<uintptr_t>(q) & 3) == 0;
+#define SAP_L(C, D)                                                                                                 \
+    hipLaunchKernelGGL((sap_select_kernel<C, D>), grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m, \
+                       epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B)
+    if (steps_out) {
+        if (d64) SAP_L(true, true);
+        else SAP_L(true, false);
+    } else {
+        if (d64) SAP_L(false, true);
+        else SAP_L(false, false);
+    }
+#undef SAP_L
     return hipGetLastError();
 }
 

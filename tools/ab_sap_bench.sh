@@ -14,9 +14,9 @@ for rep in $(seq 1 ${REPS:-2}); do
     python3 - "$OUT/bench_${tag}_$rep.log" "$lib" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-r = d["roofline_lsa"]
-print(f"{sys.argv[2]:28s} value {d['value']:.4g} sap_kernel_ms {r['kernel_ms']} cyc/step {r['cycles_per_step_per_simd']} "
-      f"exact_problems {r.get('problems_on_exact_solver')}")
+r = d.get("roofline_lsa") or {}
+print(f"{sys.argv[2]:28s} value {d['value']:.4g} sap_kernel_ms {r.get('kernel_ms', d['kernels_ms'].get('sap_select'))} "
+      f"cyc/step {r.get('cycles_per_step_per_simd')} exact_problems {r.get('problems_on_exact_solver')}")
 PY
   done
 done
