@@ -1186,6 +1186,9 @@ struct HNext {
     int mode;
 };
 
+#ifndef ASG_ROLLOUT_LATE
+#define ASG_ROLLOUT_LATE 1
+#endif
 template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, bool AGENT, class RA>
 __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
@@ -1399,7 +1402,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt) xv[c][nt] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
-                if (st_now) {
+                auto store_rows = [&]() {
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -1418,7 +1421,12 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                                     }
                             }
                         }
-                }
+                };
+                // an L2 weight slice (no W2 in LDS: the large shapes, 19 of 24 slices at 256 x 256):
+                // its weights are loaded before this block's row stores and the stores follow the
+                // MFMAs, so the loads wait for the previous block's stores only
+                const bool late = ASG_ROLLOUT_LATE && !W2L && AGENT && l * Ub + u >= s_l2;
+                if (st_now && !late) store_rows();
                 if (AGENT) {
                     // the agent kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
                     const int sl = l * Ub + u;
@@ -1454,6 +1462,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                     else
                         mma(false);
                 }
+                if (st_now && late) store_rows();
             }
         }
         if (!AGENT) return;
