@@ -27,6 +27,38 @@ def test_layout_matches_reference_dump(golden):
             assert str(v.dtype).replace("torch.", "") == str(ref.dtype), k
 
 
+def test_bench_store_ceiling_and_sap_steps(monkeypatch, tmp_path):
+    """The fused roofline's store_ceiling block (writes = all bytes but h in and the actions row
+    the kernel keeps in LDS, against the newest tools/store_bw.hip record) and the SAP step
+    counts' fast / exact split (low / high 16 bits of asg_sap_select's path_steps_out)."""
+    import json
+    import types
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r4_store_bw_s1.txt").write_text("# x\n" + json.dumps({"GBps": 4000.0}) + "\n")
+    (prof / "r4_store_bw_s2.txt").write_text(json.dumps({"GBps": 4500.0}) + "\n" + json.dumps({"GBps": 5000.0}) + "\n")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.store_ceiling() == (5000.0, "r4_store_bw_s2.txt")
+    a = types.SimpleNamespace(n=64, m=64, L=3)
+    E = 16384
+    roof = bench.fused_roofline(a, E, 0.5)
+    per = (bench.step_bytes(64, 64, 3) + 64 * (2 * 4 * 64 + 8)) * E
+    writes = per - 64 * 4 * 64 * E - 8 * 64 * E
+    sc = roof["store_ceiling"]
+    assert roof["bytes_per_launch"] == per and sc["write_bytes_per_launch"] == writes
+    assert sc["frac"] == pytest.approx(writes / 0.5e-3 / 1e9 / 5000.0, rel=1e-3)
+    # SAP step-count split as bench.run_leg decodes it
+    import torch
+    cs = torch.tensor([(3 << 16) | 700, 650, (1200 << 16) | 900], dtype=torch.int32).long()
+    assert int((cs & 0xFFFF).sum()) == 2250 and int((cs >> 16).sum()) == 1203 and int(((cs >> 16) > 0).sum()) == 2
+    res = {"path_steps_per_launch": 3453, "path_steps_fast": 2250, "path_steps_exact": 1203, "exact_problems": 2,
+           "lsa_ms": 0.5}
+    monkeypatch.setattr(bench, "pmc_lookup", lambda pattern, **kw: None)
+    r = bench.lsa_roofline(a, 3, res)
+    assert r["path_steps_fast"] == 2250 and r["path_steps_exact"] == 1203 and r["problems_on_exact_solver"] == 2
+
+
 @pytest.mark.parametrize("time_major", [False, True])
 def test_update_and_slicing_semantics(time_major):
     n, m, T = 3, 4, 5
