@@ -99,8 +99,7 @@ def fast_path(C):
                 key = np.where(rem, spc, INF)
                 lowest = key.min()
                 cand = np.where(key == lowest)[0]
-            free = [c for c in cand if y[c] == -1] if len(tie) else []
-            j = int(free[0]) if free else int(cand[0])  # an unassigned tied column ends the search
+            j = int(cand[0])
             minv = lowest
             rem[j] = False
             if y[j] == -1:
