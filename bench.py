@@ -297,7 +297,7 @@ def parse(argv=None):
     p.add_argument("--benefits", default=None, choices=["bump", "dense"])
     p.add_argument("--rng", default="philox", choices=["philox", "mt19937"],
                    help="mt19937: the same-seed mode (env e replays numpy's legacy stream seeded with seed + e; "
-                        "float64 benefit tables)")
+                        "float32 benefit table + recorded draws)")
     p.add_argument("--agent", default=None, choices=["rnn", "rnn_fused", "rnn_torch"],
                    help="rnn (the reference's name; default): the RNNAgent with its inference forward as one HIP "
                         "kernel wherever the shape allows (= rnn_fused); rnn_torch: the plain PyTorch module")
@@ -789,24 +789,28 @@ def main():
                                      "= 32 MB per launch"}}
             # the same-seed mode (rng="mt19937": env e replays numpy's legacy stream seeded with
             # seed + e, the reference's draws) on the episode kernel: configs[2] with the handle's
-            # float64 tables read for the lookahead rows (and the reset's MT19937 table draws)
+            # float32 benefit table read for the lookahead rows (the float64 rewards evaluated from
+            # the reset's recorded MT19937 draws, which the reset writes with that table)
             rc = run_leg(a, dev, world, E, sk, sw, env_rng="mt19937")
             leg = {**leg_base(rc, sk, sw),
                    "workload": "configs[2] in the same-seed mode: rng mt19937 (per env np.random.seed(seed + env)), "
-                               "float64 benefit tables; asg_reset (MT19937 table draws) + the episode kernel",
+                               "float32 benefit table + recorded draws; asg_reset (MT19937 draws, table write) + the "
+                               "episode kernel",
                    "kernels_ms": {"fused_rollout_per_step": round(rc["fused_ms"], 4) if rc.get("fused_ms") else None,
                                   "fused_note": "the episode launches of the window, their asg_reset (table draws) "
                                                 "included"}}
             if rc.get("fused_ms"):
-                tb = 8 * a.n * a.m * E  # one float64 table slice read per env-step (+ its write at the reset)
+                tb = 4 * a.n * a.m * E  # one float32 table slice read per env-step (+ its write at the reset)
+                pb = 32 * a.n * a.m * E // a.T  # the draws (16 B per pair) written and read once per episode
                 croof = fused_roofline(a, E, rc["fused_ms"], resets_per_step=res_resets(rc))
-                per = croof["bytes_per_launch"] + 2 * tb
+                per = croof["bytes_per_launch"] + 2 * tb + pb
                 croof.update({"bytes_per_launch": per, "achieved": round(per / (rc["fused_ms"] * 1e-3) / 1e9, 1),
                              "frac": round(per / (rc["fused_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": None, "kernel": "asg::rollout_kernel<TAB> (+ asg_reset's table draws)",
-                             "per_launch_note": "the Philox accounting + 8nm per env-step of table read (one new "
-                                                "float64 slice per step) + 8nm of table write (the reset's T slices "
-                                                "over T steps)"})
+                             "per_launch_note": "the Philox accounting + 4nm per env-step of table read (one new "
+                                                "float32 slice per step) + 4nm of table write (the reset's T slices "
+                                                "over T steps) + 32nm / T of draws (written and read once per "
+                                                "episode)"})
                 croof.pop("traffic_pmc", None)
                 croof.pop("traffic_over_algorithmic", None)
                 croof.pop("traffic_note", None)

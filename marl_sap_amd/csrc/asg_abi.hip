@@ -137,9 +137,11 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
         if ((e = hipMemcpy(tt, cfg->T_trans, sizeof(double) * m * m, hipMemcpyHostToDevice)) != hipSuccess) goto oom;
         st.T_trans = tt;
     }
-    if (st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED) {
+    if (st.benefit_mode == ASG_BENEFIT_INJECTED) {
         if ((e = hipMalloc(&st.table, sizeof(double) * E * T * n * m)) != hipSuccess) goto oom;
         if ((e = hipMemsetAsync(st.table, 0, sizeof(double) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
+    }
+    if (st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED) {
         if ((e = hipMalloc(&st.table32, sizeof(float) * E * T * n * m)) != hipSuccess) goto oom;
         if ((e = hipMemsetAsync(st.table32, 0, sizeof(float) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
     }
@@ -148,9 +150,10 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
     }
     if (st.rng_mode == ASG_RNG_MT19937) {
         if ((e = hipMalloc(&st.mt, sizeof(uint32_t) * E * 625)) != hipSuccess) goto oom;
-        if (st.benefit_mode != ASG_BENEFIT_INJECTED &&
-            (e = hipMalloc(&st.mtpar, sizeof(double2) * E * n * m)) != hipSuccess)
-            goto oom;
+        if (st.benefit_mode != ASG_BENEFIT_INJECTED) {  // zero draws = the zero table before a reset
+            if ((e = hipMalloc(&st.mtpar, sizeof(double2) * E * n * m)) != hipSuccess) goto oom;
+            if ((e = hipMemsetAsync(st.mtpar, 0, sizeof(double2) * E * n * m, h->stream)) != hipSuccess) goto oom;
+        }
         if ((e = asg::launch_mt_seed(st, h->stream)) != hipSuccess) goto oom;
     }
     *out = h;

@@ -67,6 +67,15 @@ __device__ __forceinline__ double bump_value(double scale, double center, double
     return scale * exp(-(x * x) / s2 * 0.5);  // "/ 2" is exact as "* 0.5"
 }
 
+// the table entry B[t] of one recorded MT19937 bump p = (center, +-spread; scale 10 as a negative
+// spread, (0, 0) for no bump): every reader of the compat-mode benefits evaluates it through
+// this one function, so the float32 table written at reset and the float64 values evaluated
+// later agree bit for bit
+__device__ __forceinline__ double mt_par_value(double2 p, int t) {
+    if (p.y == 0.0) return 0.0;
+    return bump_value(p.y < 0.0 ? 10.0 : 1.0, p.x, bump_s2(__builtin_fabs(p.y)), t);
+}
+
 // purposes of Philox counters (counter.z); counter.w = episode
 enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u,
                   kCtrSapNoise = 7u, kCtrPair2 = 8u, kCtrPair4 = 9u };

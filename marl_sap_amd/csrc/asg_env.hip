@@ -6,7 +6,9 @@
 // actions_onehot).  Benefits come from one of two sources:
 //   * BumpSrc  (Philox, native throughput mode): bump parameters are regenerated on the
 //     fly from a counter-based key each step -- no benefit table in HBM at all;
-//   * TableSrc (MT19937 compat / injected / exported): float64 table [E][T][n][m].
+//   * ParSrc   (MT19937 compat): the reset's recorded draws [E][m][n] (float64 values) and
+//     their float32 table [E][T][n][m] (the rows);
+//   * TableSrc (injected): float64 table [E][T][n][m].
 // Reference: envs/mock_constellation_env.py:94-175 (reset / step / pre-transition data),
 // runners/episode_runner.py:60-100 and runners/parallel_runner.py:113-200 (which rows
 // get which fields), components/transforms.py:12-22 (OneHot, int64).
@@ -68,7 +70,7 @@ struct BumpSrc {  // Philox, float32 bumps regenerated on the fly (no table in H
     }
 };
 
-struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
+struct TableSrc {  // float64 table [E][T][n][m] (injected)
     const double *tab;
     int n, m, T;
 
@@ -93,6 +95,40 @@ struct TableSrc {  // float64 table [E][T][n][m] (MT19937 compat / injected)
     __device__ Env bind(int64_t e, const float *) const {
         const int64_t nm = (int64_t)n * m;
         return Env{tab + e * (int64_t)T * nm, m, nm};
+    }
+};
+
+// MT19937 compat mode: the rows' float32 benefits from the reset's float32 table, the float64
+// ones (rewards, export) evaluated from the recorded draws par [E][m][n] (mt_par_value, the
+// function the table was written with): no float64 table in HBM
+struct ParSrc {
+    const float *tab32;
+    const double2 *par;
+    int n, m, T;
+
+    static constexpr bool kNeedsScale = false;
+    struct Env {
+        const float *p;  // &tab32[e][0][0][0]
+        const double2 *q;  // &par[e][0][0]
+        int n, m;
+        int64_t nm;
+        struct Pair {
+            const float *p;
+            const double2 *q;
+            int64_t tstride;
+            __device__ float at(int t) const { return p[t * tstride]; }
+            __device__ double at64(int t) const { return mt_par_value(*q, t); }
+        };
+        __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, q + (int64_t)j * n + i, nm}; }
+        __device__ void pair4(int i, int j, Pair (&P)[4]) const {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) P[k] = pair(i, j + k);
+        }
+    };
+    __device__ void fill_scale(int64_t, float *) const {}
+    __device__ Env bind(int64_t e, const float *) const {
+        const int64_t nm = (int64_t)n * m;
+        return Env{tab32 + e * (int64_t)T * nm, par + e * nm, n, m, nm};
     }
 };
 
@@ -631,18 +667,17 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
     if (lane == 0) g[kMtN] = (uint32_t)mt.pos;
 }
 
-// the reset's float64 table B[e][t][i][j] = bump_value(scale, center, s2, t) for a recorded
-// bump, else 0 (the reference's zeros + bumps, mock :276-299): the draws of `rows` agents
-// (rows * m <= 1024: 16 KiB) staged transposed in LDS, then all T rows of those agents written
-// as whole rows
+// the reset's table B[e][t][i][j] = mt_par_value(draw, t) (the reference's zeros + bumps, mock
+// :276-299) rounded to float32, the rows' dtype: the draws of `rows` agents (rows * m <= 1024:
+// 16 KiB) staged transposed in LDS, then all T rows of those agents written as whole rows.  The
+// float64 values are not stored: their readers evaluate them from the draws (ParSrc).
 static int mt_table_rows(int m) { return m >= 1024 ? 1 : (1024 / m < 16 ? 1024 / m : 16); }
-__global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, double *tab, int R) {
+__global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, int R) {
     extern __shared__ double2 s_par[];  // [R agents][m tasks]
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m, T = st.T;
     const int64_t nm = (int64_t)n * m;
     const double2 *pe = par + e * nm;
-    double *te = tab + e * T * nm;
     for (int i0 = 0; i0 < n; i0 += R) {
         const int rows = min(R, n - i0);
         __syncthreads();
@@ -653,18 +688,11 @@ __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvSt
         }
         __syncthreads();
         // each thread owns elements (ii, j) of the chunk and writes them for every t: per t the
-        // block's stores cover the chunk's rows whole (rows * m contiguous doubles)
+        // block's stores cover the chunk's rows whole (rows * m contiguous floats)
         for (int idx = threadIdx.x; idx < rows * m; idx += blockDim.x) {
             const double2 p = s_par[idx];
-            const bool on = p.y != 0.0;
-            const double sc = p.y < 0.0 ? 10.0 : 1.0, s2 = on ? bump_s2(__builtin_fabs(p.y)) : 1.0;
-            double *o = te + (int64_t)i0 * m + idx;
             float *o32 = st.table32 + e * T * nm + (int64_t)i0 * m + idx;
-            for (int t = 0; t < T; ++t) {
-                const double x = on ? bump_value(sc, p.x, s2, t) : 0.0;
-                o[(int64_t)t * nm] = x;
-                o32[(int64_t)t * nm] = (float)x;
-            }
+            for (int t = 0; t < T; ++t) o32[(int64_t)t * nm] = (float)mt_par_value(p, t);
         }
     }
 }
@@ -752,6 +780,7 @@ static BumpSrc bump_src(const EnvState &st) {
                    st.benefit_mode == ASG_BENEFIT_DENSE};
 }
 static TableSrc table_src(const EnvState &st) { return TableSrc{st.table, st.n, st.m, st.T}; }
+static ParSrc par_src(const EnvState &st) { return ParSrc{st.table32, st.mtpar, st.n, st.m, st.T}; }
 
 static bool uses_table(const EnvState &st) {
     return st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
@@ -769,9 +798,9 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
         if (err != hipSuccess) return err;
         if (gen) {
             const int R = mt_table_rows(st.m);
-            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), sizeof(double2) * R * st.m, s, st.mtpar, st,
-                               st.table, R);
+            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), sizeof(double2) * R * st.m, s, st.mtpar, st, R);
             if ((err = hipGetLastError()) != hipSuccess) return err;
+            return launch_reset_src(par_src(st), bv, st, ts, false, s);
         }
         return launch_reset_src(table_src(st), bv, st, ts, false, s);
     }
@@ -780,6 +809,7 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
 }
 
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
+    if (st.mtpar) return launch_step_src(par_src(st), bv, st, ts, k, s);
     if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s);
     return launch_step_src(bump_src(st), bv, st, ts, k, s);
 }
@@ -797,7 +827,9 @@ hipError_t launch_export_bump_params(const EnvState &st, float *out, hipStream_t
 
 hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s) {
     const size_t lds = sizeof(float) * st.m + 16;
-    if (uses_table(st))
+    if (st.mtpar)
+        hipLaunchKernelGGL((export_table_kernel<ParSrc>), dim3(st.E), dim3(256), lds, s, par_src(st), st, out);
+    else if (uses_table(st))
         hipLaunchKernelGGL((export_table_kernel<TableSrc>), dim3(st.E), dim3(256), lds, s, table_src(st), st, out);
     else
         hipLaunchKernelGGL((export_table_kernel<BumpSrc>), dim3(st.E), dim3(256), lds, s, bump_src(st), st, out);

@@ -1004,8 +1004,9 @@ struct RolloutArgs {
     int reset;  // the envs' reset (asg_reset) runs first, in this launch
     // benefits: NULL = Philox bumps regenerated in registers; else the handle's float64 table
     // [E][T][n][m] (MT19937 compat / injected sat_prox_mat), read for the L lookahead rows
-    const double *table;
-    const float *table32;  // the table rounded to float32: the lookahead rows' reads
+    const double *table;   // injected float64 benefits (rewards), or
+    const double2 *par;    // the MT19937 reset's draws: rewards evaluated from them (mt_par_value)
+    const float *table32;  // the benefits rounded to float32: the lookahead rows' reads
     // QOUT instances: the agent's Q rows [E n][m] f32 (the forward of asg_rnn_agent_forward)
     // instead of the epsilon-greedy selection -- a selector outside the kernel (SAP) acts on them
     float *Q;
@@ -1129,7 +1130,8 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
                 const int j = s_act[i], p = s_prev[i];
                 double beta;
                 if constexpr (TAB) {
-                    beta = ra.table[(((int64_t)e * ra.T + k) * n + i) * m + j];
+                    beta = ra.par ? mt_par_value(ra.par[(e * m + j) * n + i], k)
+                                  : ra.table[(((int64_t)e * ra.T + k) * n + i) * m + j];
                 } else {
                     const Bump32 b =
                         philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
@@ -1677,7 +1679,7 @@ hipError_t launch_rollout_tab(const RolloutArgs &ra, const RolloutLaunch &lc, hi
 }
 #elif ASG_H2_TU == 2
 hipError_t launch_rollout_q(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
-    return ra.table ? launch_rollout_inst<true, true>(ra, lc, s) : launch_rollout_inst<false, true>(ra, lc, s);
+    return ra.table32 ? launch_rollout_inst<true, true>(ra, lc, s) : launch_rollout_inst<false, true>(ra, lc, s);
 }
 #else
 // shapes the rollout kernel takes: the split-f16 agent with the mock env's obs layout
@@ -1736,6 +1738,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.reset = reset;
     const bool tab = st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
     ra.table = tab ? st.table : nullptr;
+    ra.par = tab ? st.mtpar : nullptr;
     ra.table32 = tab ? st.table32 : nullptr;
     if (tab && reset) return hipErrorInvalidValue;  // the table modes' reset is asg_reset (MT19937 stream)
     // Q output: one transition and the forward of the row after it (asg_step_forward)

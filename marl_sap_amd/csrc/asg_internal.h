@@ -29,10 +29,11 @@ struct EnvState {
     const double *T_trans; // device [m][m] or nullptr (= 1 - I)
     int *prev;             // [E][n] previous assignment (state for beta_hat)
     double *returns;       // [E] float64 episode returns
-    double *table;         // [E][T][n][m] float64 (MT19937 / injected modes)
-    float *table32;        // the same rounded to float32 (the rows' dtype): the episode kernel's lookahead reads
+    double *table;         // [E][T][n][m] float64 (injected mode only)
+    float *table32;        // [E][T][n][m] the benefits rounded to float32 (the rows' dtype; MT19937 / injected)
     uint32_t *mt;          // [E][625] MT19937 key + pos (compat mode)
-    double2 *mtpar;        // [E][m][n] the reset's bump draws (center, +-spread; 0: no bump) (compat mode)
+    double2 *mtpar;        // [E][m][n] the reset's bump draws (center, +-spread; 0: no bump) (compat mode):
+                           // the float64 benefits are mt_par_value() of these, no float64 table is kept
     int *assign;           // [E][n] LSA assignments of the bids (bids_as_actions)
     int *err;              // sticky device error code
 };

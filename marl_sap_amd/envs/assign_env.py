@@ -150,7 +150,7 @@ class AssignEnvBatch(MultiAgentEnv):
         """Whether asg_rollout (env steps fused with the agent forward + epsilon-greedy
         selections, up to a whole episode per launch) takes this env: integer actions,
         16 <= m <= 256, n <= 256, L >= 1 -- with the GRU or the Linear RNNAgent -- and any
-        benefit source: Philox bumps regenerated in the kernel, or the float64 table of the
+        benefit source: Philox bumps regenerated in the kernel, or the float32 table of the
         MT19937-compat / injected modes read for the lookahead rows.  `prefer` (kept for
         callers that ask whether it is also the faster schedule): measured on MI355X it is
         wherever it applies."""
