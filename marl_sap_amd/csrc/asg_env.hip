@@ -668,31 +668,61 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
 }
 
 // the reset's table B[e][t][i][j] = mt_par_value(draw, t) (the reference's zeros + bumps, mock
-// :276-299) rounded to float32, the rows' dtype: the draws of `rows` agents (rows * m <= 1024:
-// 16 KiB) staged transposed in LDS, then all T rows of those agents written as whole rows.  The
-// float64 values are not stored: their readers evaluate them from the draws (ParSrc).
+// :276-299) rounded to float32, the rows' dtype.  Per chunk of `rows` agents (rows * m <= 1024):
+// the draws staged transposed in LDS and the chunk's bumps listed (about one pair in four);
+// then per group of kTableTG times the bumps' values are evaluated into a zeroed LDS tile, one
+// bump per thread (the float64 exp / division run for bumps only, not for every element), and
+// the tile is written as whole rows.  The float64 values are not stored: their readers evaluate
+// them from the draws (ParSrc).
+#ifndef ASG_TABLE_TG
+#define ASG_TABLE_TG 4
+#endif
+constexpr int kTableTG = ASG_TABLE_TG;
 static int mt_table_rows(int m) { return m >= 1024 ? 1 : (1024 / m < 16 ? 1024 / m : 16); }
+static size_t mt_table_lds(int R, int m) {
+    return (sizeof(double2) + sizeof(int) + sizeof(float) * kTableTG) * (size_t)R * m;
+}
 __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, int R) {
-    extern __shared__ double2 s_par[];  // [R agents][m tasks]
+    extern __shared__ double2 s_par[];                               // [R agents][m tasks]
+    int *s_list = reinterpret_cast<int *>(s_par + R * st.m);         // the chunk's bumps
+    float *s_tile = reinterpret_cast<float *>(s_list + R * st.m);    // [kTableTG][R * m]
+    __shared__ int s_cnt;
     const int64_t e = blockIdx.x;
     const int n = st.n, m = st.m, T = st.T;
     const int64_t nm = (int64_t)n * m;
     const double2 *pe = par + e * nm;
+    float *te = st.table32 + e * T * nm;
+    for (int x = threadIdx.x; x < kTableTG * R * m; x += blockDim.x) s_tile[x] = 0.f;
     for (int i0 = 0; i0 < n; i0 += R) {
-        const int rows = min(R, n - i0);
+        const int rows = min(R, n - i0), ne = rows * m;
         __syncthreads();
+        if (threadIdx.x == 0) s_cnt = 0;
         // par is [task][agent]: `rows` consecutive agents of a task are contiguous
-        for (int idx = threadIdx.x; idx < rows * m; idx += blockDim.x) {
+        for (int idx = threadIdx.x; idx < ne; idx += blockDim.x) {
             const int ii = idx % rows, j = idx / rows;
             s_par[ii * m + j] = pe[(int64_t)j * n + i0 + ii];
         }
         __syncthreads();
-        // each thread owns elements (ii, j) of the chunk and writes them for every t: per t the
-        // block's stores cover the chunk's rows whole (rows * m contiguous floats)
-        for (int idx = threadIdx.x; idx < rows * m; idx += blockDim.x) {
-            const double2 p = s_par[idx];
-            float *o32 = st.table32 + e * T * nm + (int64_t)i0 * m + idx;
-            for (int t = 0; t < T; ++t) o32[(int64_t)t * nm] = (float)mt_par_value(p, t);
+        for (int idx = threadIdx.x; idx < ne; idx += blockDim.x)
+            if (s_par[idx].y != 0.0) s_list[atomicAdd(&s_cnt, 1)] = idx;
+        __syncthreads();
+        const int cnt = s_cnt;
+        float *o = te + (int64_t)i0 * m;
+        for (int t0 = 0; t0 < T; t0 += kTableTG) {
+            const int tg = min(kTableTG, T - t0);
+            for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+                const int id = s_list[k];
+                const double2 p = s_par[id];
+                for (int tt = 0; tt < tg; ++tt) s_tile[tt * ne + id] = (float)mt_par_value(p, t0 + tt);
+            }
+            __syncthreads();
+            // whole rows out; the tile is left zeroed for the next group
+            for (int tt = 0; tt < tg; ++tt)
+                for (int id = threadIdx.x; id < ne; id += blockDim.x) {
+                    o[(int64_t)(t0 + tt) * nm + id] = s_tile[tt * ne + id];
+                    s_tile[tt * ne + id] = 0.f;
+                }
+            __syncthreads();
         }
     }
 }
@@ -798,7 +828,7 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
         if (err != hipSuccess) return err;
         if (gen) {
             const int R = mt_table_rows(st.m);
-            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), sizeof(double2) * R * st.m, s, st.mtpar, st, R);
+            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), mt_table_lds(R, st.m), s, st.mtpar, st, R);
             if ((err = hipGetLastError()) != hipSuccess) return err;
             return launch_reset_src(par_src(st), bv, st, ts, false, s);
         }
