@@ -818,7 +818,9 @@ static bool uses_table(const EnvState &st) {
 
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s) {
     if (st.rng_mode == ASG_RNG_MT19937) {
-        const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m + 16;
+        // 10,240 B at m = 64: exactly 16 workgroups in a CU's 160 KiB (the LDS is allocated in
+        // 512-byte granules: 16 bytes more would round up to 10,752 B and 15 workgroups)
+        const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m;
         const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
         // with an injected table (sat_prox_mat=) neither __init__ nor reset draw a
         // table: only the permutation consumes the stream (mock :32-37, :99-105)
