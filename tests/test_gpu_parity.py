@@ -222,6 +222,25 @@ def test_mt_multi_env_streams(replicate):
             np.testing.assert_array_equal(prev[e], oe.prev_assigns)
 
 
+@pytest.mark.parametrize("n,m,T,L", [(12, 16, 8, 3), (64, 64, 20, 3), (5, 9, 6, 2)])
+def test_mt_generated_steps_exact_on_export(n, m, T, L):
+    """Same-seed mode keeps no float64 table: the rows come from the reset's float32 table and
+    the rewards / export evaluate the recorded draws.  Replaying the exported table through the
+    oracle must reproduce every row bit for bit (obs == float32 of the export, rewards exact)."""
+    E = 4
+    env = AssignEnvBatch(n, m, T, L, 0.5, seed=21, num_envs=E, device=DEV, rng="mt19937")
+    b = new_batch(env, E)
+    for episode in range(2):
+        env.reset(b, 0)
+        table = env.export_benefits().cpu().numpy()
+        prev0 = env.export_prev_assigns().cpu().numpy()
+        for t in range(T):
+            env.random_actions(b, t)
+            env.step(b, t)
+        env.sync()
+        replay_and_compare(n, m, T, L, 0.5, table, prev0, host(b), env.get_returns().cpu().numpy())
+
+
 def test_mt_injected_steps_golden(golden):
     """Injected tables (sat_prox_mat=) + fixed action sequences, incl. bids."""
     g = golden("mock_step")
