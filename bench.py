@@ -45,6 +45,7 @@ The JSON line also carries:
                   (BASELINE configs[4]: 256 x 256 dense, 2,048 envs, fused rollout).
 """
 import argparse
+import gc
 import glob
 import json
 import os
@@ -191,16 +192,20 @@ def reset_bytes(n, m, L):
     return n * m * (4 * (L + 1) + 4 + 1) + 8 * n + 8
 
 
-def store_ceiling():
-    """The measured HBM store ceiling (GB/s): the best shape of the newest tools/store_bw.hip
-    record under profiles/ (store-only streams over a 4 GiB buffer), with the file name."""
+def store_ceiling(hbm=True):
+    """The measured store ceiling (GB/s): the best shape of the newest tools/store_bw.hip record
+    under profiles/, with the file name.  hbm=True: store-only streams over a buffer far larger
+    than the 256 MiB MALL (the HBM write ceiling); False: the `reuse` shape (one 256 MiB buffer
+    rewritten in a loop, the REDA Q buffer's pattern -- a MALL rate, not an HBM one)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*store_bw*.txt")), key=profile_order, reverse=True)
     for f in files:
         best = 0.0
         for line in open(f):
             if line.startswith("{"):
                 try:
-                    best = max(best, float(json.loads(line)["GBps"]))
+                    d = json.loads(line)
+                    if bool(d.get("hbm", d.get("shape") != "reuse")) == hbm:
+                        best = max(best, float(d["GBps"]))
                 except (ValueError, KeyError):
                     pass
         if best > 0:
@@ -219,9 +224,13 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
     in-order vmcnt queue behind their own row stores).  q_out: the
     asg_step_forward instances (REDA's step_q schedule), which also write the Q rows (4 m per
     agent) and read the actions row the SAP kernel wrote instead of writing one."""
-    # the episode's reset runs in its first launch (asg_reset_rollout): its row counts too
-    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8 + (4 * a.m if q_out else 0))
+    # the episode's reset runs in its first launch (asg_reset_rollout): its row counts too.
+    # q_out: the Q rows go to ONE reused [E n][m] f32 buffer (basic_controller._q_buf, 256 MiB at
+    # configs[2] = the MALL's size) rewritten every step and read back by the SAP kernel: much of
+    # it stays in the Infinity Cache, so its bytes are reported apart (q_buffer), not as HBM traffic
+    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)
                   + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E
+    q_bytes = 4 * a.n * a.m * E if q_out else 0
     per_launch = int(round(per_launch))
     achieved = per_launch / (fused_ms * 1e-3) / 1e9
     frac = achieved / HBM_PEAK_GBS
@@ -252,6 +261,8 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
         rpl = pm.get("resets_per_launch", 1 if spl > 1 else 0)
         rb = reset_bytes(a.n, a.m, a.L) * E
         traffic = round((pm["hbm_bytes_per_launch"] - rpl * rb) / spl + resets_per_step * rb)
+        if q_out:
+            traffic = None  # the PMC bytes mix the Q buffer's MALL-resident writes with HBM
     out = {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(frac, 4),
            "traffic": traffic,
@@ -271,14 +282,46 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
         wgbs = writes / (fused_ms * 1e-3) / 1e9
         out["store_ceiling"] = {"write_bytes_per_launch": int(writes), "achieved_write_GBps": round(wgbs, 1),
                                 "ceiling_GBps": ceil, "frac": round(wgbs / ceil, 4), "source": ceil_src,
-                                "note": "HBM store-only ceiling measured by tools/store_bw.hip on MI355X"}
-    if pm:
+                                "note": "the batch rows' writes (the Q buffer excluded) against the HBM store-only "
+                                        "ceiling measured by tools/store_bw.hip on MI355X (streams over a buffer far "
+                                        "larger than the MALL)"}
+    if q_out:
+        qc, _ = store_ceiling(hbm=False)
+        out["q_buffer"] = {"bytes_per_launch": q_bytes, "GBps_if_alone": round(q_bytes / (fused_ms * 1e-3) / 1e9, 1),
+                           "reuse_store_GBps": qc,
+                           "note": "Q rows [E n][m] f32 written to one reused 256 MiB buffer every step (read back by "
+                                   "the SAP kernel): MALL-resident in large part, so not counted in bytes_per_launch / "
+                                   "frac / store_ceiling; reuse_store_GBps = tools/store_bw.hip's 'reuse' shape"}
+    if pm and traffic:
         out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
         out["traffic_over_algorithmic"] = round(traffic / per_launch, 4)
         out["traffic_note"] = ("PMC bytes per step of the profiled whole-episode launch, its reset row's share "
                                "replaced by this window's resets_per_step (same accounting as bytes_per_launch)")
     if issue:
         out["issue"] = issue
+    return out
+
+
+def random_roofline(a, E, ms, resets_per_step):
+    """The random policy's episode kernel (asg_random_rollout -> random_rollout_kernel), per env
+    step: B_step (the actions row written instead of read) plus the reset row per env for each
+    reset in the window, over its HIP-event time per step."""
+    per_launch = int(round((step_bytes(a.n, a.m, a.L) + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E))
+    achieved = per_launch / (ms * 1e-3) / 1e9
+    pm = pmc_lookup("*pmc_random_rollout*.json", n=a.n, m=a.m, E=E, L=a.L)
+    out = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "asg::random_rollout_kernel (uniform actions + transition, per step)",
+           "kernel_ms": round(ms, 4), "bytes_per_launch": per_launch, "resets_per_step": round(resets_per_step, 4),
+           "b_env_survey_per_launch": (a.n * a.m * (4 * a.L + 13) + 20 * a.n + 9) * E,
+           "per_launch_note": "per env step of the launch: B_step = SURVEY §8(d)'s B_env + the fused int64 one-hot "
+                              "(8nm) - the table read (bumps regenerated, 4nm), + the reset row amortised"}
+    if pm:
+        spl = pm.get("steps_per_launch", 1)
+        rpl = pm.get("resets_per_launch", 1)
+        rb = reset_bytes(a.n, a.m, a.L) * E
+        out["traffic"] = round((pm["hbm_bytes_per_launch"] - rpl * rb) / spl + resets_per_step * rb)
+        out["traffic_pmc"] = os.path.basename(pm.get("_path", ""))
     return out
 
 
@@ -388,6 +431,10 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     from marl_sap_amd.runners import REGISTRY as r_REGISTRY
 
     selector = selector or a.selector
+    mac_name = mac
+    fused_sched = (a.fused_rollout if fused is None else fused) != 0
+    t_setup = time.perf_counter()
+    mem0 = leg_memory(dev)
     args = make_args(a, E, selector, agent, fused, mac=mac, use_rnn=use_rnn, **extra)
     runner = r_REGISTRY["gpu"](args, NullLogger())
     env = runner.get_env()
@@ -466,10 +513,23 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         # on the episode schedule the env reset runs in the episode's first launch
         # (asg_reset_rollout), else as its own launch
         with torch.no_grad():
-            state["mode"] = None if selector == "random" else mac.fused_mode(env, runner.batch, runner.t_env)
-        state["fuse_reset"] = state["mode"] == "episode" and bool(a.fuse_reset)
+            if selector == "random":
+                # the random policy's episode launch (asg_random_rollout), or the split launches
+                state["mode"] = "random_episode" if fused_sched else None
+            else:
+                state["mode"] = mac.fused_mode(env, runner.batch, runner.t_env)
+        state["fuse_reset"] = state["mode"] in ("episode", "random_episode") and bool(a.fuse_reset)
         if not state["fuse_reset"]:
             env.reset(runner.batch, ts=0)
+
+    def advance_random(s_):
+        """s_ steps of the random policy (actions + transitions) in one asg_random_rollout launch"""
+        t = state["t"]
+        rs = t == 0 and state.pop("fuse_reset", False)
+        timed(fused_pairs, lambda: env.random_rollout(runner.batch, t, s_, reset=rs), s_)
+        if rs and state["timing"]:
+            state["fused_resets"] = state.get("fused_resets", 0) + 1
+        state["t"] = t + s_
 
     def advance(s_):
         """s_ transitions (+ their selections) of the current episode in one asg_rollout launch"""
@@ -509,14 +569,15 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         while k > 0:
             if state["t"] >= a.T:
                 new_episode()
-            if state["mode"] == "episode":
+            if state["mode"] in ("episode", "random_episode"):
                 s_ = min(k, a.T - state["t"])
-                advance(s_)
+                (advance if state["mode"] == "episode" else advance_random)(s_)
                 k -= s_
             else:
                 one_step()
                 k -= 1
 
+    setup_elapsed = time.perf_counter() - t_setup
     tw = time.perf_counter()
     run_steps(warmup)
     asg_dist.barrier()
@@ -575,10 +636,30 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
         res["elapsed"], res["kern_ms"], res["sel_ms"] = (float(allr[:, i].max()) for i in range(3))
     res["global_envs"] = runner.global_envs
     runner.close_env()
-    del runner, mac, env
+    # the timing wrappers are instance attributes closing over bound methods of their own
+    # objects (env -> env.step_forward -> env, selector -> select_action -> selector): reference
+    # cycles that only the cyclic GC frees.  Break them, collect, then return the cached blocks,
+    # so the next leg's allocations never meet this leg's buffers still held (round 4: a
+    # ~6 s stall in a later leg's first episode)
+    env.__dict__.pop("step_forward", None)
+    sel_obj.__dict__.pop("select_action", None)
+    del runner, mac, env, sel_obj, inner, inner_fwd
+    gc.collect()
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
+    res["setup_elapsed"] = setup_elapsed
+    res["memory"] = {"before": mem0, "after": leg_memory(dev)}
+    print(f"[bench] leg envs={E} selector={selector} mac={mac_name} setup {setup_elapsed:.2f} s, warmup "
+          f"{warm_elapsed:.3f} s ({warmup} steps), timed {elapsed:.4f} s ({steps} steps), memory {res['memory']}",
+          file=sys.stderr, flush=True)
     return res
+
+
+def leg_memory(dev):
+    """Device memory at a leg's edges (GB): torch's allocated / reserved, and free per hipMemGetInfo."""
+    free, total = torch.cuda.mem_get_info(dev)
+    return {"allocated_gb": round(torch.cuda.memory_allocated(dev) / 1e9, 2),
+            "reserved_gb": round(torch.cuda.memory_reserved(dev) / 1e9, 2), "free_gb": round(free / 1e9, 2)}
 
 
 def res_resets(res):
@@ -658,6 +739,8 @@ def main():
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     if res.get("mode") == "step_q" and res.get("step_forward_ms"):
         roof = fused_roofline(a, E, res["step_forward_ms"], use_rnn=a.use_rnn, q_out=True)
+    elif res.get("mode") == "random_episode" and res.get("fused_ms"):
+        roof = random_roofline(a, E, res["fused_ms"], res_resets(res))
     elif res.get("fused_ms"):
         roof = fused_roofline(a, E, res["fused_ms"], resets_per_step=res_resets(res))
     else:
@@ -768,25 +851,31 @@ def main():
             for k in ("n", "m", "envs", "benefits", "selector"):
                 setattr(c1, k, CONFIGS[1][k])
             c1.config = 1
-            r1 = run_leg(c1, dev, world, c1.envs, sk, sw)
-            sb = step_bytes(c1.n, c1.m, c1.L) * c1.envs
-            gbs = sb / (r1["kern_ms"] * 1e-3) / 1e9 if r1["kern_ms"] else None
-            pm1 = pmc_lookup("*pmc_step_kernel*.json", n=c1.n, m=c1.m, E=c1.envs, L=c1.L)
+            # the random policy's episode launch (asg_random_rollout: reset + T x (actions +
+            # transition) in one launch), with the split launches (asg_random_actions + asg_step per
+            # step) beside it
+            r1 = run_leg(c1, dev, world, c1.envs, max(sk, 4 * a.T), sw)
+            sk1 = max(sk, 4 * a.T)
             extra["config1"] = {
-                **leg_base(r1, sk, sw),
-                "workload": CONFIGS[1]["label"] + f"; T={a.T}, L={a.L}: asg_random_actions + asg_step per step",
+                **leg_base(r1, sk1, sw),
+                "workload": CONFIGS[1]["label"] + f"; T={a.T}, L={a.L}: asg_random_rollout (the episode's reset, "
+                                                  "uniform actions and transitions in one launch)",
                 "envs_per_gpu": c1.envs, "n": c1.n, "m": c1.m,
-                "kernels_ms": {"env_step": round(r1["kern_ms"], 4) if r1["kern_ms"] else None,
-                               "random_actions": round(r1["sel_ms"], 4) if r1["sel_ms"] else None},
-                "roofline": {"bound": "hbm", "kernel": "asg::step_kernel", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                             "achieved": round(gbs, 1) if gbs else None,
-                             "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
-                             "bytes_per_launch": sb, "b_env_survey_per_launch": (c1.n * c1.m * (4 * c1.L + 13)
-                                                                                 + 20 * c1.n + 9) * c1.envs,
-                             "traffic": pm1.get("hbm_bytes_per_launch") if pm1 else None,
-                             "note": "B_step = SURVEY §8(d)'s B_env + the fused int64 one-hot (8nm) - the table read "
-                                     "(bumps regenerated, 4nm); launch-bound at this size: 4,096 envs x 7.75 KB "
-                                     "= 32 MB per launch"}}
+                "kernels_ms": {"random_rollout_per_step": round(r1["fused_ms"], 4) if r1.get("fused_ms") else None},
+                "roofline": random_roofline(c1, c1.envs, r1["fused_ms"], res_resets(r1)) if r1.get("fused_ms") else None}
+            r1s = run_leg(c1, dev, world, c1.envs, sk, sw, fused=0)
+            sb = step_bytes(c1.n, c1.m, c1.L) * c1.envs
+            gbs = sb / (r1s["kern_ms"] * 1e-3) / 1e9 if r1s["kern_ms"] else None
+            extra["config1_split"] = {
+                **leg_base(r1s, sk, sw),
+                "workload": CONFIGS[1]["label"] + f"; T={a.T}, L={a.L}: asg_random_actions + asg_step per step",
+                "kernels_ms": {"env_step": round(r1s["kern_ms"], 4) if r1s["kern_ms"] else None,
+                               "random_actions": round(r1s["sel_ms"], 4) if r1s["sel_ms"] else None},
+                "env_step_roofline": {"kernel": "asg::step_kernel", "unit": "GB/s",
+                                      "achieved": round(gbs, 1) if gbs else None,
+                                      "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None, "bytes_per_launch": sb,
+                                      "note": "one launch per step: 4,096 envs x 7.75 KB = 32 MB per launch, "
+                                              "launch-bound"}}
             # the same-seed mode (rng="mt19937": env e replays numpy's legacy stream seeded with
             # seed + e, the reference's draws) on the episode kernel: configs[2] with the handle's
             # float32 benefit table read for the lookahead rows (the float64 rewards evaluated from

@@ -22,7 +22,8 @@
  *                              OneHot preprocess (episode_runner.py:80-95,
  *                              parallel_runner.py:141-200, components/episode_buffer.py:89-129,
  *                              components/transforms.py:12-22)
- *   asg_random_actions         a uniform random policy (BASELINE config 2)
+ *   asg_random_actions         a uniform random policy (BASELINE configs[1])
+ *   asg_random_rollout         that policy's episode (reset + T x (actions + step)) in one launch
  *   asg_set_benefits           MockConstellationEnv(sat_prox_mat=...) injection
  *                              (mock_constellation_env.py:22, :32-37)
  *   asg_beta_hat               MockConstellationEnv.beta_hat (mock_constellation_env.py:228-274)
@@ -156,6 +157,13 @@ int asg_reset(asg_handle *h, const asg_batch_view *b, int ts);
 int asg_step(asg_handle *h, const asg_batch_view *b, int ts);
 /* Uniform random actions in [0, m) at row ts (Philox keyed (seed, env, episode, t)). */
 int asg_random_actions(asg_handle *h, const asg_batch_view *b, int ts);
+/* The random policy's episode in one launch: for the next `steps` steps of every env, the
+ * actions asg_random_actions draws (written at rows ts ..) and the transitions asg_step makes
+ * (rows ts .. ts + steps); reset != 0 first runs asg_reset's reset into row ts (not in the
+ * MT19937 mode: its reset is asg_reset).  Results equal asg_reset + steps x
+ * (asg_random_actions + asg_step), bit for bit (episode_runner.py:60-100 with a uniform
+ * policy over mock_constellation_env.py:94-162). */
+int asg_random_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int reset);
 /* Blocks until the handle's stream drains; returns the first sticky device error. */
 int asg_sync_status(asg_handle *h);
 

@@ -42,7 +42,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_filtered_benefits", "asg_filtered_epsilon_greedy", "asg_filtered_soft_map", "asg_real_haal_select",
            "asg_real_haal_num_sequences", "asg_step_select", "asg_step_select_l2_slices", "asg_rollout",
            "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward",
-           "asg_sap_noise"]
+           "asg_sap_noise", "asg_random_rollout"]
 
 
 class AsgField(ctypes.Structure):
@@ -106,6 +106,7 @@ def lib():
         L.asg_set_stream.argtypes = [vp, vp]
         for f in ("asg_reset", "asg_step", "asg_random_actions"):
             getattr(L, f).argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
+        L.asg_random_rollout.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, i32, i32]
         L.asg_sync_status.argtypes = [vp]
         L.asg_set_benefits.argtypes = [vp, vp, i64, i32]
         L.asg_export_benefits.argtypes = [vp, vp]

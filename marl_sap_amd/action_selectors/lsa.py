@@ -54,8 +54,9 @@ def raise_on_status(status):
 
 class DeferredStatus:
     """Accumulates LSA status on the device so the rollout loop never syncs per step;
-    `flush()` (called by the runner once per episode) raises the first error.  `sticky(B)`:
-    a zeroed per-env int32 word that kernels min-accumulate into themselves
+    `flush()` (called by the runner once per episode) raises the minimum status seen (error
+    codes are negative: the most negative, not necessarily the first).  `sticky(B)`: a zeroed
+    per-env int32 word that kernels min-accumulate into themselves
     (asg_sap_select_into) -- no reduction launches per call."""
 
     def __init__(self):

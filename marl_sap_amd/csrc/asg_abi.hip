@@ -232,6 +232,37 @@ int asg_random_actions(asg_handle *h, const asg_batch_view *b, int ts) {
     return ASG_OK;
 }
 
+int asg_random_rollout(asg_handle *h, const asg_batch_view *b, int ts, int steps, int reset) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    if (int rc = check_view(h, b, ts, false)) return rc;
+    const asg::EnvState &st = h->st;
+    if (st.bids) return fail(h, ASG_E_INVALID_ARG, "asg_random_rollout: integer actions only (not bids_as_actions)");
+    if (b->actions.ptr && b->actions.dtype != ASG_I64)
+        return fail(h, ASG_E_INVALID_ARG, "random actions need an int64 actions field");
+    if (reset && st.rng_mode == ASG_RNG_MT19937)
+        return fail(h, ASG_E_INVALID_ARG, "asg_random_rollout: the MT19937 mode's reset is asg_reset (its stream)");
+    if (reset && st.benefit_mode == ASG_BENEFIT_INJECTED && !h->table_ready)
+        return fail(h, ASG_E_STATE, "benefit_mode=injected needs asg_set_benefits before reset");
+    if (!h->has_reset && !reset) return fail(h, ASG_E_STATE, "step called before reset");
+    const int k0 = reset ? 0 : h->k;
+    if (steps < 1 || k0 + steps > st.T)
+        return fail(h, ASG_E_STATE, "asg_random_rollout: steps must be >= 1 and stay within the episode (k + steps <= T)");
+    if (ts < 0 || ts + steps > st.T)
+        return fail(h, ASG_E_INVALID_ARG, "asg_random_rollout: batch rows ts .. ts + steps must lie in the [T + 1]-row batch");
+    DeviceGuard g(h->device);
+    asg::EnvState lst = h->st;
+    if (reset && h->has_reset) lst.episode += 1;  // as asg_reset: a fresh Philox key per episode
+    hipError_t e = asg::launch_random_rollout(*b, lst, ts, k0, steps, reset != 0, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_random_rollout");
+    h->st.episode = lst.episode;
+    if (reset) {
+        h->constructed = true;
+        h->has_reset = true;
+    }
+    h->k = k0 + steps;
+    return ASG_OK;
+}
+
 int asg_sync_status(asg_handle *h) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     DeviceGuard g(h->device);

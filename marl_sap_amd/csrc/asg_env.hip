@@ -373,6 +373,102 @@ __global__ void random_actions_kernel(asg_batch_view bv, EnvState st, int ts, in
 }
 
 // ------------------------------------------------------------------------------------
+// the random policy's whole episode in one launch (asg_random_rollout): for steps k0 ..
+// k0 + steps - 1 of every env, the uniform actions of asg_random_actions (same Philox
+// counters) and the transition of step_kernel, optionally after the reset of reset_kernel
+// (same Fisher-Yates draws) -- one workgroup per env keeps prev_assigns, the actions, the
+// task scales and the return in LDS across the steps; results are those of asg_reset +
+// T x (asg_random_actions + asg_step), bit for bit.  Reference: mock_constellation_env.py:
+// 94-162 (reset / step) driven by episode_runner.py:60-100 with a uniform policy.
+// ------------------------------------------------------------------------------------
+template <int VEC, class Src>
+__global__ void __launch_bounds__(256) random_rollout_kernel(Src src, asg_batch_view bv, EnvState st, int ts0,
+                                                             int k0, int steps, int reset) {
+    extern __shared__ int s_dyn[];
+    const int64_t e = blockIdx.x;
+    const int n = st.n, m = st.m, T = st.T, L = st.L;
+    int *s_act = s_dyn;                                                          // [n]
+    int *s_cnt = s_act + n;                                                      // [m] (the reset's permutation)
+    float *s_scale = reinterpret_cast<float *>(s_cnt + m);                       // [m]
+    int *s_prev = reinterpret_cast<int *>(s_scale + m);                          // [n]
+    double *s_rew = reinterpret_cast<double *>(s_prev + n + ((2 * n + 2 * m) & 1));  // [n], 8-aligned
+    __shared__ double s_ret;
+    src.fill_scale(e, s_scale);
+    const auto env = src.bind(e, s_scale);
+    const EnvKey key = env_key(st.seed, st.env_base + e);
+    if (reset) {
+        // reset_kernel: Fisher-Yates from the top, Philox-drawn, one thread (the same draws)
+        for (int j = threadIdx.x; j < m; j += blockDim.x) s_cnt[j] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = m - 1; i >= 1; --i) {
+                const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, 0u, kCtrPerm, st.episode}, key.k0, key.k1);
+                const int jj = (int)(((uint64_t)r.x * (uint64_t)(i + 1)) >> 32);
+                const int t = s_cnt[i];
+                s_cnt[i] = s_cnt[jj];
+                s_cnt[jj] = t;
+            }
+            s_ret = 0.0;
+            if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts0, 0, 0) = 1;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            s_prev[i] = s_cnt[i];
+            if (bv.prev_assigns.ptr)
+                *fptr<int64_t>(bv.prev_assigns, e, ts0, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : s_cnt[i];
+        }
+        write_pre_row<VEC>(env, bv, e, ts0, 0, n, m, T, L, nullptr, -1);
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) s_prev[i] = st.prev[e * n + i];
+        if (threadIdx.x == 0) s_ret = st.returns[e];
+    }
+    for (int it = 0; it < steps; ++it) {
+        const int k = k0 + it, ts = ts0 + it;
+        __syncthreads();  // the previous step's counts / actions are consumed
+        for (int j = threadIdx.x; j < m; j += blockDim.x) s_cnt[j] = 0;
+        __syncthreads();
+        // random_actions_kernel's draw: action of agent i at step k
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const u32x4 r = philox4x32_10(u32x4{(uint32_t)i, (uint32_t)k, kCtrAction, st.episode}, key.k0, key.k1);
+            const int a = (int)(((uint64_t)r.x * (uint64_t)m) >> 32);
+            if (bv.actions.ptr) *fptr<int64_t>(bv.actions, e, ts, i, 0) = a;
+            s_act[i] = a;
+            atomicAdd(&s_cnt[a], 1);
+        }
+        __syncthreads();
+        // step_kernel's rewards (mock :126-138)
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const int j = s_act[i];
+            const int p = s_prev[i];
+            const double beta = env.pair(i, j).at64(k);
+            const double tt = st.T_trans ? st.T_trans[(int64_t)p * m + j] : (j == p ? 0.0 : 1.0);
+            const double pen = tt * (beta > 1e-12 ? 1.0 : 0.0);
+            const double bh = beta - st.lambda_ * pen;
+            const double r = bh > 0.0 ? bh / (double)s_cnt[j] : bh;
+            s_rew[i] = r;
+            if (bv.rewards.ptr) *fptr<float>(bv.rewards, e, ts, i, 0) = (float)r;
+            s_prev[i] = j;
+            if (bv.prev_assigns.ptr)
+                *fptr<int64_t>(bv.prev_assigns, e, ts + 1, i, 0) = (st.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : j;
+        }
+        write_pre_row<VEC>(env, bv, e, ts + 1, k + 1, n, m, T, L, s_act, ts);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double sum = 0.0;  // Python's sum(rewards), left to right
+            for (int i = 0; i < n; ++i) sum += s_rew[i];
+            s_ret += sum;
+            bool term = k + 1 >= T;
+            if (st.quirks & ASG_QUIRK_PARALLEL_TERMINATED) term = (e != 0);
+            if (bv.terminated.ptr) *fptr<uint8_t>(bv.terminated, e, ts, 0, 0) = term;
+            if (bv.filled.ptr) *fptr<int64_t>(bv.filled, e, ts + 1, 0, 0) = 1;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) st.prev[e * n + i] = s_prev[i];
+    if (threadIdx.x == 0) st.returns[e] = s_ret;
+}
+
+// ------------------------------------------------------------------------------------
 // table export (Philox bumps -> [E][n][m][T] float64, the reference layout)
 // ------------------------------------------------------------------------------------
 template <class Src>
@@ -844,6 +940,29 @@ hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int
     if (st.mtpar) return launch_step_src(par_src(st), bv, st, ts, k, s);
     if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s);
     return launch_step_src(bump_src(st), bv, st, ts, k, s);
+}
+
+template <class Src>
+static hipError_t launch_random_rollout_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts,
+                                            int k0, int steps, bool reset, hipStream_t s) {
+    const size_t lds = sizeof(int) * (size_t)(2 * st.n + 2 * st.m + 2) + sizeof(double) * st.n + 16;
+    // one wave per 64 work items of the row writer (VEC tasks each), at most 4 waves
+    const int64_t items = (int64_t)st.n * ((st.m + 3) / 4);
+    const int threads = items >= 256 ? 256 : (int)((items + 63) / 64 * 64);
+    if (vec4_ok(bv, st.m))
+        hipLaunchKernelGGL((random_rollout_kernel<4, Src>), dim3(st.E), dim3(threads), lds, s, src, bv, st, ts, k0, steps,
+                           reset ? 1 : 0);
+    else
+        hipLaunchKernelGGL((random_rollout_kernel<1, Src>), dim3(st.E), dim3(threads), lds, s, src, bv, st, ts, k0, steps,
+                           reset ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_random_rollout(const asg_batch_view &bv, const EnvState &st, int ts, int k0, int steps, bool reset,
+                                 hipStream_t s) {
+    if (st.mtpar) return launch_random_rollout_src(par_src(st), bv, st, ts, k0, steps, reset, s);
+    if (uses_table(st)) return launch_random_rollout_src(table_src(st), bv, st, ts, k0, steps, reset, s);
+    return launch_random_rollout_src(bump_src(st), bv, st, ts, k0, steps, reset, s);
 }
 
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {

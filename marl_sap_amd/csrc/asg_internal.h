@@ -55,6 +55,8 @@ struct SelectArgs {
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s);
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
+hipError_t launch_random_rollout(const asg_batch_view &bv, const EnvState &st, int ts, int k0, int steps, bool reset,
+                                 hipStream_t s);
 hipError_t launch_export_table(const EnvState &st, double *out, hipStream_t s);
 hipError_t launch_export_bump_params(const EnvState &st, float *out, hipStream_t s);
 hipError_t launch_import_table(const double *in, int64_t src_envs, const EnvState &st, hipStream_t s);

@@ -294,8 +294,8 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
         }
     }
     if (kCount && lane == 0) steps_out[b] = steps;
-    // asg_sap_select_into accumulates: the env's status word keeps its minimum (the first error)
-    // over the episode's calls, read once per episode instead of reduced after every call
+    // asg_sap_select_into accumulates: the env's status word keeps its minimum over the episode's
+    // calls (error codes are negative: the most negative code seen, not the first one), read once per episode instead of reduced after every call
     if (lane == 0 && status_out) status_out[b] = act_out ? min(status_out[b], status) : status;
 }
 
@@ -366,16 +366,14 @@ hipError_t launch_sap_noise(const float *q, const int64_t qs[3], int64_t B, int 
     return hipGetLastError();
 }
 
-// occupancy experiments: ASG_SAP_LDS_PAD=<bytes> of unused dynamic LDS per 4-wave workgroup
-// caps the resident waves (e.g. 81920: 2 workgroups = 2 waves per SIMD) -- the rollout
-// kernel's residency, to price an LSA fused into it; 0 (default) = none
-static size_t sap_lds_pad() {
-    static const size_t v = [] {
-        const char *e = getenv("ASG_SAP_LDS_PAD");
-        return e ? (size_t)atol(e) : (size_t)0;
-    }();
-    return v;
-}
+// occupancy experiments (compile-time, like ASG_SAP_STAGE_ONLY): -DASG_SAP_LDS_PAD=<bytes> of
+// unused dynamic LDS per 4-wave workgroup caps the resident waves (e.g. 81920: 2 workgroups = 2
+// waves per SIMD) -- the rollout kernel's residency, to price an LSA fused into it; 0 = none
+#ifndef ASG_SAP_LDS_PAD
+#define ASG_SAP_LDS_PAD 0
+#endif
+static_assert(ASG_SAP_LDS_PAD >= 0 && ASG_SAP_LDS_PAD <= 160 * 1024, "ASG_SAP_LDS_PAD exceeds the CU's LDS");
+static constexpr size_t sap_lds_pad() { return (size_t)ASG_SAP_LDS_PAD; }
 
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,

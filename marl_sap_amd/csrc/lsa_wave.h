@@ -600,7 +600,9 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
     const uint64_t colmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
     const float kOutF = __builtin_bit_cast(float, 0x7fc00000u);
     // row reduction (u_k = min_j c_kj, float32: exact) then column reduction of the rest
-    // (v_j = min_k (c_kj - u_k), float64: exact for float32 operands): both the agents' and the
+    // (v_j = min_k (c_kj - u_k) in float64: each difference rounded once, relative 2^-53, far
+    // inside the certificate's S 2^-40 slack -- not exact when the operands' exponents differ by
+    // more than ~29 bits; dual feasibility is re-checked by the certificate): both the agents' and the
     // tasks' common offsets come out, so the column minima spread over more rows than a column
     // reduction alone leaves them (SAP Q: -16..28 % augmenting-path steps in the host model)
     float amax = 0.0f;

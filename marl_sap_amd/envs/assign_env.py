@@ -217,6 +217,14 @@ class AssignEnvBatch(MultiAgentEnv):
     def random_actions(self, batch, ts):
         self._call("asg_random_actions", ctypes.byref(batch_view(batch)), int(ts))
 
+    def random_rollout(self, batch, ts, steps, reset=False):
+        """The uniform random policy's next `steps` steps in one launch (asg_random_rollout):
+        random_actions(ts + s) + step(ts + s) for s < steps, after reset(ts) when `reset` --
+        bit-identical to those separate calls."""
+        self._call("asg_random_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps), int(bool(reset)))
+        self.k = (0 if reset else self.k) + int(steps)
+        return self.k >= self.T
+
     def sync(self):
         """Block on the env's stream and raise the first sticky device error, if any."""
         self._call("asg_sync_status")

@@ -154,14 +154,17 @@ class GpuVecRunner:
             self.flush_pending()
 
     def flush_pending(self):
-        """Host side of the finished episodes: device errors, selector status, logging."""
-        self.env.sync()
+        """Host side of the finished episodes: selector status, device errors, logging.
+        The selectors' status goes first: an env whose noisy Q was invalid gets -1 in its actions
+        row (asg_sap_select_into) and the next transition then sets the env's sticky action-range
+        error -- the LSA's "invalid numeric entries" is the cause and is the error raised."""
         for sel in (getattr(self.mac, "action_selector", None), getattr(self.mac, "jumpstart_action_selector", None)):
             if hasattr(sel, "flush"):
                 sel.flush()
             st = getattr(sel, "status", None)
             if hasattr(st, "flush"):
                 st.flush()
+        self.env.sync()
         for (returns, test_mode), steps in zip(self._pending, self._pending_steps):
             self.last_returns = returns
             cur_stats = self.test_stats if test_mode else self.train_stats

@@ -1,0 +1,131 @@
+"""The random policy's whole-episode launch (asg_random_rollout, BASELINE configs[1]): one
+launch per episode (reset + T x (uniform actions + transition)) against the separate
+asg_reset + asg_random_actions + asg_step launches it replaces -- every batch field, the
+returns and the env state bit for bit -- and, at configs[1]'s full size (16 x 16, 4,096 envs),
+the size-independent invariants plus the oracle replay of test_gpu_parity.py's
+test_full_size_episode_properties.  Reference: mock_constellation_env.py:94-162 driven by
+episode_runner.py:60-100 under a uniform policy."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected on CPU, but never run there
+    pytest.skip("needs a ROCm GPU", allow_module_level=True)
+
+from marl_sap_amd.components import EpisodeBatch  # noqa: E402
+from marl_sap_amd.envs import AssignEnvBatch  # noqa: E402
+from oracle.check import replay_and_compare  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def new_batch(env, E, time_major=True):
+    return EpisodeBatch(env.scheme, {"agents": env.n}, E, env.T + 1, preprocess=env.preprocess, device=DEV,
+                        time_major=time_major)
+
+
+def host(batch):
+    return {k: v.cpu().numpy() for k, v in batch.data.transition_data.items()}
+
+
+def split_episode(env, b, T):
+    env.reset(b, 0)
+    for t in range(T):
+        env.random_actions(b, t)
+        env.step(b, t)
+
+
+@pytest.mark.parametrize("n,m,E,T,L,chunks,time_major,kw", [
+    (16, 16, 512, 20, 3, (20,), True, {}),              # configs[1]'s shape, one launch per episode
+    (16, 16, 256, 20, 3, (7, 1, 12), True, {}),          # chunked launches
+    (64, 64, 64, 20, 3, (20,), True, {}),                # 256-thread workgroups
+    (20, 25, 96, 11, 2, (5, 6), False, {}),              # m % 4 != 0 (scalar row writer), batch-major view
+    (33, 41, 40, 9, 0, (9,), True, {}),                  # L = 0: no lookahead blocks
+    (16, 16, 128, 12, 3, (12,), True, {"benefits": "dense"}),
+    (16, 16, 64, 10, 3, (10,), True, {"quirks": ("prev_assigns_zero", "parallel_terminated")}),
+])
+def test_random_rollout_equals_split_launches(n, m, E, T, L, chunks, time_major, kw):
+    a = AssignEnvBatch(n, m, T, L, 0.5, seed=77, num_envs=E, device=DEV, **kw)
+    f = AssignEnvBatch(n, m, T, L, 0.5, seed=77, num_envs=E, device=DEV, **kw)
+    for episode in range(2):  # the second episode: a fresh Philox key, as asg_reset's
+        ba, bf = new_batch(a, E, time_major), new_batch(f, E, time_major)
+        split_episode(a, ba, T)
+        t = 0
+        for i, s in enumerate(chunks):
+            done = f.random_rollout(bf, t, s, reset=(i == 0))
+            t += s
+            assert done == (t >= T)
+        a.sync()
+        f.sync()
+        ha, hf = host(ba), host(bf)
+        assert ha.keys() == hf.keys()
+        for k in ha:
+            np.testing.assert_array_equal(ha[k], hf[k], err_msg=f"{k} (episode {episode})")
+        assert torch.equal(a.get_returns(), f.get_returns())
+        assert torch.equal(a.export_prev_assigns(), f.export_prev_assigns())
+    a.close()
+    f.close()
+
+
+def test_random_rollout_continues_split_state():
+    """A launch that starts mid-episode (no reset) picks up the handle's state the split
+    launches left (prev_assigns, returns, the step counter)."""
+    n, m, E, T, L = 16, 16, 128, 10, 3
+    a = AssignEnvBatch(n, m, T, L, 0.5, seed=5, num_envs=E, device=DEV)
+    f = AssignEnvBatch(n, m, T, L, 0.5, seed=5, num_envs=E, device=DEV)
+    ba, bf = new_batch(a, E), new_batch(f, E)
+    split_episode(a, ba, T)
+    f.reset(bf, 0)
+    for t in range(4):
+        f.random_actions(bf, t)
+        f.step(bf, t)
+    f.random_rollout(bf, 4, T - 4)
+    ha, hf = host(ba), host(bf)
+    for k in ha:
+        np.testing.assert_array_equal(ha[k], hf[k], err_msg=k)
+    assert torch.equal(a.get_returns(), f.get_returns())
+
+
+def test_random_rollout_rejects_bad_ranges():
+    n, m, E, T, L = 16, 16, 8, 5, 1
+    env = AssignEnvBatch(n, m, T, L, 0.5, seed=1, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    with pytest.raises(Exception, match="before reset"):
+        env.random_rollout(b, 0, 2)
+    with pytest.raises(Exception, match="stay within the episode"):
+        env.random_rollout(b, 0, T + 1, reset=True)
+    env.random_rollout(b, 0, T, reset=True)
+    with pytest.raises(Exception, match="stay within the episode"):
+        env.random_rollout(b, T, 1)
+
+
+def test_random_rollout_full_size_configs1():
+    """configs[1] at full size on the episode launch: invariants on every env and the oracle
+    replay of sampled envs (as test_full_size_episode_properties does for the split launches)."""
+    n, m, E, T, L = 16, 16, 4096, 20, 3
+    env = AssignEnvBatch(n, m, T, L, 0.5, seed=2024, num_envs=E, device=DEV)
+    b = new_batch(env, E)
+    env.random_rollout(b, 0, T, reset=True)
+    env.sync()
+    prev0 = b["prev_assigns"][:, 0].clone()
+    obs, beta = b["obs"], b["beta"]
+    acts = b["actions"][:, :T, :, 0]
+    oh = torch.zeros((E, T, n, m), dtype=torch.int64, device=DEV).scatter_(-1, acts.unsqueeze(-1), 1)
+    assert torch.equal(obs[:, 1:, :, :m].to(torch.int64), oh)
+    assert torch.equal(b["actions_onehot"][:, :T], oh)
+    assert torch.equal(beta[:, :T], obs[:, :T, :, m:2 * m])
+    assert torch.equal(obs[:, 1:T, :, 2 * m:3 * m], obs[:, 2:T + 1, :, m:2 * m])
+    assert (beta[:, T] == 0).all() and (obs[:, T, :, m:] == 0).all()
+    assert b["avail_actions"].all() and (b["filled"] == 1).all()
+    assert torch.equal(b["prev_assigns"][:, 1:], acts)
+    srt = prev0.sort(dim=1)[0]
+    assert (srt[:, 1:] != srt[:, :-1]).all() and (prev0 >= 0).all() and (prev0 < m).all()
+    r = env.get_returns()
+    assert torch.allclose(b["rewards"][:, :T].double().sum((1, 2)), r, rtol=1e-5, atol=1e-4)
+    idx = np.array(sorted({0, 1, 777, E // 4 + 3, E // 2 - 1, E // 2 + 5, 3 * E // 4 + 7, E - 2, E - 1}))
+    table = env.export_benefits()[idx].cpu().numpy()
+    td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
+    replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy(), philox=True)

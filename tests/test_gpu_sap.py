@@ -186,3 +186,36 @@ def test_sap_fast_path_full_size():
         col = ora.lsa(noisy[b].astype(np.float64), maximize=True)[1]
         assert np.array_equal(out[b], col.astype(np.float32)), b
     assert ((steps >> 16) == 0).mean() > 0.99
+
+
+@pytest.mark.parametrize("gap_log2,expect", [(-40, "fallback"), (-30, "fallback"), (-23, "any"), (-20, "certified")])
+def test_sap_fast_path_planted_near_tie(gap_log2, expect):
+    """A second assignment planted at a small cost gap from the unique optimum: rows i1, i2 can
+    only take columns i1, i2 (every other entry of theirs is -10; every other row prefers its
+    own diagonal by ~9), and Q[i2, i1] = base - gap makes the swap worse by exactly `gap`
+    (base = 2^-22: ulp 2^-45, so the gap is exact in float32).  With S (max|c| + max|u| +
+    max|v|) of order 2^4..2^5, gaps 2^-40 (~S 2^-45) and 2^-30 (~S 2^-35) leave both swap
+    edges near-tight (<= S 2^-30): the certificate must refuse and the scipy-exact solver run;
+    2^-20 (~S 2^-25) must certify; 2^-23 sits just above the threshold band.  Every problem
+    equals scipy's assignment (the C oracle)."""
+    rng = np.random.RandomState(1000 - gap_log2)
+    B, n = 256, 64
+    q = (rng.uniform(-1.0, 1.0, size=(B, n, n)) + 10.0 * np.eye(n)).astype(np.float32)
+    base, gap = np.float32(2.0 ** -22), 2.0 ** gap_log2
+    for b in range(B):
+        i1, i2 = rng.choice(n, 2, replace=False)
+        q[b, [i1, i2], :] = -10.0
+        q[b, :, [i1, i2]] = np.minimum(q[b, :, [i1, i2]], -10.0)
+        q[b, i1, i1] = q[b, i2, i2] = q[b, i1, i2] = base
+        q[b, i2, i1] = np.float32(float(base) - gap)
+        assert float(q[b, i1, i1]) + float(q[b, i2, i2]) - float(q[b, i1, i2]) - float(q[b, i2, i1]) == gap
+    out, st, steps = _sap_raw(torch.as_tensor(q, device=DEV), 0.0, 1, 1)
+    out, st, steps = out.cpu().numpy(), st.cpu().numpy(), steps.cpu().numpy()
+    assert (st == 0).all()
+    for b in range(B):
+        assert np.array_equal(out[b], ora.lsa(q[b].astype(np.float64), maximize=True)[1].astype(np.float32)), b
+    exact = steps >> 16
+    if expect == "fallback":
+        assert (exact > 0).all(), (exact == 0).sum()
+    elif expect == "certified":
+        assert (exact == 0).all(), (exact > 0).sum()
