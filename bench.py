@@ -638,15 +638,17 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     runner.close_env()
     # the timing wrappers are instance attributes closing over bound methods of their own
     # objects (env -> env.step_forward -> env, selector -> select_action -> selector): reference
-    # cycles that only the cyclic GC frees.  Break them, collect, then return the cached blocks,
-    # so the next leg's allocations never meet this leg's buffers still held (round 4: a
-    # ~6 s stall in a later leg's first episode)
+    # cycles that only the cyclic GC frees.  Break them and collect, so this leg's buffers go
+    # back to torch's caching allocator -- and stay there: the next leg's batch (the same 41 GB
+    # at configs[2]) reuses the cached block.  No empty_cache(): handing the blocks back to the
+    # driver made every leg hipMalloc a fresh 41 GB, and once the never-used VRAM ran out (~7
+    # legs) the driver cleared recycled pages on allocation -- a 5.5-6.1 s torch.zeros in a
+    # later leg's first episode (round 4's `jumpstart_phase_value` stall)
     env.__dict__.pop("step_forward", None)
     sel_obj.__dict__.pop("select_action", None)
     del runner, mac, env, sel_obj, inner, inner_fwd
     gc.collect()
     torch.cuda.synchronize()
-    torch.cuda.empty_cache()
     res["setup_elapsed"] = setup_elapsed
     res["memory"] = {"before": mem0, "after": leg_memory(dev)}
     print(f"[bench] leg envs={E} selector={selector} mac={mac_name} setup {setup_elapsed:.2f} s, warmup "

@@ -551,7 +551,20 @@ __device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[
                             if (j0 + v < nout) qp[v] = qv[v];
                     }
                 }
-                if (SEL) {
+                if (SEL && ALLAV && !GEN) {
+                    // every task available and inside the row (the rollout at m % 32 == 0): the
+                    // lane's first task (c = 0, v = 0) is its first candidate, then strictly
+                    // greater or the first NaN -- the torch.max order below without the
+                    // availability / range terms
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int j = j0 + v;
+                        const float x = qv[v];
+                        const bool b = (c == 0 && v == 0) | ((best[nt] == best[nt]) & !(x <= best[nt]));
+                        best[nt] = b ? x : best[nt];
+                        bj[nt] = b ? j : bj[nt];
+                    }
+                } else if (SEL) {
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
                         // a lane meets its tasks in increasing j, so torch.max order reduces
@@ -567,6 +580,12 @@ __device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[
                 }
             }
         }
+    }
+    if (SEL && ALLAV && !GEN) {
+        // the availability masks the exploration draw reads: every task of the lane's tiles
+        const uint64_t all = nct >= 16 ? ~0ull : ((1ull << (4 * nct)) - 1ull);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) amask[nt][0] = all;
     }
     if (SEL) {
         const int act = select_finish<false, NT>(best, bj, amask, rows, ok, oidx, nct, sel, q);
@@ -1050,18 +1069,27 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <class RA>
+// The env shape as the rollout code reads it: SQ = 0 takes n, m from the launch arguments; the
+// SQ = 64 instances (n = m = 64, configs[2]'s shape) see them as compile-time constants, so the
+// tile's loops unroll and its row / task offsets fold into immediates
+template <int SQ, class RA>
+__device__ __forceinline__ int rs_n(RA &ra) { return SQ ? SQ : ra.n; }
+template <int SQ, class RA>
+__device__ __forceinline__ int rs_m(RA &ra) { return SQ ? SQ : ra.m; }
+
+template <int SQ = 0, class RA>
 __device__ __forceinline__ H2Args rollout_h2args(RA &ra) {
     H2Args a{};
-    a.R = ra.E * ra.n;
-    a.g.K = ra.m * (ra.L + 1);
-    a.g.P = ra.m;
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra);
+    a.R = ra.E * n;
+    a.g.K = m * (ra.L + 1);
+    a.g.P = m;
     a.g.NB = ra.L + 1;
-    a.g.Pp = rollout_mp(ra.m);
+    a.g.Pp = rollout_mp(m);
     a.g.Kp = a.g.Pp * (ra.L + 1);
     a.g.prefix = 1;
-    a.g.nout = ra.m;
-    a.g.nct = (ra.m + 15) / 16;
+    a.g.nout = m;
+    a.g.nct = (m + 15) / 16;
     a.pre = 1;
     a.pk = ra.pk;
     a.W1T = ra.W1T;
@@ -1071,8 +1099,8 @@ __device__ __forceinline__ H2Args rollout_h2args(RA &ra) {
     a.b2 = ra.b2;
     a.Hout = ra.Hout;
     a.w1_lds = ra.w1_lds;
-    a.sel = SelectArgs{nullptr, 0, 0, ra.n, ra.epsilon, ra.sk0, ra.sk1, ra.counter, ra.env_base * ra.n, nullptr,
-                       (int64_t)ra.n, 1, ra.sel_err};
+    a.sel = SelectArgs{nullptr, 0, 0, n, ra.epsilon, ra.sk0, ra.sk1, ra.counter, ra.env_base * n, nullptr,
+                       (int64_t)n, 1, ra.sel_err};
     return a;
 }
 
@@ -1101,7 +1129,7 @@ __device__ __forceinline__ void rollout_actions_from_batch(RA &ra, int64_t e, in
 // one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
 // terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
 // launch, or read from the batch by the env prologue)
-template <bool TAB, class RA>
+template <bool TAB, int SQ, class RA>
 __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int ts, const EnvKey &key,
                                                    const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
                                                    uint16_t *s_prev, double *s_ret) {
@@ -1111,7 +1139,7 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
     int lane_ = threadIdx.x & 63;
     asm volatile("" : "+v"(lane_));
     const int lane = lane_;
-    const int n = ra.n, m = ra.m, mp = rollout_mp(m);
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), mp = rollout_mp(m);
     for (int j = lane; j < mp; j += 64) s_cnt[j] = 0;
     wave_lds_fence();
     for (int i = lane; i < n; i += 64) atomicAdd(&s_cnt[s_act[i]], 1);
@@ -1188,10 +1216,14 @@ struct HNext {
     int mode;
 };
 
+// 1: the n = m = 64 shape runs the compile-time-shape instances (0: the runtime-shape ones, A/B)
+#ifndef ASG_ROLLOUT_SQ64
+#define ASG_ROLLOUT_SQ64 1
+#endif
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
-template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, bool AGENT, class RA>
+template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, bool AGENT, int SQ, class RA>
 __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
                                              uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
@@ -1204,7 +1236,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
     int lane_ = threadIdx.x & 63;
     asm volatile("" : "+v"(lane_));
     const int lane = lane_, r = lane & 15, q = lane >> 4;
-    const int n = ra.n, m = ra.m, T = ra.T, L = ra.L;
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), T = ra.T, L = ra.L;
     const int K = m * (L + 1);
     const int Ub = rollout_mp(m) >> 5;
     const int64_t row0 = e * n + RT * sub;
@@ -1479,7 +1511,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
         if (attempt > 0 || __ballot(any) == 0) break;
     }
     if constexpr (AGENT) {
-        H2Args a = rollout_h2args(ra);
+        H2Args a = rollout_h2args<SQ>(ra);
         a.sel.counter = ra.counter + (uint32_t)pass;
         a.sel.out = ra.act + (int64_t)tsr * ra.E * n;
         if constexpr (QOUT) a.Q = ra.Q;
@@ -1521,7 +1553,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
     }
 }
 
-template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT>
+template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, int SQ>
 __global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
 rollout_kernel(RolloutArgs ra) {
     extern __shared__ u32x4v s_h2[];
@@ -1529,7 +1561,7 @@ rollout_kernel(RolloutArgs ra) {
     h2_stage<RNN, W2L>(rollout_h2args(ra), s_h2, sw);
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n = ra.n, m = ra.m, mp = rollout_mp(m), np = rollout_np(n);
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), mp = rollout_mp(m), np = rollout_np(n);
     char *scr = reinterpret_cast<char *>(s_h2 + ra.scratch_off) + wv * rollout_scratch_bytes(n, m);
     uint64_t *s_scl = reinterpret_cast<uint64_t *>(scr);
     double *s_ret = reinterpret_cast<double *>(scr + 32);
@@ -1614,7 +1646,7 @@ rollout_kernel(RolloutArgs ra) {
             const int ts = ri.ts0 + (k - ri.k0);
             const bool first_sel = it < sf;
             if (!first_sel)
-                rollout_transition<TAB>(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
+                rollout_transition<TAB, SQ>(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
             const int kk = k + 1;
             if (has_agent(ri, it)) {
                 const bool next_agent = has_agent(ri, it + 1);
@@ -1626,14 +1658,14 @@ rollout_kernel(RolloutArgs ra) {
                                                     (int64_t)(16 * kH2NT) * (sub + 1), 1};
                     else if (next_agent) nx = HNext{ri.Hout, kHid, 0, 1};
                     // the reset row (select_first) is stored here when the reset runs in this launch
-                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, true>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
+                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, true, SQ>(RA_, e, sub, kk, ts + 1, !first_sel || ri.reset, !first_sel, pass,
                                                       key, s_scl, s_act, s_h2, sw, hN, hpf, nx);
                     hpf = nx.mode != 0;
                 }
                 ++pass;
             } else {
                 for (int sub = 0; sub < ntile; ++sub)
-                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, false>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
+                    rollout_tile<RNN, W2L, GEN, TAB, QOUT, false, SQ>(RA_, e, sub, kk, ts + 1, true, true, 0, key, s_scl, s_act, s_h2,
                                                        sw, hN, false, HNext{nullptr, kHid, 0, 0});
             }
 #undef RA_
@@ -1652,18 +1684,21 @@ struct RolloutLaunch {
     unsigned grid;
     size_t lds;
     bool rnn, w2l, gen;
+    bool sq64;  // n = m = 64 (W2 in LDS, no ragged tiles): the compile-time-shape instances
 };
 template <bool TAB, bool QOUT>
 static hipError_t launch_rollout_inst(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
-#define LR_(RNN, W2L, GEN) \
-    hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, TAB, QOUT>), dim3(lc.grid), dim3(64 * kH2Waves), lc.lds, s, ra)
-#define LR2_(RNN)                                                        \
-    do {                                                                 \
-        if (lc.w2l) {                                                    \
-            if (lc.gen) LR_(RNN, true, true); else LR_(RNN, true, false);   \
-        } else {                                                         \
-            if (lc.gen) LR_(RNN, false, true); else LR_(RNN, false, false); \
-        }                                                                \
+#define LR_(RNN, W2L, GEN, SQ) \
+    hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, TAB, QOUT, SQ>), dim3(lc.grid), dim3(64 * kH2Waves), lc.lds, s, ra)
+#define LR2_(RNN)                                                                \
+    do {                                                                         \
+        if (lc.sq64) {                                                           \
+            LR_(RNN, true, false, 64);                                           \
+        } else if (lc.w2l) {                                                     \
+            if (lc.gen) LR_(RNN, true, true, 0); else LR_(RNN, true, false, 0);   \
+        } else {                                                                 \
+            if (lc.gen) LR_(RNN, false, true, 0); else LR_(RNN, false, false, 0); \
+        }                                                                        \
     } while (0)
     if (lc.rnn) LR2_(true); else LR2_(false);
 #undef LR2_
@@ -1771,6 +1806,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     lc.rnn = rnn;
     lc.w2l = plan.w2l;
     lc.gen = st.m % 32 != 0 || st.n % 32 != 0;
+    lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64;
     if (Q) return launch_rollout_q(ra, lc, s);
     if (tab) return launch_rollout_tab(ra, lc, s);
     return launch_rollout_inst<false, false>(ra, lc, s);
