@@ -251,6 +251,10 @@ __device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4
 // also receives each row's selected task (index lrow0 + row within the tile).
 // 1: the GRU's (1 - z) n + z h takes h back from its split-f16 planes (h_hi + h_lo, exact to
 // 2^-22) instead of keeping the f32 h live through the gate products
+// 1: the GRU layer is compiled once per h_zero case (no branch between its hidden blocks)
+#ifndef ASG_GRU_HOIST
+#define ASG_GRU_HOIST 1
+#endif
 #ifndef ASG_H2_H_FROM_PLANES
 #define ASG_H2_H_FROM_PLANES 0
 #endif
@@ -377,6 +381,10 @@ __device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[
             scS[nt] = pow2f(Sg[nt]);
         }
         const lds_u4p Wih = Wr, Whh = (lds_u4p)(Wl + 3 * kGateF4);
+        // the whole recurrent layer per h_zero case: no branch between the four hidden blocks,
+        // so the scheduler can overlap one block's gate math with the next block's MFMAs
+        auto gru = [&](auto hz_tag) {
+        constexpr bool HZ = decltype(hz_tag)::value;
 #pragma unroll
         for (int hb = 0; hb < 4; ++hb) {
             // r and z sum the input and hidden products in one accumulator, from b_i + b_h;
@@ -402,7 +410,7 @@ __device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[
                         acc_ = mfma_h2(w, xP[sl][nt], acc_);
                     }
                 }
-            if (!h_zero) {
+            if (!HZ && !h_zero) {
 #pragma unroll
                 for (int sl = 0; sl < 2; ++sl)
 #pragma unroll
@@ -441,6 +449,13 @@ __device__ __forceinline__ void h2_tail(A &a, const u32x4v *Wl, const int (&sw)[
                     *reinterpret_cast<float4 *>(a.Hout + rows[nt] * kHid + 16 * hb + 4 * q) =
                         make_float4(hp[hb][nt][0], hp[hb][nt][1], hp[hb][nt][2], hp[hb][nt][3]);
         }
+        };
+#if ASG_GRU_HOIST
+        if (h_zero) gru(std::true_type{});
+        else gru(std::false_type{});
+#else
+        gru(std::false_type{});  // h_zero tested per block inside (the round-4 form)
+#endif
     } else {
         // Linear + ReLU (use_rnn = False): h' = relu(W_rnn x + b_rnn), one gate of planes
         float scS[NT], un[NT];
@@ -1069,6 +1084,14 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// 1: the n = m = 64 shape runs the compile-time-shape instances (0: the runtime-shape ones, A/B)
+#ifndef ASG_ROLLOUT_SQ64
+#define ASG_ROLLOUT_SQ64 1
+#endif
+// 1: the SQ = 64 instances also fix L = 3 (launched only when L == 3)
+#ifndef ASG_SQ64_L3
+#define ASG_SQ64_L3 1
+#endif
 // The env shape as the rollout code reads it: SQ = 0 takes n, m from the launch arguments; the
 // SQ = 64 instances (n = m = 64, configs[2]'s shape) see them as compile-time constants, so the
 // tile's loops unroll and its row / task offsets fold into immediates
@@ -1076,17 +1099,20 @@ template <int SQ, class RA>
 __device__ __forceinline__ int rs_n(RA &ra) { return SQ ? SQ : ra.n; }
 template <int SQ, class RA>
 __device__ __forceinline__ int rs_m(RA &ra) { return SQ ? SQ : ra.m; }
+// ... and L = 3 (configs[2]'s lookahead) when ASG_SQ64_L3: the lookahead loop unrolls
+template <int SQ, class RA>
+__device__ __forceinline__ int rs_L(RA &ra) { return (SQ && ASG_SQ64_L3) ? 3 : ra.L; }
 
 template <int SQ = 0, class RA>
 __device__ __forceinline__ H2Args rollout_h2args(RA &ra) {
     H2Args a{};
-    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra);
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), L = rs_L<SQ>(ra);
     a.R = ra.E * n;
-    a.g.K = m * (ra.L + 1);
+    a.g.K = m * (L + 1);
     a.g.P = m;
-    a.g.NB = ra.L + 1;
+    a.g.NB = L + 1;
     a.g.Pp = rollout_mp(m);
-    a.g.Kp = a.g.Pp * (ra.L + 1);
+    a.g.Kp = a.g.Pp * (L + 1);
     a.g.prefix = 1;
     a.g.nout = m;
     a.g.nct = (m + 15) / 16;
@@ -1216,10 +1242,6 @@ struct HNext {
     int mode;
 };
 
-// 1: the n = m = 64 shape runs the compile-time-shape instances (0: the runtime-shape ones, A/B)
-#ifndef ASG_ROLLOUT_SQ64
-#define ASG_ROLLOUT_SQ64 1
-#endif
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
@@ -1236,7 +1258,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
     int lane_ = threadIdx.x & 63;
     asm volatile("" : "+v"(lane_));
     const int lane = lane_, r = lane & 15, q = lane >> 4;
-    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), T = ra.T, L = ra.L;
+    const int n = rs_n<SQ>(ra), m = rs_m<SQ>(ra), T = ra.T, L = rs_L<SQ>(ra);
     const int K = m * (L + 1);
     const int Ub = rollout_mp(m) >> 5;
     const int64_t row0 = e * n + RT * sub;
@@ -1806,7 +1828,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     lc.rnn = rnn;
     lc.w2l = plan.w2l;
     lc.gen = st.m % 32 != 0 || st.n % 32 != 0;
-    lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64;
+    lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64 && (!ASG_SQ64_L3 || st.L == 3);
     if (Q) return launch_rollout_q(ra, lc, s);
     if (tab) return launch_rollout_tab(ra, lc, s);
     return launch_rollout_inst<false, false>(ra, lc, s);
