@@ -237,6 +237,17 @@ int asg_sap_select(const float *q, const int64_t q_strides[3], int64_t B, int n,
 int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
                         double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
                         int64_t *act_out, int32_t *status_out, int32_t *path_steps_out, void *hip_stream);
+/* asg_sap_select_into with the certified fast path warm-started (square problems): duals
+ * [B][64] float64 (device, 8-B aligned) holds each env's column duals from its previous call
+ * and receives this call's (NaN for an env whose fast path did not finish); warm = 0 ignores
+ * the input (the first call).  Same assignments as asg_sap_select_into -- scipy's, whatever
+ * duals the search starts from (the result is used only under the uniqueness certificate,
+ * else the scipy-exact solver runs) -- in fewer augmenting-path steps on consecutive steps'
+ * SAP Q-values (sap_selectors.py:60-98 called once per step of an episode). */
+int asg_sap_select_warm(const float *q, const int64_t q_strides[3], int64_t B, int n, int m,
+                        double epsilon, uint64_t seed, uint64_t counter, int64_t env_index_base,
+                        int64_t *act_out, int32_t *status_out, int32_t *path_steps_out, double *duals,
+                        int warm, void *hip_stream);
 /* The matrix asg_sap_select solves for the same arguments: q_out [B][n][m] f32 contiguous =
  * Q + the selector's noise (parity tooling: the selection at epsilon > 0 is checked against
  * scipy on it).  status_out [B] (may be NULL): 0 or ASG_E_LSA_INVALID. */

@@ -42,7 +42,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_filtered_benefits", "asg_filtered_epsilon_greedy", "asg_filtered_soft_map", "asg_real_haal_select",
            "asg_real_haal_num_sequences", "asg_step_select", "asg_step_select_l2_slices", "asg_rollout",
            "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward",
-           "asg_sap_noise", "asg_random_rollout"]
+           "asg_sap_noise", "asg_random_rollout", "asg_sap_select_warm"]
 
 
 class AsgField(ctypes.Structure):
@@ -106,7 +106,8 @@ def lib():
         L.asg_set_stream.argtypes = [vp, vp]
         for f in ("asg_reset", "asg_step", "asg_random_actions"):
             getattr(L, f).argtypes = [vp, ctypes.POINTER(AsgBatchView), i32]
-        L.asg_random_rollout.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, i32, i32]
+        if hasattr(L, "asg_random_rollout"):  # absent from older A/B builds (tools/build_rev.sh)
+            L.asg_random_rollout.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, i32, i32]
         L.asg_sync_status.argtypes = [vp]
         L.asg_set_benefits.argtypes = [vp, vp, i64, i32]
         L.asg_export_benefits.argtypes = [vp, vp]
@@ -162,10 +163,12 @@ def lib():
                                         i32, vp, i64, vp, dbl, u64, u64, vp, vp]
         L.asg_sap_select_into.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp, vp]
         L.asg_sap_noise.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp]
+        if hasattr(L, "asg_sap_select_warm"):  # absent from older A/B builds
+            L.asg_sap_select_warm.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp, vp, i32, vp]
         L.asg_step_forward.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, vp, vp, vp, vp, vp, i32, i32, i32, vp,
                                        i64, vp, vp, vp]
         for f in EXPORTS:
-            if f not in ("asg_last_error", "asg_real_destroy"):
+            if f not in ("asg_last_error", "asg_real_destroy") and hasattr(L, f):
                 getattr(L, f).restype = i32
         L.asg_rnn_agent_packed_size.restype = i64
         if L.asg_abi_version() != 1:

@@ -22,7 +22,9 @@ class SequentialAssignmentProblemSelector:
     """REDA selector: Gaussian noise of std 2*eps*mean|Q| per env, then LSA(maximize).
 
     n <= m <= 64: one fused HIP kernel (asg_sap_select: noise drawn in registers from
-    Philox keyed by (seed, global env index, call counter), register-resident LSA).
+    Philox keyed by (seed, global env index, call counter), register-resident LSA); writing
+    into the batch's actions row (the runner's step_q schedule) with n == m, the certified
+    fast path starts from each env's previous column duals (asg_sap_select_warm).
     Larger problems: the noise from torch, then asg_lsa_batched."""
 
     def __init__(self, args):
@@ -37,6 +39,11 @@ class SequentialAssignmentProblemSelector:
         # instrumentation (bench.py): an int32 [B] device tensor receives every env's count of
         # augmenting-path steps of the next fused call
         self.count_steps = None
+        # the fast path's warm start (asg_sap_select_warm): each env's column duals from its
+        # previous selection, [B, 64] float64 on the device; args.sap_warm_start = False opts out.
+        # Assignments do not depend on it (certified or solved by scipy's algorithm).
+        self.warm_start = bool(getattr(args, "sap_warm_start", True))
+        self._duals = None
 
     def _env_index_base(self):
         return env_index_base(self)
@@ -62,6 +69,15 @@ class SequentialAssignmentProblemSelector:
             with torch.cuda.device(q.device):
                 if into:
                     status = self.status.sticky(B, q.device)  # min-accumulated by the kernel
+                    if self.warm_start and n == m:
+                        d = self._duals
+                        warm = int(d is not None and d.shape[0] == B and d.device == q.device)
+                        if not warm:
+                            d = self._duals = torch.empty((B, 64), dtype=torch.float64, device=q.device)
+                        _lib.check(_lib.lib().asg_sap_select_warm(
+                            *common, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), steps,
+                            ctypes.c_void_p(d.data_ptr()), warm, _lib.stream_ptr(q.device)))
+                        return out
                     _lib.check(_lib.lib().asg_sap_select_into(
                         *common, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), steps,
                         _lib.stream_ptr(q.device)))

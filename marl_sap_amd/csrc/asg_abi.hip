@@ -426,6 +426,22 @@ int asg_sap_select_into(const float *q, const int64_t q_strides[3], int64_t B, i
     return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select_into");
 }
 
+int asg_sap_select_warm(const float *q, const int64_t q_strides[3], int64_t B, int n, int m, double epsilon,
+                        uint64_t seed, uint64_t counter, int64_t env_index_base, int64_t *act_out,
+                        int32_t *status_out, int32_t *path_steps_out, double *duals, int warm, void *hip_stream) {
+    if (!q || !q_strides || !act_out || !duals || B < 0 || n <= 0 || m <= 0 || env_index_base < 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_warm: bad arguments");
+    if (n > m || m > 64) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_warm: needs n <= m <= 64");
+    if (!(epsilon >= 0.0)) return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_warm: epsilon must be >= 0");
+    if ((reinterpret_cast<uintptr_t>(duals) & 7) != 0)
+        return fail(nullptr, ASG_E_INVALID_ARG, "asg_sap_select_warm: duals must be 8-B aligned");
+    if (B == 0) return ASG_OK;
+    hipError_t e = asg::launch_sap_select(q, q_strides, B, n, m, (float)epsilon, seed, (uint32_t)counter,
+                                          env_index_base, nullptr, status_out, path_steps_out,
+                                          static_cast<hipStream_t>(hip_stream), act_out, duals, warm ? 1 : 0);
+    return e == hipSuccess ? ASG_OK : hip_fail(nullptr, e, "asg_sap_select_warm");
+}
+
 int asg_sap_noise(const float *q, const int64_t q_strides[3], int64_t B, int n, int m, double epsilon,
                   uint64_t seed, uint64_t counter, int64_t env_index_base, float *q_out, int32_t *status_out,
                   void *hip_stream) {

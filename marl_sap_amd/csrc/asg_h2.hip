@@ -183,7 +183,8 @@ struct H2Args {
     const float *b1, *bi, *bh, *b2;  // GRU: b_ih, b_hh; Linear: b_rnn, unused
     float *Hout, *Q;
     SelectArgs sel;
-    int w1_lds;        // W1 slices [s0, s0 + w1_lds) staged in LDS (s0 = pre ? Pp / 32 : 0)
+    int w1_lds;        // W1 slices [s0 + w1_off, s0 + w1_off + w1_lds) staged in LDS (s0 = pre ? Pp / 32 : 0)
+    int w1_off;        // 1: the first main slice (s0) stays in L2 (the rollout reads it before its stores)
 };
 
 constexpr int kH2NT = 2;                        // 16-row tiles per wave: 32 rows
@@ -234,7 +235,7 @@ __device__ __forceinline__ void h2_stage(const H2Args &a, u32x4v *s, int (&sw)[4
         for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) s[off + i] = rec[nrec + i];
     }
     {
-        const u32x4v *w1 = a.pk + 1 + w1_idx(h2_s0(a), 0, 0, 0);
+        const u32x4v *w1 = a.pk + 1 + w1_idx(h2_s0(a) + a.w1_off, 0, 0, 0);
         const int64_t n1 = (int64_t)a.w1_lds * 4 * 2 * 64, off = lds_w1_off(RNN, g.nct, W2L);
         for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) s[off + i] = w1[i];
     }
@@ -1050,7 +1051,7 @@ struct RolloutArgs {
     int64_t hs;
     float *Hout;
     const float *b1, *bi, *bh, *b2;
-    int w1_lds;
+    int w1_lds, w1_off;  // LDS-resident W1 slices: [s0 + w1_off, s0 + w1_off + w1_lds)
     float epsilon;
     uint32_t sk0, sk1, counter;
     int *sel_err;
@@ -1088,9 +1089,10 @@ __device__ __forceinline__ void wave_lds_fence() {
 #ifndef ASG_ROLLOUT_SQ64
 #define ASG_ROLLOUT_SQ64 1
 #endif
-// 1: the SQ = 64 instances also fix L = 3 (launched only when L == 3)
+// 1: the SQ = 64 instances also fix L = 3 (launched only when L == 3): the unrolled lookahead
+// loop spills 28 VGPRs instead of 14 and ran 0.709-0.713 vs 0.570-0.574 ms/step (r5 A/B) -- off
 #ifndef ASG_SQ64_L3
-#define ASG_SQ64_L3 1
+#define ASG_SQ64_L3 0
 #endif
 // The env shape as the rollout code reads it: SQ = 0 takes n, m from the launch arguments; the
 // SQ = 64 instances (n = m = 64, configs[2]'s shape) see them as compile-time constants, so the
@@ -1125,6 +1127,7 @@ __device__ __forceinline__ H2Args rollout_h2args(RA &ra) {
     a.b2 = ra.b2;
     a.Hout = ra.Hout;
     a.w1_lds = ra.w1_lds;
+    a.w1_off = ra.w1_off;
     a.sel = SelectArgs{nullptr, 0, 0, n, ra.epsilon, ra.sk0, ra.sk1, ra.counter, ra.env_base * n, nullptr,
                        (int64_t)n, 1, ra.sel_err};
     return a;
@@ -1242,6 +1245,16 @@ struct HNext {
     int mode;
 };
 
+// 1: with W2 in LDS and an fc1 slice in L2 (64 x 64: 1 of 6; the SQ64 instances), that slice is
+// the tile's first, consumed before its stores (0: the last one, read behind them -- round 4)
+#ifndef ASG_ROLLOUT_L2FIRST
+#define ASG_ROLLOUT_L2FIRST 1
+#endif
+// 1: under l2first the first block's rows are stored after its MFMAs (the L2 weights then wait
+// for the prefix rows only)
+#ifndef ASG_L2FIRST_LATE
+#define ASG_L2FIRST_LATE 1
+#endif
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
@@ -1312,7 +1325,12 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(hN[t][nt]));
     }
-    if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
+    // w1_off (the SQ64 instances): the first main slice's weights live in L2; they are loaded
+    // in the tile's first lookahead block and consumed by its MFMAs before any store of the
+    // tile is issued (the prefix rows are deferred behind them), so the wait for them covers no
+    // store of this tile -- loaded last (round 4), they waited for nearly all of them
+    const bool l2first = AGENT && SQ == 64 && ra.w1_off;
+    auto prefix_stores = [&]() {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
         // actions_onehot of the transition before the row (none before the reset row)
         int64_t *oh_r = (ra.onehot && have_act) ? ra.onehot + ((int64_t)(tss - 1) * ra.E * n + sro) * m : nullptr;
@@ -1350,13 +1368,14 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 for (int off = off0; off < nrow * m; off += 64) ab[off] = 1;
             }
         }
-    }
+    };
+    if (stores && !(ASG_ROLLOUT_XSKIP & 1)) prefix_stores();
     // ---- the lookahead blocks 1..L (times kk .. kk + L - 1), fc1 on them -------------------
     BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
     bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
     const lds_f4v Bs = (lds_f4v)(Wl + rec_f4(RNN));
     const u32x4v *W1g = ra.pk + 1;
-    const int s0 = Ub, s_l2 = s0 + ra.w1_lds;
+    const int s0 = Ub, s_l2 = s0 + ra.w1_off + ra.w1_lds;
     float *beta_r = ra.beta ? ra.beta + ((int64_t)tss * ra.E * n + sro) * m : nullptr;
     const bool live = kk < T;  // rows past T are zeros: no bump parameters needed
     for (int attempt = 0;; ++attempt) {
@@ -1422,6 +1441,9 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
             }
             for (int l = 1; l <= L; ++l) {
                 const int t = kk + l - 1;
+                // the tile's first slice under l2first: the L2 one, read (mma(false)) before any
+                // store of this tile; its rows and the deferred prefix rows follow its MFMAs
+                const bool first = l2first && u == 0 && l == 1 && attempt == 0;
                 // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
                 // past T are zeros)
                 float4 xv[2][NT];
@@ -1481,7 +1503,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 // an L2 weight slice (no W2 in LDS: the large shapes, 19 of 24 slices at 256 x 256):
                 // its weights are loaded before this block's row stores and the stores follow the
                 // MFMAs, so the loads wait for the previous block's stores only
-                const bool late = ASG_ROLLOUT_LATE && !W2L && AGENT && l * Ub + u >= s_l2;
+                const bool late = (ASG_ROLLOUT_LATE && !W2L && AGENT && l * Ub + u >= s_l2) || (ASG_L2FIRST_LATE && first);
                 if (st_now && !late) store_rows();
                 if (AGENT) {
                     // the agent kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
@@ -1504,7 +1526,8 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                                 const lds_u4p W1s = (lds_u4p)(Wl + lds_w1_off(RNN, (m + 15) / 16, W2L));
 #pragma unroll
                                 for (int pl = 0; pl < 2; ++pl)
-                                    w[pl] = W1s[w1_idx((ASG_ROLLOUT_XSKIP & 4) && sl >= s_l2 ? 0 : sl - s0, mt, pl, lane)];
+                                    w[pl] = W1s[w1_idx((ASG_ROLLOUT_XSKIP & 4) && sl >= s_l2 ? 0 : sl - s0 - ra.w1_off, mt,
+                                                       pl, lane)];
                             } else {
 #pragma unroll
                                 for (int pl = 0; pl < 2; ++pl) w[pl] = W1g[w1_idx(sl, mt, pl, lane)];
@@ -1513,7 +1536,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma_h2(w, xp[nt], acc[mt][nt]);
                         }
                     };
-                    if (sl < s_l2 || (ASG_ROLLOUT_XSKIP & 4))
+                    if ((sl >= s0 + ra.w1_off && sl < s_l2) || (ASG_ROLLOUT_XSKIP & 4))
                         mma(true);
                     else
                         mma(false);
@@ -1819,6 +1842,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     const int64_t scr_f4 = ((int64_t)rollout_scratch_bytes(st.n, st.m) * kH2Waves + 15) / 16;
     const H2Lds plan = h2_lds_plan(g, rnn, g.Pp / 32, scr_f4);
     ra.w1_lds = plan.w1_lds;
+    ra.w1_off = 0;  // 1 with the SQ64 instances (below)
     ra.scratch_off = plan.scratch_off;
     const int ncu = stream_cus(s);
     const int64_t wgs = (st.E + kH2Waves - 1) / kH2Waves;
@@ -1829,6 +1853,8 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     lc.w2l = plan.w2l;
     lc.gen = st.m % 32 != 0 || st.n % 32 != 0;
     lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64 && (!ASG_SQ64_L3 || st.L == 3);
+    // the L2 fc1 slice read first, before the tile's stores (rollout_tile's l2first)
+    if (lc.sq64 && ASG_ROLLOUT_L2FIRST && plan.l2_slices >= 1) ra.w1_off = 1;
     if (Q) return launch_rollout_q(ra, lc, s);
     if (tab) return launch_rollout_tab(ra, lc, s);
     return launch_rollout_inst<false, false>(ra, lc, s);

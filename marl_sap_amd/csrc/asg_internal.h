@@ -72,7 +72,8 @@ hipError_t launch_beta_hat(const void *beta, int dtype, const int64_t bs[3], con
                            double *out, hipStream_t s);
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             int32_t *steps_out, hipStream_t s, int64_t *act_out = nullptr);
+                             int32_t *steps_out, hipStream_t s, int64_t *act_out = nullptr,
+                             double *duals = nullptr, int warm = 0);
 hipError_t launch_sap_noise(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon, uint64_t seed,
                             uint32_t counter, int64_t env_base, float *q_out, int32_t *status_out, hipStream_t s);
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],

@@ -302,11 +302,15 @@ __device__ __forceinline__ void sap_emit(int64_t b, int status, int c4r, int ste
 #ifndef ASG_SAP_PIN
 #define ASG_SAP_PIN 1
 #endif
-template <bool kCount, bool kDense64>
+// kWarm: `duals` [B][64] float64 holds each env's column duals from its previous selection --
+// the fast path's warm start (lsa_fast_reg64) -- and receives this selection's (NaN when the
+// fast path did not finish: the next call starts that env cold)
+template <bool kCount, bool kDense64, bool kWarm = false>
 __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_eu(ASG_LSA_REG_WAVES))) sap_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n,
                                                         int m, float epsilon, uint64_t seed, uint32_t counter,
                                                         int64_t env_base, float *col_out, int64_t *act_out,
-                                                        int32_t *status_out, int32_t *steps_out, int64_t B) {
+                                                        int32_t *status_out, int32_t *steps_out, int64_t B,
+                                                        double *duals = nullptr, int warm = 0) {
     __shared__ uint64_t s_slot[kLsaWpb][64];
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
@@ -330,8 +334,18 @@ __global__ void __launch_bounds__(64 * kLsaWpb) __attribute__((amdgpu_waves_per_
     return;
 #endif
     bool done = false;
-    if (ASG_SAP_FAST && status == ASG_OK && n == m)
+    if constexpr (kWarm) {
+        const int lane = threadIdx.x & 63;
+        double *dp = duals + b * 64 + lane;
+        const double vin = warm ? *dp : __builtin_nan("");
+        double vnew = __builtin_nan("");
+        if (ASG_SAP_FAST && status == ASG_OK && n == m)
+            done = lsa_fast_reg64<decltype(rc), kCount, true>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6], vin, &vnew) ==
+                   ASG_OK;
+        *dp = vnew;
+    } else if (ASG_SAP_FAST && status == ASG_OK && n == m) {
         done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
+    }
     if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
     // instrumented instance: fast-path steps in the low 16 bits, scipy-exact steps above
     sap_emit<kCount>(b, status, c4r[0], nfast | (nsteps << 16), n, m, col_out, act_out, status_out, steps_out);
@@ -377,15 +391,27 @@ static constexpr size_t sap_lds_pad() { return (size_t)ASG_SAP_LDS_PAD; }
 
 hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon,
                              uint64_t seed, uint32_t counter, int64_t env_base, float *col_out, int32_t *status_out,
-                             int32_t *steps_out, hipStream_t s, int64_t *act_out) {
+                             int32_t *steps_out, hipStream_t s, int64_t *act_out, double *duals, int warm) {
     const dim3 grid = lsa_reg_grid(B);
     const size_t pad = sap_lds_pad();
     // the rollout's Q rows ([B][64][64] contiguous): the unguarded staging instance
     const bool d64 = n == 64 && m == 64 && qs[2] == 1 && qs[1] == 64 && (reinterpret_cast<uintptr_t>(q) & 3) == 0;
 #define SAP_L(C, D)                                                                                                 \
     hipLaunchKernelGGL((sap_select_kernel<C, D>), grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m, \
-                       epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B)
-    if (steps_out) {
+                       epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B, nullptr, 0)
+#define SAP_LW(C, D)                                                                                                   \
+    hipLaunchKernelGGL((sap_select_kernel<C, D, true>), grid, dim3(64 * kLsaWpb), pad, s, q, qs[0], qs[1], qs[2], n, m, \
+                       epsilon, seed, counter, env_base, col_out, act_out, status_out, steps_out, B, duals, warm)
+    if (duals) {  // warm-started fast path (square problems; the runner's selection)
+        if (steps_out) {
+            if (d64) SAP_LW(true, true);
+            else SAP_LW(true, false);
+        } else {
+            if (d64) SAP_LW(false, true);
+            else SAP_LW(false, false);
+        }
+#undef SAP_LW
+    } else if (steps_out) {
         if (d64) SAP_L(true, true);
         else SAP_L(true, false);
     } else {

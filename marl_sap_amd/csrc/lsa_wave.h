@@ -584,6 +584,17 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 // scipy-exact solver from scratch.
 // Returns ASG_OK (col4row set), or kLsaUncertified.  `slot`: 64 uint64 of LDS scratch for
 // this wave.
+//
+// Warm start (kWarm, `vwarm` = this lane's column dual from an earlier call, e.g. the previous
+// step's selection of the same env): the column duals carry the task profile the SAP Q-values
+// share from step to step, so the row reduction runs against them -- u_k = min_j (c_kj - v_j),
+// each row taking the lowest untaken column at that exact minimum, whose v is then re-rounded
+// as fl(c_kj - u_k) so the augmenting step sees its reduced cost as exactly 0 -- and only the
+// rows left free are augmented (REDA's step-to-step Q: 0.71x the cold start's steps at eps = 0,
+// 0.80x at eps = 0.05 in the host model).  The result is the same: whatever duals the search
+// starts from, the assignment is used only under the certificate below, else the
+// scipy-exact solver runs.  Non-finite warm duals start from v = 0 (a row reduction).  `vout`
+// (optional) receives the final column duals, shifted so their minimum is 0.
 constexpr int kLsaUncertified = 1;
 
 __device__ __forceinline__ double lane_dbl(double x, int src) {
@@ -592,21 +603,63 @@ __device__ __forceinline__ double lane_dbl(double x, int src) {
                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src));
 }
 
-template <class Acc, bool kCount = false>
-__device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *steps, uint64_t *slot) {
+template <class Acc, bool kCount = false, bool kWarm = false>
+__device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *steps, uint64_t *slot, double vwarm = 0.0,
+                              double *vout = nullptr) {
     int nsteps = 0;
     const int lane = threadIdx.x & (kWave - 1);
     const bool live = lane < n;
     const uint64_t colmask = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
     const float kOutF = __builtin_bit_cast(float, 0x7fc00000u);
+    int r4c = -1, c4r = -1;
+    double v = 0.0, u = 0.0;
+    float amax = 0.0f;
+    if constexpr (kWarm) {
+        // warm row reduction against the given column duals (see above); non-finite duals (the
+        // first call) start from v = 0: a row reduction alone
+        const bool ok = __ballot(live && !(__builtin_fabs(vwarm) < __builtin_inf())) == 0;
+        v = (live && ok) ? vwarm : 0.0;
+        uint64_t taken = 0;
+#pragma unroll 1
+        for (int k = 0; k < 64; ++k) {
+            if (k < n) {
+                const float x = acc.col(k);  // a rolled loop: the row through the indexed read
+                amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+                const double d = live ? (double)x - v : __builtin_inf();
+                const float key = (float)d;
+                const float kmin = wave_min_f32_nonan(live ? key : __builtin_inff());
+                const uint64_t cm = __ballot(key == kmin);
+                if (cm == 0) {  // every entry NaN: the exact solver reports it
+                    if (kCount) *steps = nsteps;
+                    return kLsaUncertified;
+                }
+                double dk = lane_dbl(d, sff1(cm));
+                if ((__ballot(d != dk) & cm) != 0) {  // distinct doubles behind one float key
+                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(((cm >> lane) & 1ull) ? d : __builtin_inf()));
+                    dk = dbl_of(__builtin_amdgcn_readfirstlane((uint32_t)lb),
+                                __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32)));
+                }
+                u = lane == k ? dk : u;
+                const uint64_t tm = __ballot(live && d == dk) & ~taken;
+                if (tm != 0) {
+                    const int j = sff1(tm);
+                    taken |= 1ull << j;
+                    if (lane == j) {
+                        r4c = k;
+                        v = (double)x - dk;  // the augmenting step's ((0 + c) - u) - v is then exactly 0
+                    }
+                    c4r = lane == k ? j : c4r;
+                }
+            }
+        }
+    } else {
     // row reduction (u_k = min_j c_kj, float32: exact) then column reduction of the rest
     // (v_j = min_k (c_kj - u_k) in float64: each difference rounded once, relative 2^-53, far
     // inside the certificate's S 2^-40 slack -- not exact when the operands' exponents differ by
     // more than ~29 bits; dual feasibility is re-checked by the certificate): both the agents' and the
     // tasks' common offsets come out, so the column minima spread over more rows than a column
     // reduction alone leaves them (SAP Q: -16..28 % augmenting-path steps in the host model)
-    float amax = 0.0f;
-    double vmin = __builtin_inf(), u = 0.0;
+    double vmin = __builtin_inf();
     int imin = 0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
@@ -629,9 +682,10 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
     if (live) atomicMin(&slot32[imin], (uint32_t)lane);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t won = slot32[imin], mine = slot32[lane];
-    int r4c = (live && won == (uint32_t)lane) ? imin : -1;
-    int c4r = (live && mine != 0xffffffffu) ? (int)mine : -1;
-    double v = live ? vmin : 0.0;
+    r4c = (live && won == (uint32_t)lane) ? imin : -1;
+    c4r = (live && mine != 0xffffffffu) ? (int)mine : -1;
+    v = live ? vmin : 0.0;
+    }
     int path = -1;
     uint64_t freerows = __ballot(live && c4r < 0);
     int ncand = 1;
@@ -714,6 +768,11 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
         }
     }
     if (kCount) *steps = nsteps;
+    if (kWarm && vout) {
+        // the next call's warm start, shifted to a zero minimum (bounded S across calls)
+        const double vm = wave_min_f64(live ? v : __builtin_inf());
+        *vout = v - vm;
+    }
 #ifdef ASG_LSA_FAST_NOCERT  // timing experiments only: what the certificate costs (wrong on ties)
     col4row[0] = c4r;
     return ASG_OK;

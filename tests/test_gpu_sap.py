@@ -219,3 +219,61 @@ def test_sap_fast_path_planted_near_tie(gap_log2, expect):
         assert (exact > 0).all(), (exact == 0).sum()
     elif expect == "certified":
         assert (exact == 0).all(), (exact > 0).sum()
+
+
+def _sap_warm(q, eps, seed, counter, duals, warm):
+    """asg_sap_select_warm through the C-ABI: (int64 actions, status, steps)"""
+    import ctypes
+    from marl_sap_amd import _lib
+    B, n, m = q.shape
+    out = torch.empty((B, n), dtype=torch.int64, device=DEV)
+    st = torch.zeros((B,), dtype=torch.int32, device=DEV)
+    steps = torch.zeros((B,), dtype=torch.int32, device=DEV)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(_lib.lib().asg_sap_select_warm(p(q), _lib.i64arr(q.stride()), B, n, m, float(eps), seed, counter, 0,
+                                              p(out), p(st), p(steps), p(duals), int(warm), _lib.stream_ptr(DEV)))
+    torch.cuda.synchronize()
+    return out, st, steps
+
+
+@pytest.mark.parametrize("eps,n", [(0.0, 64), (0.05, 64), (0.3, 64), (0.05, 33)])
+def test_sap_warm_start_episodes_are_scipy(eps, n):
+    """Whole warm-started episodes: T = 20 consecutive selections per env on slowly drifting
+    SAP-like Q (each step starting from the env's previous column duals) equal scipy's LSA of
+    exactly the noisy matrix the kernel formed, step by step; and the warm start takes fewer
+    augmenting-path steps than the cold one on the same calls."""
+    rng = np.random.RandomState(int(eps * 100) + n)
+    B, T = 512, 20
+    base = sap_like_q(rng, B, n, n)
+    duals = torch.empty((B, 64), dtype=torch.float64, device=DEV)
+    warm_steps = cold_steps = 0
+    for t in range(T):
+        q = (base + 0.02 * t * rng.normal(size=(B, 1, n)) + 0.01 * rng.normal(size=(B, n, n))).astype(np.float32)
+        qd = torch.as_tensor(q, device=DEV)
+        out, st, steps = _sap_warm(qd, eps, 4, t + 1, duals, warm=t > 0)
+        ref_out, _, ref_steps = _sap_raw(qd, eps, 4, t + 1)
+        noisy = _noisy(qd, eps, 4, t + 1).cpu().numpy()
+        out, st = out.cpu().numpy(), st.cpu().numpy()
+        assert (st == 0).all()
+        np.testing.assert_array_equal(out, ref_out.cpu().numpy().astype(np.int64))
+        for b in range(0, B, 7):
+            assert np.array_equal(out[b], ora.lsa(noisy[b].astype(np.float64), maximize=True)[1]), (t, b)
+        if t > 0:
+            warm_steps += int((steps & 0xFFFF).sum().item()) + int((steps >> 16).sum().item())
+            cold_steps += int((ref_steps & 0xFFFF).sum().item()) + int((ref_steps >> 16).sum().item())
+        assert torch.isfinite(duals[:, :n]).all() or eps > 0.2  # the next call's warm start
+    assert warm_steps < cold_steps, (warm_steps, cold_steps)
+
+
+def test_sap_warm_start_ignores_garbage_duals():
+    """Any duals -- NaN (cold start), huge, or another problem's -- give scipy's assignment."""
+    rng = np.random.RandomState(5)
+    B, n = 256, 64
+    qd = torch.as_tensor(sap_like_q(rng, B, n, n), device=DEV)
+    ref = _sap_raw(qd, 0.05, 9, 2)[0].cpu().numpy().astype(np.int64)
+    for fill in (float("nan"), 1e30, -3.0):
+        duals = torch.full((B, 64), fill, dtype=torch.float64, device=DEV)
+        duals[::2] = torch.as_tensor(rng.normal(size=(B // 2, 64)) * 5, device=DEV)
+        out, st, _ = _sap_warm(qd, 0.05, 9, 2, duals, warm=1)
+        assert (st.cpu().numpy() == 0).all()
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
