@@ -630,8 +630,13 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
         return fail(h, ASG_E_INVALID_ARG, "asg_step_forward: q_out must be 16-B aligned");
     const asg::EnvState &st = h->st;
     if (!h->has_reset && !reset) return fail(h, ASG_E_STATE, "step called before reset");
-    if (reset && (st.rng_mode != ASG_RNG_PHILOX || st.benefit_mode == ASG_BENEFIT_INJECTED))
-        return fail(h, ASG_E_INVALID_ARG, "asg_reset_rollout: Philox bump/dense benefits only");
+    // the reset inside the launch: Philox bump / dense benefits (the permutation drawn in the
+    // kernel), or the MT19937 mode (its draws and table by the reset's draw kernels first, the
+    // reset row by the episode launch); not an injected table under Philox
+    if (reset && st.rng_mode == ASG_RNG_PHILOX && st.benefit_mode == ASG_BENEFIT_INJECTED)
+        return fail(h, ASG_E_INVALID_ARG, "asg_reset_rollout: not with an injected table in the Philox mode (asg_reset)");
+    if (reset && st.benefit_mode == ASG_BENEFIT_INJECTED && !h->table_ready)
+        return fail(h, ASG_E_STATE, "benefit_mode=injected needs asg_set_benefits before reset");
     const int k0 = reset ? 0 : h->k;
     if (steps < 1 || k0 + steps > st.T)
         return fail(h, ASG_E_STATE, "asg_rollout: steps must be >= 1 and stay within the episode (k + steps <= T)");
@@ -673,6 +678,10 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     // as asg_reset: a fresh Philox key per episode, committed once the launch succeeded
     asg::EnvState lst = h->st;
     if (reset && h->has_reset) lst.episode += 1;
+    if (reset && st.rng_mode == ASG_RNG_MT19937) {
+        hipError_t e0 = asg::launch_reset_draws(lst, !h->constructed, s);
+        if (e0 != hipSuccess) return hip_fail(h, e0, "asg_reset_rollout (MT19937 draws)");
+    }
     hipError_t e = asg::launch_rollout(sl, lst, ts, k0, steps, select_first, select_last, reset,
                                        static_cast<const float4 *>(packed), b1, b_r0, b_r1, b2, use_rnn, h_in, h_stride,
                                        h_out, q_out, (float)epsilon, seed, (uint32_t)counter, st.env_base * n, status, s);

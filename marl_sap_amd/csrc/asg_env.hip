@@ -936,6 +936,20 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
     return launch_reset_src(bump_src(st), bv, st, ts, true, s);
 }
 
+// The MT19937 mode's reset without its row write: the draws (and the float32 table) only --
+// the episode launch that follows writes the reset row (asg_reset_rollout in the same-seed mode)
+hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s) {
+    if (st.rng_mode != ASG_RNG_MT19937) return hipErrorInvalidValue;
+    const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m;
+    const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
+    hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen, gen);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess || !gen) return err;
+    const int R = mt_table_rows(st.m);
+    hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), mt_table_lds(R, st.m), s, st.mtpar, st, R);
+    return hipGetLastError();
+}
+
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
     if (st.mtpar) return launch_step_src(par_src(st), bv, st, ts, k, s);
     if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s);

@@ -1089,6 +1089,10 @@ __device__ __forceinline__ void wave_lds_fence() {
 #ifndef ASG_ROLLOUT_SQ64
 #define ASG_ROLLOUT_SQ64 1
 #endif
+// 1: the table modes (same-seed / injected) take the SQ64 instances too
+#ifndef ASG_ROLLOUT_SQ64_TAB
+#define ASG_ROLLOUT_SQ64_TAB 1
+#endif
 // 1: the SQ = 64 instances also fix L = 3 (launched only when L == 3): the unrolled lookahead
 // loop spills 28 VGPRs instead of 14 and ran 0.709-0.713 vs 0.570-0.574 ms/step (r5 A/B) -- off
 #ifndef ASG_SQ64_L3
@@ -1255,6 +1259,11 @@ struct HNext {
 #ifndef ASG_L2FIRST_LATE
 #define ASG_L2FIRST_LATE 1
 #endif
+// 1: the table modes load each chunk's first kTabPre lookahead blocks at the chunk start
+#ifndef ASG_TAB_PRELOAD
+#define ASG_TAB_PRELOAD 1
+#endif
+constexpr int kTabPre = 3;
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
@@ -1402,6 +1411,33 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
         for (int u = 0; u < Ub; ++u) {
             // bump parameters of the lane's 16 (row, task) pairs of this chunk (Philox mode)
             Bump32 bp[2][4][NT];
+            // table modes: the chunk's lookahead values of the first kTabPre blocks, loaded at
+            // once at the chunk start (in place of the Philox parameters): one wait behind the
+            // tile's stores per chunk instead of one per block (gfx9's in-order vmcnt)
+            float4 tv[kTabPre][2][NT];
+            if constexpr (TAB && ASG_TAB_PRELOAD) {
+#pragma unroll
+                for (int l = 1; l <= kTabPre; ++l) {
+                    const int t = kk + l - 1;
+                    if (l > L || t >= T) continue;
+                    const float *trow = ra.table32 + ((int64_t)e * T + t) * n * m;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            const int j0 = 32 * u + 16 * c + 4 * q;
+                            const float *tp = trow + (int64_t)ia[nt] * m + j0;
+                            if (!GEN) {
+                                tv[l - 1][c][nt] = *reinterpret_cast<const float4 *>(tp);
+                            } else {
+                                float v4[4];
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) v4[v] = (ok[nt] && j0 + v < m) ? tp[v] : 0.f;
+                                tv[l - 1][c][nt] = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                            }
+                        }
+                }
+            }
             if constexpr (!TAB) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
@@ -1447,7 +1483,18 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
                 // past T are zeros)
                 float4 xv[2][NT];
-                if (TAB && t < T) {
+                if (TAB && ASG_TAB_PRELOAD && t < T && l <= kTabPre) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) {
+                            // l is a loop variable: the preloaded block by a uniform select
+                            float4 x = tv[0][c][nt];
+#pragma unroll
+                            for (int ll = 2; ll <= kTabPre; ++ll) x = l == ll ? tv[ll - 1][c][nt] : x;
+                            xv[c][nt] = x;
+                        }
+                } else if (TAB && t < T) {
                     // the table's benefits rounded to float32 (the batch's dtype, as the separate
                     // step's rows), from its float32 copy: B[e][t][row][j0 .. j0 + 3], one 16-byte
                     // load (the float64 table would take two behind the tile's stores)
@@ -1660,9 +1707,15 @@ rollout_kernel(RolloutArgs ra) {
             if (lane == 0 && ra.filled) ra.filled[(int64_t)ra.ts0 * ra.E + e] = 1;
         } else {
             for (int i = lane; i < np; i += 64) {
-                s_prev[i] = (uint16_t)(i < n ? ra.prev[e * n + i] : 0);
+                const int p = i < n ? ra.prev[e * n + i] : 0;
+                s_prev[i] = (uint16_t)p;
                 s_act[i] = 0;
+                // table modes' reset in this launch: the permutation the reset's draw kernel
+                // left in prev; the reset row's prev_assigns / filled here, its obs by the tiles
+                if (TAB && ra.reset && i < n && ra.prevb)
+                    ra.prevb[((int64_t)ra.ts0 * ra.E + e) * n + i] = (ra.quirks & ASG_QUIRK_PREV_ASSIGNS_ZERO) ? 0 : p;
             }
+            if (TAB && ra.reset && lane == 0 && ra.filled) ra.filled[(int64_t)ra.ts0 * ra.E + e] = 1;
         }
         if (lane == 0) *s_ret = ra.reset ? 0.0 : ra.returns[e];
         if (!ra.select_first) rollout_actions_from_batch(ra, e, ra.ts0, s_act);
@@ -1820,7 +1873,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.table = tab ? st.table : nullptr;
     ra.par = tab ? st.mtpar : nullptr;
     ra.table32 = tab ? st.table32 : nullptr;
-    if (tab && reset) return hipErrorInvalidValue;  // the table modes' reset is asg_reset (MT19937 stream)
+    // the table modes' reset in this launch: the MT19937 draws ran before it (asg_reset_rollout)
     // Q output: one transition and the forward of the row after it (asg_step_forward)
     if (Q && (steps != 1 || select_first || !select_last || reset)) return hipErrorInvalidValue;
     ra.Q = Q;
@@ -1852,7 +1905,8 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     lc.rnn = rnn;
     lc.w2l = plan.w2l;
     lc.gen = st.m % 32 != 0 || st.n % 32 != 0;
-    lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64 && (!ASG_SQ64_L3 || st.L == 3);
+    lc.sq64 = st.n == 64 && st.m == 64 && plan.w2l && ASG_ROLLOUT_SQ64 && (!ASG_SQ64_L3 || st.L == 3) &&
+              (!tab || ASG_ROLLOUT_SQ64_TAB);
     // the L2 fc1 slice read first, before the tile's stores (rollout_tile's l2first)
     if (lc.sq64 && ASG_ROLLOUT_L2FIRST && plan.l2_slices >= 1) ra.w1_off = 1;
     if (Q) return launch_rollout_q(ra, lc, s);

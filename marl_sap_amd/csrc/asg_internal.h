@@ -53,6 +53,7 @@ struct SelectArgs {
 };
 
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s);
+hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s);
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_rollout(const asg_batch_view &bv, const EnvState &st, int ts, int k0, int steps, bool reset,

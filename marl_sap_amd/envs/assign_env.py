@@ -159,9 +159,10 @@ class AssignEnvBatch(MultiAgentEnv):
 
     @property
     def fused_reset_ok(self):
-        """asg_reset_rollout (the reset inside the episode's launch) takes the Philox modes; the
-        table modes reset with asg_reset (the MT19937 stream / the injected table)."""
-        return self.rng == "philox" and self.benefits in ("bump", "dense")
+        """asg_reset_rollout (the reset inside the episode's launch) takes the Philox bump / dense
+        modes and the MT19937 mode (its draw kernels, then the launch writes the reset row); an
+        injected table under Philox resets with asg_reset."""
+        return (self.rng == "philox" and self.benefits in ("bump", "dense")) or self.rng == "mt19937"
 
     def step_select(self, batch, ts, agent, hidden_state, epsilon, seed, counter, status):
         """asg_step at row ts and the fused agent forward + epsilon-greedy for row ts + 1 in
