@@ -641,17 +641,30 @@ __device__ __forceinline__ void mt_temper(const uint32_t *k, uint32_t *o) {
     }
     wave_sync();
 }
+// ASG_MT_TEMPER_ON_READ: the tempered copies are not kept -- a word is tempered when read (4
+// shift / mask steps) -- so a draw wave holds only the two raw blocks, 5 KiB of LDS instead of
+// 10: twice the waves per CU hide each other's dependent LDS reads (the draws are latency-bound)
+#ifndef ASG_MT_TEMPER_ON_READ
+#define ASG_MT_TEMPER_ON_READ 1
+#endif
+__device__ __forceinline__ uint32_t mt_temper1(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
 struct MtWave2 {
     uint32_t *key, *key2;  // [624] raw states of the current and the next block (LDS)
-    uint32_t *out;         // [1248] tempered words of both
+    uint32_t *out;         // [1248] tempered words of both (unused with ASG_MT_TEMPER_ON_READ)
     int pos;               // wave-uniform, < 624 between calls
     __device__ void init(int pos0) {
         const int lane = threadIdx.x & (kWave - 1);
-        mt_temper(key, out);
+        if (!ASG_MT_TEMPER_ON_READ) mt_temper(key, out);
         for (int i = lane; i < kMtN; i += kWave) key2[i] = key[i];
         wave_sync();
         mt_twist_inplace(key2);
-        mt_temper(key2, out + kMtN);
+        if (!ASG_MT_TEMPER_ON_READ) mt_temper(key2, out + kMtN);
         pos = pos0;
         if (pos >= kMtN) shift();
     }
@@ -659,14 +672,20 @@ struct MtWave2 {
         const int lane = threadIdx.x & (kWave - 1);
         for (int i = lane; i < kMtN; i += kWave) {
             key[i] = key2[i];
-            out[i] = out[kMtN + i];
+            if (!ASG_MT_TEMPER_ON_READ) out[i] = out[kMtN + i];
         }
         wave_sync();
         mt_twist_inplace(key2);
-        mt_temper(key2, out + kMtN);
+        if (!ASG_MT_TEMPER_ON_READ) mt_temper(key2, out + kMtN);
         pos -= kMtN;
     }
-    __device__ uint32_t word(int k) const { return out[pos + k]; }  // k < 624, uniform
+    __device__ uint32_t word(int k) const {  // k < 624 (per lane: the speculative reads)
+        if (ASG_MT_TEMPER_ON_READ) {
+            const int i = pos + k;
+            return mt_temper1(i < kMtN ? key[i] : key2[i - kMtN]);
+        }
+        return out[pos + k];
+    }
     __device__ void advance(int c) {
         pos += c;
         if (pos >= kMtN) shift();
@@ -705,7 +724,7 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
                                                        bool generate) {
     extern __shared__ uint32_t s_mt[];
     uint32_t *key = s_mt, *key2 = s_mt + kMtN, *out = s_mt + 2 * kMtN;
-    int *perm = reinterpret_cast<int *>(out + 2 * kMtN);
+    int *perm = reinterpret_cast<int *>(out + (ASG_MT_TEMPER_ON_READ ? 0 : 2 * kMtN));
     const int64_t e = blockIdx.x;
     const int lane = threadIdx.x;
     const int n = st.n, m = st.m, T = st.T;
@@ -914,9 +933,10 @@ static bool uses_table(const EnvState &st) {
 
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s) {
     if (st.rng_mode == ASG_RNG_MT19937) {
-        // 10,240 B at m = 64: exactly 16 workgroups in a CU's 160 KiB (the LDS is allocated in
-        // 512-byte granules: 16 bytes more would round up to 10,752 B and 15 workgroups)
-        const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m;
+        // the two raw MT19937 blocks + the permutation: 5,248 B at m = 64 (29 workgroups in a
+        // CU's 160 KiB, LDS in 512-byte granules); with the tempered copies kept
+        // (ASG_MT_TEMPER_ON_READ=0) 10,240 B, exactly 16 workgroups
+        const size_t lds = sizeof(uint32_t) * (ASG_MT_TEMPER_ON_READ ? 2 : 4) * kMtN + sizeof(int) * st.m;
         const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
         // with an injected table (sat_prox_mat=) neither __init__ nor reset draw a
         // table: only the permutation consumes the stream (mock :32-37, :99-105)
@@ -940,7 +960,7 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
 // the episode launch that follows writes the reset row (asg_reset_rollout in the same-seed mode)
 hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s) {
     if (st.rng_mode != ASG_RNG_MT19937) return hipErrorInvalidValue;
-    const size_t lds = sizeof(uint32_t) * 4 * kMtN + sizeof(int) * st.m;
+    const size_t lds = sizeof(uint32_t) * (ASG_MT_TEMPER_ON_READ ? 2 : 4) * kMtN + sizeof(int) * st.m;
     const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
     hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen, gen);
     hipError_t err = hipGetLastError();
