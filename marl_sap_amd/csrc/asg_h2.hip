@@ -1259,6 +1259,9 @@ struct HNext {
 #ifndef ASG_L2FIRST_LATE
 #define ASG_L2FIRST_LATE 1
 #endif
+#ifndef ASG_ROLLOUT_STAGGER
+#define ASG_ROLLOUT_STAGGER 0
+#endif
 // 1: the table modes load each chunk's first kTabPre lookahead blocks at the chunk start
 #ifndef ASG_TAB_PRELOAD
 #define ASG_TAB_PRELOAD 1
@@ -1662,6 +1665,12 @@ rollout_kernel(RolloutArgs ra) {
     uint16_t *s_prev = s_act + np;
     const int ntile = np / (16 * kH2NT);
     const int64_t GW = (int64_t)gridDim.x * kH2Waves;
+#if ASG_ROLLOUT_STAGGER > 0
+    // A/B: the second wave of each SIMD (waves 4-7) starts ASG_ROLLOUT_STAGGER x ~8K cycles late,
+    // so the two waves' store-heavy and compute-heavy phases do not start in step
+    if (wv >= 4)
+        for (int i = 0; i < ASG_ROLLOUT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
     for (int64_t e0 = (int64_t)blockIdx.x * kH2Waves + wv; e0 < ra.E; e0 += GW) {
         // addresses are recomputed from e each env: strength-reduced per-lane pointers carried
         // across the env loop were spilled around the tile loop, and their reloads waited for

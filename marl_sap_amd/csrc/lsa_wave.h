@@ -593,7 +593,7 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 // rows left free are augmented (REDA's step-to-step Q: 0.71x the cold start's steps at eps = 0,
 // 0.80x at eps = 0.05 in the host model).  The result is the same: whatever duals the search
 // starts from, the assignment is used only under the certificate below, else the
-// scipy-exact solver runs.  Non-finite warm duals start from v = 0 (a row reduction).  `vout`
+// scipy-exact solver runs.  Non-finite warm duals start from the cold reduction's column duals.  `vout`
 // (optional) receives the final column duals, shifted so their minimum is 0.
 constexpr int kLsaUncertified = 1;
 
@@ -619,6 +619,22 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
         // first call) start from v = 0: a row reduction alone
         const bool ok = __ballot(live && !(__builtin_fabs(vwarm) < __builtin_inf())) == 0;
         v = (live && ok) ? vwarm : 0.0;
+        if (!ok) {
+            // no usable duals (the first call): the cold start's column duals -- v_j = min_k
+            // (c_kj - min_l c_kl) -- as the warm start (v = 0, a row reduction alone, took 4x
+            // the cold start's steps)
+            double vmin = __builtin_inf();
+#pragma unroll 1
+            for (int k = 0; k < 64; ++k) {
+                if (k < n) {
+                    const float x = acc.col(k);
+                    const float uk = wave_min_f32_nonan(live ? x : __builtin_inff());
+                    const double r = (double)x - (double)uk;
+                    vmin = r < vmin ? r : vmin;
+                }
+            }
+            v = live ? vmin : 0.0;
+        }
         uint64_t taken = 0;
 #pragma unroll 1
         for (int k = 0; k < 64; ++k) {
