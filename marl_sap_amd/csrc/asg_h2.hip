@@ -1250,17 +1250,11 @@ struct HNext {
 };
 
 // 1: with W2 in LDS and an fc1 slice in L2 (64 x 64: 1 of 6; the SQ64 instances), that slice is
-// the tile's first, consumed before its stores (0: the last one, read behind them -- round 4)
+// the tile's first (0: the last one, its weights read behind nearly all the tile's stores --
+// round 4): 0.556-0.559 vs 0.575 ms/step (runtime-shape instances) on one box (r5 A/B); its rows
+// stored after its MFMAs as well spilled 43 VGPRs and ran 0.65 ms)
 #ifndef ASG_ROLLOUT_L2FIRST
 #define ASG_ROLLOUT_L2FIRST 1
-#endif
-// 1: under l2first the first block's rows are stored after its MFMAs (the L2 weights then wait
-// for the prefix rows only)
-#ifndef ASG_L2FIRST_LATE
-#define ASG_L2FIRST_LATE 1
-#endif
-#ifndef ASG_ROLLOUT_STAGGER
-#define ASG_ROLLOUT_STAGGER 0
 #endif
 // 1: the table modes load each chunk's first kTabPre lookahead blocks at the chunk start
 #ifndef ASG_TAB_PRELOAD
@@ -1337,12 +1331,10 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(hN[t][nt]));
     }
-    // w1_off (the SQ64 instances): the first main slice's weights live in L2; they are loaded
-    // in the tile's first lookahead block and consumed by its MFMAs before any store of the
-    // tile is issued (the prefix rows are deferred behind them), so the wait for them covers no
-    // store of this tile -- loaded last (round 4), they waited for nearly all of them
-    const bool l2first = AGENT && SQ == 64 && ra.w1_off;
-    auto prefix_stores = [&]() {
+    // w1_off (the SQ64 instances): the L2-resident fc1 slice is the tile's FIRST main slice, so
+    // the wait for its weights covers only the prefix rows and the first block's rows of the
+    // tile -- as the last slice (round 4) it waited for nearly all of the tile's stores
+    if (stores && !(ASG_ROLLOUT_XSKIP & 1)) {
         // obs block 0 = onehot(a) (row kk), actions_onehot (row kk - 1), avail = 1 (row kk)
         // actions_onehot of the transition before the row (none before the reset row)
         int64_t *oh_r = (ra.onehot && have_act) ? ra.onehot + ((int64_t)(tss - 1) * ra.E * n + sro) * m : nullptr;
@@ -1380,8 +1372,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 for (int off = off0; off < nrow * m; off += 64) ab[off] = 1;
             }
         }
-    };
-    if (stores && !(ASG_ROLLOUT_XSKIP & 1)) prefix_stores();
+    }
     // ---- the lookahead blocks 1..L (times kk .. kk + L - 1), fc1 on them -------------------
     BumpShape bsh = bump_shape(T, ra.wmin, ra.wmax);
     bsh.q = __builtin_amdgcn_readfirstlane(bsh.q);  // uniform: keep the grid exponent scalar
@@ -1480,9 +1471,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
             }
             for (int l = 1; l <= L; ++l) {
                 const int t = kk + l - 1;
-                // the tile's first slice under l2first: the L2 one, read (mma(false)) before any
-                // store of this tile; its rows and the deferred prefix rows follow its MFMAs
-                const bool first = l2first && u == 0 && l == 1 && attempt == 0;
+
                 // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
                 // past T are zeros)
                 float4 xv[2][NT];
@@ -1553,7 +1542,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 // an L2 weight slice (no W2 in LDS: the large shapes, 19 of 24 slices at 256 x 256):
                 // its weights are loaded before this block's row stores and the stores follow the
                 // MFMAs, so the loads wait for the previous block's stores only
-                const bool late = (ASG_ROLLOUT_LATE && !W2L && AGENT && l * Ub + u >= s_l2) || (ASG_L2FIRST_LATE && first);
+                const bool late = ASG_ROLLOUT_LATE && !W2L && AGENT && l * Ub + u >= s_l2;
                 if (st_now && !late) store_rows();
                 if (AGENT) {
                     // the agent kernel's slice: abs-max, split, 4 output tiles x NT rows of MFMAs
@@ -1665,12 +1654,6 @@ rollout_kernel(RolloutArgs ra) {
     uint16_t *s_prev = s_act + np;
     const int ntile = np / (16 * kH2NT);
     const int64_t GW = (int64_t)gridDim.x * kH2Waves;
-#if ASG_ROLLOUT_STAGGER > 0
-    // A/B: the second wave of each SIMD (waves 4-7) starts ASG_ROLLOUT_STAGGER x ~8K cycles late,
-    // so the two waves' store-heavy and compute-heavy phases do not start in step
-    if (wv >= 4)
-        for (int i = 0; i < ASG_ROLLOUT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
     for (int64_t e0 = (int64_t)blockIdx.x * kH2Waves + wv; e0 < ra.E; e0 += GW) {
         // addresses are recomputed from e each env: strength-reduced per-lane pointers carried
         // across the env loop were spilled around the tile loop, and their reloads waited for
