@@ -36,6 +36,10 @@ for v in "q:--selector sap --use-rnn 0:2"; do
   prof write_$tag 400 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$tag" -o run -- python3 $B $args --config $cfg $E1
   prof sq1_$tag 400 --pmc $SQ1 --output-format csv -d "$OUT/sq1_$tag" -o run -- python3 $B $args --config $cfg $E1
 done
+# BASELINE configs[1]: the random policy's episode kernel (asg_random_rollout)
+prof kt_c1 300 --kernel-trace --stats --output-format csv -d "$OUT/kt_c1" -o run -- python3 $B --config 1
+prof fetch_c1 300 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_c1" -o run -- python3 $B --config 1 $E1
+prof write_c1 300 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_c1" -o run -- python3 $B --config 1 $E1
 prof kt_sap 400 --kernel-trace --stats --output-format csv -d "$OUT/kt_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5
 timeout -k 10 300 python bench.py --selector sap --cpu-baseline 0 --secondary 0 --steps 20 --warmup 5 > "$OUT/bench_sap.log" 2>&1 || exit 1
 prof sq_sap 400 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq_sap" -o run -- python3 $B --selector sap --steps 20 --warmup 5

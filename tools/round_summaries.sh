@@ -20,3 +20,8 @@ if [ -d $R/fetch_q ]; then
 fi
 cp $R/kt_sap/run_kernel_stats.csv $P/${RN}_kernel_stats_sap_$T.csv
 python tools/pmc_sap_summary.py $R/sq_sap $R/bench_sap.log $P/${RN}_pmc_sap_kernel_$T.json
+if [ -d $R/fetch_c1 ]; then
+  python tools/pmc_summary.py $R/fetch_c1 $R/write_c1 $P/${RN}_pmc_random_rollout_$T.json --kernel random_rollout_kernel \
+      --n 16 --m 16 --L 3 --E 4096 --steps-per-launch 20 --use-rnn 0 --fetch-doubled
+  cp $R/kt_c1/run_kernel_stats.csv $P/${RN}_kernel_stats_c1_$T.csv
+fi
