@@ -356,6 +356,8 @@ def parse(argv=None):
                         "(asg_rollout); 3: one asg_rollout launch per step (env step t + selection t + 1); 0: separate "
                         "asg_step + agent select launches; 2: as 1")
     p.add_argument("--use-rnn", type=int, default=1, help="0: the Linear + ReLU RNNAgent (use_rnn: False)")
+    p.add_argument("--sap-warm", type=int, default=1,
+                   help="1 (default): the SAP selector's fast path warm-started from the previous step's duals")
     p.add_argument("--fuse-reset", type=int, default=1,
                    help="1 (default, the runner's): on the episode schedule the env reset runs in the episode's "
                         "first launch (asg_reset_rollout); 0: asg_reset as its own launch")
@@ -381,7 +383,8 @@ def make_args(a, E, selector=None, agent=None, fused=None, mac="basic_mac", use_
         obs_last_action=False, obs_agent_id=False, agent_output_type="q", action_selector=sel,
         agent=agent or a.agent, seed=a.seed,
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac=mac,
-        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always", 3: "step"}[fused])
+        reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always", 3: "step"}[fused],
+        sap_warm_start=bool(a.sap_warm))
     for k, v in extra.items():
         setattr(args, k, v)
     return args
@@ -603,14 +606,24 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
            "fused_resets": state.get("fused_resets", 0),
            "gather_ms": mean(gather_pairs) if gather_pairs else None, "gathers": len(gather_pairs)}
     if count_lsa and selector == "sap" and a.n <= a.m <= 64:
-        # one more selection on the current state, with the step-counting kernel instance
-        sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
-        t = state["t"] if state["t"] < a.T else 0
+        # one more selection with the step-counting kernel instance.  On the step_q schedule it
+        # is a genuine next step (env step t + agent forward + the selection of row t + 1, warm-
+        # started from row t's duals, as in the timed window); else a selection on the current row
         with torch.no_grad():
-            if state["t"] >= a.T:
-                runner.reset()
-                mac.init_hidden(E)
-            mac.select_actions(runner.batch, t_ep=t, t_env=runner.t_env)
+            if state.get("mode") == "step_q":
+                if state["t"] + 1 >= a.T:
+                    new_episode()
+                if not state["selected"]:
+                    runner.select_into_batch(state["t"])
+                sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
+                mac.fused_step_select(env, runner.batch, state["t"], runner.t_env)
+            else:
+                sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
+                t = state["t"] if state["t"] < a.T else 0
+                if state["t"] >= a.T:
+                    runner.reset()
+                    mac.init_hidden(E)
+                mac.select_actions(runner.batch, t_ep=t, t_env=runner.t_env)
         # fast-path steps in the low 16 bits, scipy-exact steps (uncertified or rectangular
         # problems) above (asg_sap_select)
         cs = sel_obj.count_steps.long()
@@ -812,7 +825,8 @@ def main():
             for name, sel_, yaml in (("iql", "eps", "mock_constellation_iql.yaml"),
                                      ("reda", "sap", "mock_constellation_reda.yaml")):
                 eps_over = dict(epsilon_start=1.0, epsilon_finish=0.0, epsilon_anneal_time=20000)
-                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn", **js, **eps_over)
+                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn", count_lsa=sel_ == "sap", **js,
+                             **eps_over)
                 extra[name] = {
                     **leg_base(rj, sk, a.T),
                     "what": f"{yaml}: jumpstart_mac (haa_selector jumpstart) + "
@@ -824,6 +838,8 @@ def main():
                         "fused_rollout_per_step": round(rj["fused_ms"], 4) if rj["fused_ms"] else None,
                         "env_step": round(rj["kern_ms"], 4) if rj["kern_ms"] else None,
                         "select": round(rj["sel_ms"], 4) if rj["sel_ms"] else None}}
+                if sel_ == "sap":
+                    extra[name]["roofline_lsa"] = lsa_roofline(a, E, rj)
                 if rj.get("mode") == "step_q" and rj.get("step_forward_ms"):
                     extra[name]["roofline"] = fused_roofline(a, E, rj["step_forward_ms"], use_rnn=False, q_out=True)
                 elif rj.get("fused_ms"):

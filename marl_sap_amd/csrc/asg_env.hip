@@ -641,11 +641,12 @@ __device__ __forceinline__ void mt_temper(const uint32_t *k, uint32_t *o) {
     }
     wave_sync();
 }
-// ASG_MT_TEMPER_ON_READ: the tempered copies are not kept -- a word is tempered when read (4
+// ASG_MT_TEMPER_ON_READ=1: the tempered copies are not kept -- a word is tempered when read (4
 // shift / mask steps) -- so a draw wave holds only the two raw blocks, 5 KiB of LDS instead of
-// 10: twice the waves per CU hide each other's dependent LDS reads (the draws are latency-bound)
+// 10 (29 draw waves per CU instead of 16).  Measured slower (r5 A/B, compat leg): 0.946-0.954 vs
+// 0.892-0.900 ms/step -- the speculative reads temper every word they test; off
 #ifndef ASG_MT_TEMPER_ON_READ
-#define ASG_MT_TEMPER_ON_READ 1
+#define ASG_MT_TEMPER_ON_READ 0
 #endif
 __device__ __forceinline__ uint32_t mt_temper1(uint32_t y) {
     y ^= (y >> 11);
