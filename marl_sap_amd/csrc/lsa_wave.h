@@ -586,15 +586,12 @@ __device__ int lsa_solve_reg64(const Acc &acc, int nr, int nc, int (&col4row)[1]
 // this wave.
 //
 // Warm start (kWarm, `vwarm` = this lane's column dual from an earlier call, e.g. the previous
-// step's selection of the same env): the column duals carry the task profile the SAP Q-values
-// share from step to step, so the row reduction runs against them -- u_k = min_j (c_kj - v_j),
-// each row taking the lowest untaken column at that exact minimum, whose v is then re-rounded
-// as fl(c_kj - u_k) so the augmenting step sees its reduced cost as exactly 0 -- and only the
-// rows left free are augmented (REDA's step-to-step Q: 0.71x the cold start's steps at eps = 0,
-// 0.80x at eps = 0.05 in the host model).  The result is the same: whatever duals the search
-// starts from, the assignment is used only under the certificate below, else the
-// scipy-exact solver runs.  Non-finite warm duals start from the cold reduction's column duals.  `vout`
-// (optional) receives the final column duals, shifted so their minimum is 0.
+// step's selection of the same env): the row duals start as u_k = min_j (c_kj - vwarm_j), and
+// the usual column reduction and claims follow (see the dual start below).  The result is the
+// same: whatever duals the search starts from, the assignment is used only under the
+// certificate below, else the scipy-exact solver runs.  Non-finite warm duals (the first call)
+// take the cold start.  `vout` (optional) receives the final column duals, shifted so their
+// minimum is 0.
 constexpr int kLsaUncertified = 1;
 
 __device__ __forceinline__ double lane_dbl(double x, int src) {
@@ -614,82 +611,71 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
     int r4c = -1, c4r = -1;
     double v = 0.0, u = 0.0;
     float amax = 0.0f;
+    // the dual start: u, then the column reduction v_j = min_k (c_kj - u_k) with each row keeping
+    // the lowest column whose minimum it holds.  Cold: u_k = min_j c_kj (float32: exact).  Warm
+    // (kWarm, finite vwarm on every live lane): u_k = min_j (c_kj - vwarm_j) in float64 -- the
+    // previous call's column duals carry over into the row duals, and the column reduction then
+    // fits v to this problem (REDA's own Q sequence: 0.50x the cold start's augmenting-path
+    // steps in the host model, 0.36x on the GRU agent's at eps 0.05; taking the previous v as the
+    // start itself, without the column reduction, took 1.04x / 0.72x)
+    double vmin = __builtin_inf();
+    int imin = 0;
+    bool warm = false;
+    if constexpr (kWarm) warm = __ballot(live && !(__builtin_fabs(vwarm) < __builtin_inf())) == 0;
     if constexpr (kWarm) {
-        // warm row reduction against the given column duals (see above); non-finite duals (the
-        // first call) start from v = 0: a row reduction alone
-        const bool ok = __ballot(live && !(__builtin_fabs(vwarm) < __builtin_inf())) == 0;
-        v = (live && ok) ? vwarm : 0.0;
-        if (!ok) {
-            // no usable duals (the first call): the cold start's column duals -- v_j = min_k
-            // (c_kj - min_l c_kl) -- as the warm start (v = 0, a row reduction alone, took 4x
-            // the cold start's steps)
-            double vmin = __builtin_inf();
-#pragma unroll 1
-            for (int k = 0; k < 64; ++k) {
-                if (k < n) {
-                    const float x = acc.col(k);
-                    const float uk = wave_min_f32_nonan(live ? x : __builtin_inff());
-                    const double r = (double)x - (double)uk;
-                    vmin = r < vmin ? r : vmin;
-                }
-            }
-            v = live ? vmin : 0.0;
-        }
-        uint64_t taken = 0;
+        // one rolled loop for both starts (the row through the indexed read): two unrolled copies
+        // had overflowed the SGPR file (~200 spilled)
+        const double vw = (live && warm) ? vwarm : 0.0;
 #pragma unroll 1
         for (int k = 0; k < 64; ++k) {
             if (k < n) {
-                const float x = acc.col(k);  // a rolled loop: the row through the indexed read
-                amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
-                const double d = live ? (double)x - v : __builtin_inf();
-                const float key = (float)d;
-                const float kmin = wave_min_f32_nonan(live ? key : __builtin_inff());
-                const uint64_t cm = __ballot(key == kmin);
-                if (cm == 0) {  // every entry NaN: the exact solver reports it
-                    if (kCount) *steps = nsteps;
-                    return kLsaUncertified;
-                }
-                double dk = lane_dbl(d, sff1(cm));
-                if ((__ballot(d != dk) & cm) != 0) {  // distinct doubles behind one float key
-                    const uint64_t lb = __builtin_bit_cast(uint64_t, wave_min_f64(((cm >> lane) & 1ull) ? d : __builtin_inf()));
-                    dk = dbl_of(__builtin_amdgcn_readfirstlane((uint32_t)lb),
-                                __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32)));
-                }
-                u = lane == k ? dk : u;
-                const uint64_t tm = __ballot(live && d == dk) & ~taken;
-                if (tm != 0) {
-                    const int j = sff1(tm);
-                    taken |= 1ull << j;
-                    if (lane == j) {
-                        r4c = k;
-                        v = (double)x - dk;  // the augmenting step's ((0 + c) - u) - v is then exactly 0
+                const float x = acc.col(k);
+                double uk;
+                if (warm) {
+                    const double d = live ? (double)x - vw : __builtin_inf();
+                    const float key = (float)d;
+                    const float kmin = wave_min_f32_nonan(live ? key : __builtin_inff());
+                    const uint64_t cm = __ballot(key == kmin);
+                    if (cm == 0) {  // every entry of the row NaN: the exact solver reports it
+                        if (kCount) *steps = nsteps;
+                        return kLsaUncertified;
                     }
-                    c4r = lane == k ? j : c4r;
+                    uk = lane_dbl(d, sff1(cm));
+                    if ((__ballot(d != uk) & cm) != 0) {  // distinct doubles behind one float key
+                        const uint64_t lb =
+                            __builtin_bit_cast(uint64_t, wave_min_f64(((cm >> lane) & 1ull) ? d : __builtin_inf()));
+                        uk = dbl_of(__builtin_amdgcn_readfirstlane((uint32_t)lb),
+                                    __builtin_amdgcn_readfirstlane((uint32_t)(lb >> 32)));
+                    }
+                } else {
+                    uk = (double)wave_min_f32_nonan(live ? x : __builtin_inff());
                 }
+                u = lane == k ? uk : u;
+                const double r = (double)x - uk;
+                const bool t = r < vmin;
+                vmin = t ? r : vmin;
+                imin = t ? k : imin;
+                amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
             }
         }
     } else {
-    // row reduction (u_k = min_j c_kj, float32: exact) then column reduction of the rest
-    // (v_j = min_k (c_kj - u_k) in float64: each difference rounded once, relative 2^-53, far
-    // inside the certificate's S 2^-40 slack -- not exact when the operands' exponents differ by
-    // more than ~29 bits; dual feasibility is re-checked by the certificate): both the agents' and the
-    // tasks' common offsets come out, so the column minima spread over more rows than a column
-    // reduction alone leaves them (SAP Q: -16..28 % augmenting-path steps in the host model)
-    double vmin = __builtin_inf();
-    int imin = 0;
 #pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        if (k < n) {
-            const float x = k < 32 ? acc.lo[k] : acc.hi[k - 32];
-            const float uk = wave_min_f32_nonan(live ? x : __builtin_inff());
-            u = lane == k ? (double)uk : u;
-            const double r = (double)x - (double)uk;
-            const bool t = r < vmin;
-            vmin = t ? r : vmin;
-            imin = t ? k : imin;
-            amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+        for (int k = 0; k < 64; ++k) {
+            if (k < n) {
+                const float x = k < 32 ? acc.lo[k] : acc.hi[k - 32];
+                const float uk = wave_min_f32_nonan(live ? x : __builtin_inff());
+                u = lane == k ? (double)uk : u;
+                const double r = (double)x - (double)uk;
+                const bool t = r < vmin;
+                vmin = t ? r : vmin;
+                imin = t ? k : imin;
+                amax = __builtin_fmaxf(amax, __builtin_fabsf(x));
+            }
         }
     }
+    // (float32 row minima are exact; the column reduction's float64 differences are rounded once,
+    // relative 2^-53, far inside the certificate's S 2^-40 slack -- not exact when the operands'
+    // exponents differ by more than ~29 bits; dual feasibility is re-checked by the certificate)
     // each row keeps one of the columns whose minimum it holds (the lowest: any keeps
     // complementary slackness, rc = 0 there): one LDS minimum per column
     uint32_t *slot32 = reinterpret_cast<uint32_t *>(slot);
@@ -701,7 +687,6 @@ __device__ int lsa_fast_reg64(const Acc &acc, int n, int (&col4row)[1], int *ste
     r4c = (live && won == (uint32_t)lane) ? imin : -1;
     c4r = (live && mine != 0xffffffffu) ? (int)mine : -1;
     v = live ? vmin : 0.0;
-    }
     int path = -1;
     uint64_t freerows = __ballot(live && c4r < 0);
     int ncand = 1;

@@ -9,7 +9,8 @@ matrices, it counts the augmenting-path steps of
   * the certified fast path (csrc/lsa_wave.h lsa_fast_reg64): row + column reduction, then the
     same shortest-augmenting-path step for the rows it leaves free only,
 checks both assignments against scipy, and evaluates the fast path's uniqueness certificate
-(dual feasibility within S 2^-40, acyclic near-tight graph at S 2^-30).  The kernel's steps
+(dual feasibility within S 2^-40, acyclic near-tight graph at S 2^-30).  --q-seq: the warm start
+(asg_sap_select_warm) against the cold one on captured consecutive Q (tools/sap_reda_probe.py).  The kernel's steps
 and certificate are this model's; the GPU figures are bench.py's roofline_lsa.
 """
 import argparse
@@ -69,10 +70,11 @@ def scipy_steps(C):
     return c4r, steps
 
 
-def fast_path(C):
-    """lsa_fast_reg64: (assignment, steps, certified)."""
+def fast_path(C, vwarm=None, return_v=False):
+    """lsa_fast_reg64: (assignment, steps, certified[, final v]).  vwarm: the warm start's
+    column duals (u_k = min_j (c_kj - vwarm_j), then the same column reduction and claims)."""
     n = C.shape[0]
-    u = C.min(1).copy()  # row reduction
+    u = C.min(1).copy() if vwarm is None else (C - vwarm[None, :]).min(1)  # row reduction
     R = C - u[:, None]
     v = R.min(0).copy()  # column reduction of the rest
     imin = R.argmin(0)
@@ -135,6 +137,8 @@ def fast_path(C):
         if (nA == A).all():
             break
         A = nA
+    if return_v:
+        return x, steps, bool(ok and not A.any()), v
     return x, steps, bool(ok and not A.any())
 
 
@@ -162,12 +166,43 @@ def sap_matrices(n, m, count, use_rnn, eps, seed):
     return out
 
 
+def warm_sequence(path, eps, seed=0, envs=16):
+    """Cold vs warm-started fast path on consecutive selections of captured Q sequences
+    ([steps, envs, n, n] float32, tools/sap_reda_probe.py --save): each warm call starts from the
+    previous step's final column duals (shifted to a zero minimum, as the kernel keeps them)."""
+    from scipy.optimize import linear_sum_assignment
+    Q = np.load(path)
+    rng = np.random.RandomState(seed)
+    tc = tw = cc = cw = 0
+    for e in range(min(envs, Q.shape[1])):
+        vprev = None
+        for t in range(Q.shape[0]):
+            q = Q[t, e].astype(np.float32)
+            q = (q + rng.randn(*q.shape).astype(np.float32) * np.float32(2 * eps * np.abs(q).mean())).astype(np.float32)
+            C = -q.astype(np.float64)
+            ref = linear_sum_assignment(q, maximize=True)[1]
+            xc, sc, okc, vc = fast_path(C, return_v=True)
+            xw, sw, okw, vw = fast_path(C, vwarm=vprev, return_v=True)
+            assert (xc == ref).all() and (xw == ref).all()
+            if vprev is not None:
+                tc, tw, cc, cw = tc + sc, tw + sw, cc + okc, cw + okw
+            vprev = vw - vw.min()
+    print(f"{os.path.basename(path)} eps={eps}: cold {tc} steps, warm {tw} ({tw / max(tc, 1):.2f}x); certified "
+          f"cold {cc}, warm {cw}")
+
+
 def main():
     from scipy.optimize import linear_sum_assignment
     p = argparse.ArgumentParser()
     p.add_argument("--problems", type=int, default=4)
     p.add_argument("--seed", type=int, default=3)
+    p.add_argument("--q-seq", nargs="*", default=[], help="captured Q sequences (.npy) for the warm-start model")
+    p.add_argument("--eps", type=float, default=0.0)
     a = p.parse_args()
+    if a.q_seq:
+        for path in a.q_seq:
+            warm_sequence(path, a.eps)
+        return
     for eps in (0.0, 0.05, 0.3, 1.0):
         for rnn in (False, True):
             mats = sap_matrices(64, 64, a.problems, rnn, eps, a.seed)
