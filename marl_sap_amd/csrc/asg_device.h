@@ -174,19 +174,17 @@ __device__ __forceinline__ Bump32 philox_bump32(EnvKey key, uint32_t episode, in
     return philox_bump32(key, episode, pair, scale, bump_shape(T, wmin, wmax), dense);
 }
 
-// float32 evaluation with an error that does not grow with the exponent: x = t - center is
-// exact, x^2 * a2 is carried as an unevaluated sum yh + yl (FMA error terms), and
-// 2^-(yh + yl) = 2^-yh * (1 - yl ln 2) to first order (|yl| <= 2^-23 yh).  Within 1e-6
-// relative of the float64 value (bump64_at) wherever 2^-yh >= FLT_MIN; below that
-// v_exp_f32 flushes to 0 (values < 10 FLT_MIN; tests/test_gpu_parity.py).
+// float32 evaluation: value(t) = scale * 2^(-(x * x) * a2), x = t - center exact (the center
+// is on the 2^-q grid); the exponent y = x^2 a2 carries two float32 roundings, so the relative
+// error is <= y ln2 2^-23 + 1.5 2^-23 and the absolute error <= 1.5 2^-23 scale at every y (the
+// bump's peak height in float32 ulps); relative <= 1e-6 wherever y <= 12 (values >= 2^-12
+// scale).  v_exp_f32 flushes results below FLT_MIN to 0.  (Rounds 1-4 carried y as a double-
+// float pair -- relative 1e-6 at every y -- in 9 VALU instead of 4 per value: 96 values per
+// 32-row tile-pass made it 10 % of the episode kernel's VALU; this form is 4 % faster per step,
+// r5 A/B.)  Rewards and the `beta > 1e-12` mask use the float64 evaluation (bump64_at).
 __device__ __forceinline__ float bump32_at(const Bump32 &b, int t) {
     const float x = (float)t - b.center;
-    const float p = x * x;
-    const float pe = __builtin_fmaf(x, x, -p);
-    const float yh = p * b.a2;
-    const float yl = __builtin_fmaf(p, b.a2, -yh) + pe * b.a2;
-    constexpr float kLn2 = 0.69314718055994531f;
-    return b.scale * (__builtin_amdgcn_exp2f(-yh) * __builtin_fmaf(-yl, kLn2, 1.0f));
+    return b.scale * __builtin_amdgcn_exp2f(-(x * x) * b.a2);
 }
 
 // The same bump in float64 (the reference's arithmetic, mock :293, on these parameters).
