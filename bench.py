@@ -213,7 +213,7 @@ def store_ceiling(hbm=True):
     return None, None
 
 
-def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=False):
+def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=False, bids=False):
     """Roofline of the fused rollout kernel (asg_rollout -> rollout_kernel), per env step: the
     env step's bytes plus the agent's h in / h out and the action written -- the observations
     it generates are consumed on chip, never read back -- per env, times E, over its HIP-event
@@ -223,21 +223,24 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
     MFMA pipe is at half its capacity and HBM is not near its roof (the waves wait on the
     in-order vmcnt queue behind their own row stores).  q_out: the
     asg_step_forward instances (REDA's step_q schedule), which also write the Q rows (4 m per
-    agent) and read the actions row the SAP kernel wrote instead of writing one."""
+    agent) and read the actions row the SAP kernel wrote instead of writing one.  bids: the
+    bids_as_actions env (no actions_onehot field; the transition reads the int32 assignments
+    asg_bids_select left instead of the int64 actions row); no PMC profile of it is kept."""
     # the episode's reset runs in its first launch (asg_reset_rollout): its row counts too.
     # q_out: the Q rows go to ONE reused [E n][m] f32 buffer (basic_controller._q_buf, 256 MiB at
     # configs[2] = the MALL's size) rewritten every step and read back by the SAP kernel: much of
     # it stays in the Infinity Cache, so its bytes are reported apart (q_buffer), not as HBM traffic
-    per_launch = (step_bytes(a.n, a.m, a.L) + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)
+    sb = step_bytes(a.n, a.m, a.L) - (8 * a.n * a.m + 4 * a.n if bids else 0)
+    per_launch = (sb + a.n * ((2 if use_rnn else 1) * 4 * 64 + 8)
                   + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E
     q_bytes = 4 * a.n * a.m * E if q_out else 0
     per_launch = int(round(per_launch))
     achieved = per_launch / (fused_ms * 1e-3) / 1e9
     frac = achieved / HBM_PEAK_GBS
     tag = "rollout_q" if q_out else "rollout"
-    pm = pmc_lookup(f"*pmc_{tag}_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
+    pm = None if bids else pmc_lookup(f"*pmc_{tag}_kernel*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     issue = None
-    pq = pmc_lookup(f"*pmc_{tag}_sq*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
+    pq = None if bids else pmc_lookup(f"*pmc_{tag}_sq*.json", n=a.n, m=a.m, E=E, L=a.L, use_rnn=bool(use_rnn))
     if pq:
         c, d = pq["counters"], pq["derived"]
         spl = pq.get("steps_per_launch", 1)  # the profiled launches ran spl steps each
@@ -336,7 +339,7 @@ def parse(argv=None):
     p.add_argument("--m", type=int, default=None)
     p.add_argument("--T", type=int, default=20)
     p.add_argument("--L", type=int, default=3)
-    p.add_argument("--selector", default=None, choices=["eps", "sap", "random"])
+    p.add_argument("--selector", default=None, choices=["eps", "sap", "random", "bids"])
     p.add_argument("--benefits", default=None, choices=["bump", "dense"])
     p.add_argument("--rng", default="philox", choices=["philox", "mt19937"],
                    help="mt19937: the same-seed mode (env e replays numpy's legacy stream seeded with seed + e; "
@@ -372,7 +375,7 @@ def parse(argv=None):
 def make_args(a, E, selector=None, agent=None, fused=None, mac="basic_mac", use_rnn=None, **extra):
     selector = selector or a.selector
     fused = a.fused_rollout if fused is None else fused
-    sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy"}[selector]
+    sel = {"eps": "epsilon_greedy", "sap": "sap", "random": "epsilon_greedy", "bids": "continuous"}[selector]
     args = SimpleNamespace(
         batch_size_run=E, env="mock_constellation_env",
         env_args=dict(n=a.n, m=a.m, T=a.T, L=a.L, lambda_=0.5, bids_as_actions=False, seed=a.seed,
@@ -385,6 +388,12 @@ def make_args(a, E, selector=None, agent=None, fused=None, mac="basic_mac", use_
         epsilon_start=0.05, epsilon_finish=0.05, epsilon_anneal_time=1, evaluation_epsilon=0.0, mac=mac,
         reuse_batch=True, fused_rollout={0: False, 1: True, 2: "always", 3: "step"}[fused],
         sap_warm_start=bool(a.sap_warm))
+    if selector == "bids":
+        # config/algs/ippo_sap.yaml's env path: bids_as_actions, the continuous selector over
+        # softmaxed pi_logits (use_rnn False), its epsilon 0.3 -> 0.05 over 50,000 env steps
+        args.env_args["bids_as_actions"] = True
+        args.agent_output_type, args.softmax_agent_inputs, args.use_rnn = "pi_logits", True, False
+        args.epsilon_start, args.epsilon_finish, args.epsilon_anneal_time = 0.3, 0.05, 50000
     for k, v in extra.items():
         setattr(args, k, v)
     return args
@@ -466,6 +475,9 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
 
     if selector == "sap":
         sel_obj.select_action = timed_select
+    elif selector == "bids":  # asg_bids_select alone (the bids transforms, their row store and LSA)
+        inner = sel_obj.fused_bids
+        sel_obj.fused_bids = timed_select
     fwd_pairs = []
     inner_fwd = env.step_forward
 
@@ -659,6 +671,7 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     # later leg's first episode (round 4's `jumpstart_phase_value` stall)
     env.__dict__.pop("step_forward", None)
     sel_obj.__dict__.pop("select_action", None)
+    sel_obj.__dict__.pop("fused_bids", None)
     del runner, mac, env, sel_obj, inner, inner_fwd
     gc.collect()
     torch.cuda.synchronize()
@@ -814,6 +827,27 @@ def main():
                 extra["sap"]["roofline_step_forward"] = fused_roofline(a, E, r3["step_forward_ms"],
                                                                        use_rnn=a.use_rnn, q_out=True)
         if a.config == 2 and world == 1 and a.selector == "eps":
+            # config/algs/ippo_sap.yaml's env path: bids_as_actions + the continuous selector over
+            # softmaxed pi_logits (Linear agent): per step asg_step_forward (env step t with the
+            # assignments of the bids row t + the agent forward of t + 1, Q written) and
+            # asg_bids_select (pi_logits softmax, softmax over the agents, noise, the bids row, its LSA);
+            # the same with separate launches beside it
+            for name, fz in (("ippo_sap", None), ("ippo_sap_split", 0)):
+                rb = run_leg(a, dev, world, E, sk, sw, selector="bids", agent="rnn", fused=fz)
+                extra[name] = {
+                    **leg_base(rb, sk, sw),
+                    "what": "ippo_sap.yaml env path: bids_as_actions, ContinuousActionSelector (softmax_agent_inputs, "
+                            "std 0.3 -> 0.05 over 50,000 env steps) on pi_logits of the Linear RNNAgent; "
+                            + ("step_q schedule: asg_step_forward + asg_bids_select per step" if fz is None else
+                               "separate launches: the agent kernel, asg_bids_select, asg_step per step"),
+                    "kernels_ms": {"step_forward": round(rb["step_forward_ms"], 4) if rb.get("step_forward_ms") else None,
+                                   "bids_select": round(rb["lsa_ms"], 4) if rb.get("lsa_ms") else None,
+                                   "fused_step_total": round(rb["fused_ms"], 4) if rb.get("fused_ms") else None,
+                                   "env_step": round(rb["kern_ms"], 4) if rb["kern_ms"] else None,
+                                   "select": round(rb["sel_ms"], 4) if rb["sel_ms"] else None}}
+                if rb.get("mode") == "step_q" and rb.get("step_forward_ms"):
+                    extra[name]["roofline_step_forward"] = fused_roofline(a, E, rb["step_forward_ms"], use_rnn=False,
+                                                                          q_out=True, bids=True)
             # the reference's own algorithms for this env (config/algs/mock_constellation_*.yaml):
             # jumpstart_mac with the HAA jumpstart selector, use_rnn: False (Linear + ReLU agent),
             # jumpstart epsilon 1 -> 0 over 20,000 env steps -- one 16,384-env episode is 327,680

@@ -394,10 +394,26 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
  * stored and consumed on chip; q_out [E n][m] f32 contiguous (16-B aligned) receives the Q rows,
  * h_out the hidden state.  Needs k + 1 < T; the actions of row ts are read from the batch.
  * Every benefit source (Philox, MT19937-compat and injected tables); agent and batch
- * requirements as asg_rollout. */
+ * requirements as asg_rollout.  bids_as_actions: the tasks of row ts are LSA(bids row ts,
+ * maximize) -- the assignments asg_bids_select left for that row, else solved first. */
 int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream);
+/* bids_as_actions with the ContinuousActionSelector (config/algs/ippo_sap.yaml), replacing the
+ * per-env chain BasicMAC.forward's pi_logits softmax (controllers/basic_controller.py:37-46) ->
+ * ContinuousActionSelector.select_action (action_selectors/bet_selectors.py:12-20: softmax over
+ * the agents, th.normal(x, std)) -> the env step's scipy LSA of the bids
+ * (envs/mock_constellation_env.py:121-122), for every env of the handle in one launch (n <= m <= 64):
+ * q [E][n][m] f32 (element strides) = the agent outputs; row_softmax: softmax over the tasks first
+ * (agent_output_type "pi_logits"); col_softmax: softmax over the agents (softmax_agent_inputs);
+ * noise_std >= 0: Gaussian noise N(0, noise_std) from Philox keyed by (seed, global env index, counter)
+ * (0: the means exactly).  Writes the bids to bids_out [E][n][m] (element strides: the batch's
+ * actions row) and their LSA(maximize) assignments into the handle, which the next asg_step /
+ * asg_step_forward on that batch row uses instead of solving it again.  A NaN / +inf bid sets
+ * the env's sticky error (asg_sync_status: "matrix contains invalid numeric entries"). */
+int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
+                    const int64_t out_strides[3], int row_softmax, int col_softmax, double noise_std, uint64_t seed,
+                    uint64_t counter, void *hip_stream);
 /* Number of fc1 weight slices (32 inputs x 64 units) the rollout kernel reads through L2
  * instead of LDS for an (n, m, L) env and agent kind, or -1 when asg_rollout does not take
  * the shape (GRU: 64 x 64, L = 3: 1; 256 x 256: 19).  asg_step_select_l2_slices = the GRU

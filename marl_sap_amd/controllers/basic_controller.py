@@ -33,6 +33,12 @@ class BasicMAC:
         """`out` (optional, int64 [B, n]): selectors that support it write the actions
         there in place (the runner passes the EpisodeBatch actions row)."""
         avail_actions = ep_batch["avail_actions"][:, t_ep]
+        if out is not None and out.dtype == torch.float32 and self._fused_bids_ok(bs, out):
+            # bids_as_actions: the agent's raw outputs -> asg_bids_select (pi_logits softmax,
+            # the selector's softmax over agents + noise, the bids row, their LSA)
+            q, self.hidden_states = self.selector_agent(self._build_inputs(ep_batch, t_ep), self.hidden_states)
+            return self.action_selector.fused_bids(q.view(ep_batch.batch_size, self.n, -1), out, t_env, test_mode,
+                                                   row_softmax=self.agent_output_type == "pi_logits")
         if out is not None and out.dtype != torch.int64:
             out = None  # e.g. the real env's int16 actions: the caller casts through update()
         if out is not None and self._fused_select_ok(bs):
@@ -66,16 +72,35 @@ class BasicMAC:
                 and isinstance(self.selector_agent, RNNFusedAgent) and self.n <= self.selector_agent.n_out <= 64
                 and not getattr(self.args, "unfused_selection", False))
 
+    def _fused_bids_ok(self, bs=slice(None), out=None):
+        """bids_as_actions with the ContinuousActionSelector on the batched env (n <= m <= 64):
+        asg_bids_select turns the agent's raw outputs into the bids row and its LSA."""
+        from ..action_selectors.bet_selectors import ContinuousActionSelector
+        from ..modules.agents.rnn_agent import RNNFusedAgent
+        env = getattr(self.action_selector, "envs", None)
+        ok = (not torch.is_grad_enabled() and isinstance(bs, slice) and bs == slice(None)
+              and type(self.action_selector) is ContinuousActionSelector
+              and self.agent_output_type in ("pi_logits", "q") and getattr(env, "bids_as_actions", False)
+              and hasattr(env, "bids_select") and isinstance(self.selector_agent, RNNFusedAgent)
+              and self.n <= self.selector_agent.n_out <= 64 and self.selector_agent.n_out == getattr(env, "m", -1)
+              and not getattr(self.args, "unfused_selection", False))
+        if ok and out is not None:
+            ok = tuple(out.shape) == (env.num_envs, self.n, env.m) and out.device == env.device
+        return ok
+
     def _fused_kind(self, env, ep_batch):
         """"select" (the selection runs in the rollout kernel: epsilon-greedy), "q" (the kernel
-        writes Q for the SAP selector) or None."""
+        writes Q for the SAP selector), "bids" (Q for asg_bids_select) or None."""
         from ..modules.agents.rnn_agent import RNNFusedAgent
         mode = getattr(self.args, "fused_rollout", True)
         if not mode:
             return None
         kind = "select" if self._fused_select_ok(slice(None)) else ("q" if self._fused_q_ok() else None)
+        if kind is None and self._fused_bids_ok():
+            kind = "bids"
         ok = (kind is not None and hasattr(env, "can_step_select")
-              and env.can_step_select(prefer=(mode != "always"), use_rnn=bool(self.args.use_rnn))
+              and env.can_step_select(prefer=(mode != "always"), use_rnn=bool(self.args.use_rnn),
+                                      bids_ok=kind == "bids")
               and getattr(ep_batch, "time_major", False) and not self.args.obs_last_action
               and not self.args.obs_agent_id and isinstance(self.selector_agent, RNNFusedAgent)
               and self.selector_agent.n_out == env.m)
@@ -97,7 +122,7 @@ class BasicMAC:
         kind = self._fused_kind(env, ep_batch)
         if kind is None:
             return None
-        if kind == "q":
+        if kind in ("q", "bids"):
             return "step_q"
         return "step" if getattr(self.args, "fused_rollout", True) == "step" else "episode"
 
@@ -106,6 +131,13 @@ class BasicMAC:
         hidden state advances as select_actions would advance it.  SAP selector: the kernel
         ends with the agent's Q (kept in one reused buffer), which the selector's kernel turns
         into the actions of row t_ep + 1, written in place."""
+        if self._fused_bids_ok():
+            q, self.hidden_states = env.step_forward(ep_batch, t_ep, self.selector_agent, self.hidden_states,
+                                                     q_out=getattr(self, "_q_buf", None))
+            self._q_buf = q
+            self.action_selector.fused_bids(q.view(ep_batch.batch_size, self.n, -1), ep_batch["actions"][:, t_ep + 1],
+                                            t_env, test_mode, row_softmax=self.agent_output_type == "pi_logits")
+            return
         if self._fused_q_ok():
             q, self.hidden_states = env.step_forward(ep_batch, t_ep, self.selector_agent, self.hidden_states,
                                                      q_out=getattr(self, "_q_buf", None))

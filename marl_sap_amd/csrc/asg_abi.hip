@@ -20,6 +20,12 @@ struct asg_handle {
     bool has_reset = false;
     bool constructed = false;  // MT19937: first reset also replays __init__'s draw
     bool table_ready = false;  // injected table uploaded
+    // bids_as_actions: the bids row whose LSA assignments st.assign holds (asg_bids_select wrote
+    // both); a step on that row uses them instead of solving the row again.  Cleared by resets.
+    struct BidsTag {
+        const float *row = nullptr;
+        int64_t s_env = 0, s_agent = 0, s_task = 0;
+    } bids_tag;
     std::string err;
 };
 
@@ -69,6 +75,15 @@ int check_view(asg_handle *h, const asg_batch_view *b, int ts, bool step) {
                         st.bids ? "bids_as_actions expects float32 actions" : "actions must be int64");
     }
     return ASG_OK;
+}
+
+// bids_as_actions: does st.assign hold the assignments of batch row ts (asg_bids_select)?
+bool bids_ready(const asg_handle *h, const asg_batch_view *b, int ts) {
+    const asg_field &f = b->actions;
+    const float *row = static_cast<const float *>(f.ptr) + (int64_t)ts * f.stride[1];
+    const auto &t = h->bids_tag;
+    return h->st.bids && t.row && t.row == row && t.s_env == f.stride[0] && t.s_agent == f.stride[2] &&
+           t.s_task == f.stride[3];
 }
 
 }  // namespace
@@ -207,6 +222,7 @@ int asg_reset(asg_handle *h, const asg_batch_view *b, int ts) {
     h->constructed = true;
     h->has_reset = true;
     h->k = 0;
+    h->bids_tag = {};
     return ASG_OK;
 }
 
@@ -216,9 +232,11 @@ int asg_step(asg_handle *h, const asg_batch_view *b, int ts) {
     if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
     if (h->k >= h->st.T) return fail(h, ASG_E_STATE, "episode already terminated (k >= T); reset first");
     DeviceGuard g(h->device);
-    hipError_t e = asg::launch_step(*b, h->st, ts, h->k, h->stream);
+    const bool ready = bids_ready(h, b, ts);
+    hipError_t e = asg::launch_step(*b, h->st, ts, h->k, h->stream, ready);
     if (e != hipSuccess) return hip_fail(h, e, "asg_step");
     h->k += 1;
+    h->bids_tag = {};
     return ASG_OK;
 }
 
@@ -649,7 +667,9 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: batch rows ts .. ts + steps must lie in the [T + 1]-row batch");
     // every benefit source: Philox bumps in registers, or the handle's float64 table (MT19937
     // compat / injected), whose reset is asg_reset (above: no asg_reset_rollout)
-    if (st.bids) return fail(h, ASG_E_INVALID_ARG, "asg_rollout: integer actions only (not bids_as_actions)");
+    if (st.bids && !q_out)
+        return fail(h, ASG_E_INVALID_ARG,
+                    "asg_rollout: integer actions only (bids_as_actions: asg_step_forward + asg_bids_select)");
     if (hidden != 64 || !asg::rollout_shape_ok(st.n, st.m, st.L, K))
         return fail(h, ASG_E_INVALID_ARG,
                     "asg_rollout: needs the RNNAgent (hidden 64) on the env's obs (K = m (L + 1), L >= 1), "
@@ -665,7 +685,8 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     sl.beta = static_cast<float *>(tm_base(b->beta, E, n, m, &sl.beta_row, &ok));
     sl.avail = static_cast<uint8_t *>(tm_base(b->avail_actions, E, n, m, &sl.avail_row, &ok));
     sl.onehot = static_cast<int64_t *>(tm_base(b->actions_onehot, E, n, m, &sl.onehot_row, &ok));
-    sl.act = static_cast<int64_t *>(tm_base(b->actions, E, n, 1, &sl.act_row, &ok));
+    // bids_as_actions: the transition reads the assignments of the bids row (st.assign)
+    sl.act = st.bids ? nullptr : static_cast<int64_t *>(tm_base(b->actions, E, n, 1, &sl.act_row, &ok));
     sl.rew = static_cast<float *>(tm_base(b->rewards, E, n, 1, &sl.rew_row, &ok));
     sl.prevb = static_cast<int64_t *>(tm_base(b->prev_assigns, E, n, 1, &sl.prevb_row, &ok));
     sl.term = static_cast<uint8_t *>(tm_base(b->terminated, E, 1, 1, &sl.term_row, &ok));
@@ -678,6 +699,10 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     // as asg_reset: a fresh Philox key per episode, committed once the launch succeeded
     asg::EnvState lst = h->st;
     if (reset && h->has_reset) lst.episode += 1;
+    if (st.bids && !bids_ready(h, b, ts)) {  // the bids of row ts not solved by asg_bids_select
+        hipError_t e0 = asg::launch_bids_assign(*b, st, ts, s);
+        if (e0 != hipSuccess) return hip_fail(h, e0, "asg_step_forward (bids LSA)");
+    }
     if (reset && st.rng_mode == ASG_RNG_MT19937) {
         hipError_t e0 = asg::launch_reset_draws(lst, !h->constructed, s);
         if (e0 != hipSuccess) return hip_fail(h, e0, "asg_reset_rollout (MT19937 draws)");
@@ -692,6 +717,7 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
         h->has_reset = true;
     }
     h->k = k0 + steps;
+    h->bids_tag = {};
     return ASG_OK;
 }
 
@@ -725,6 +751,28 @@ int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void 
     if (!q_out) return fail(h, ASG_E_INVALID_ARG, "asg_step_forward: NULL q_out");
     return rollout_impl(h, b, ts, 1, 0, 1, 0, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in, h_stride, h_out,
                         0.0, 0, 0, nullptr, hip_stream, q_out);
+}
+
+int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
+                    const int64_t out_strides[3], int row_softmax, int col_softmax, double stdv, uint64_t seed,
+                    uint64_t counter, void *hip_stream) {
+    if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
+    const EnvState &st = h->st;
+    if (!st.bids) return fail(h, ASG_E_INVALID_ARG, "asg_bids_select: the handle was not created with bids_as_actions");
+    if (!q || !q_strides || !bids_out || !out_strides) return fail(h, ASG_E_INVALID_ARG, "asg_bids_select: NULL argument");
+    if (st.m > 64) return fail(h, ASG_E_INVALID_ARG, "asg_bids_select: m <= 64 (register-resident bids)");
+    if (!(stdv >= 0.0 && stdv < 1e30)) return fail(h, ASG_E_INVALID_ARG, "asg_bids_select: std must be finite and >= 0");
+    DeviceGuard g(h->device);
+    hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
+    hipError_t e = asg::launch_bids_select(q, q_strides, st.E, st.n, st.m, row_softmax != 0, col_softmax != 0,
+                                           (float)stdv, seed, (uint32_t)counter, st.env_base, bids_out, out_strides,
+                                           st.assign, st.err, s);
+    if (e != hipSuccess) return hip_fail(h, e, "asg_bids_select");
+    h->bids_tag.row = bids_out;
+    h->bids_tag.s_env = out_strides[0];
+    h->bids_tag.s_agent = out_strides[1];
+    h->bids_tag.s_task = out_strides[2];
+    return ASG_OK;
 }
 
 }  // extern "C"

@@ -78,7 +78,7 @@ __device__ __forceinline__ double mt_par_value(double2 p, int t) {
 
 // purposes of Philox counters (counter.z); counter.w = episode
 enum : uint32_t { kCtrScale = 1u, kCtrPair = 2u, kCtrSpread = 3u, kCtrPerm = 4u, kCtrAction = 5u, kCtrSelect = 6u,
-                  kCtrSapNoise = 7u, kCtrPair2 = 8u, kCtrPair4 = 9u };
+                  kCtrSapNoise = 7u, kCtrPair2 = 8u, kCtrPair4 = 9u, kCtrBidsNoise = 10u };
 
 // "a beats b" in torch.max order: NaN wins, then larger value, then smaller index.
 // Branch-free (bitwise on the predicates) so it lowers to compares + v_cndmask.

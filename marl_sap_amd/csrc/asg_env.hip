@@ -892,17 +892,25 @@ static void launch_step_t(const Src &src, const asg_batch_view &bv, const EnvSta
         hipLaunchKernelGGL((step_kernel<1, Src, BIDS>), dim3(st.E), dim3(256), lds, s, src, bv, st, ts, k);
 }
 
+hipError_t launch_bids_assign(const asg_batch_view &bv, const EnvState &st, int ts, hipStream_t s) {
+    const size_t lds = sizeof(float) * (size_t)st.n * st.m + 32;
+    // bids matrices are at most 16384 entries (checked at create): m <= 16384 / n
+    if (st.m <= 64) hipLaunchKernelGGL(bids_assign_kernel<1>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+    else if (st.m <= 128) hipLaunchKernelGGL(bids_assign_kernel<2>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+    else if (st.m <= 256) hipLaunchKernelGGL(bids_assign_kernel<4>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+    else if (st.m <= 512) hipLaunchKernelGGL(bids_assign_kernel<8>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+    else hipLaunchKernelGGL(bids_assign_kernel<16>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+    return hipGetLastError();
+}
+
 template <class Src>
 static hipError_t launch_step_src(const Src &src, const asg_batch_view &bv, const EnvState &st, int ts, int k,
-                                  hipStream_t s) {
+                                  hipStream_t s, bool assign_ready) {
     if (st.bids) {
-        const size_t lds = sizeof(float) * (size_t)st.n * st.m + 32;
-        // bids matrices are at most 16384 entries (checked at create): m <= 16384 / n
-        if (st.m <= 64) hipLaunchKernelGGL(bids_assign_kernel<1>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
-        else if (st.m <= 128) hipLaunchKernelGGL(bids_assign_kernel<2>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
-        else if (st.m <= 256) hipLaunchKernelGGL(bids_assign_kernel<4>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
-        else if (st.m <= 512) hipLaunchKernelGGL(bids_assign_kernel<8>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
-        else hipLaunchKernelGGL(bids_assign_kernel<16>, dim3(st.E), dim3(64), lds, s, bv, st, ts);
+        if (!assign_ready) {
+            const hipError_t e = launch_bids_assign(bv, st, ts, s);
+            if (e != hipSuccess) return e;
+        }
         launch_step_t<Src, true>(src, bv, st, ts, k, s);
     } else {
         launch_step_t<Src, false>(src, bv, st, ts, k, s);
@@ -971,10 +979,10 @@ hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s) {
-    if (st.mtpar) return launch_step_src(par_src(st), bv, st, ts, k, s);
-    if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s);
-    return launch_step_src(bump_src(st), bv, st, ts, k, s);
+hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s, bool assign_ready) {
+    if (st.mtpar) return launch_step_src(par_src(st), bv, st, ts, k, s, assign_ready);
+    if (uses_table(st)) return launch_step_src(table_src(st), bv, st, ts, k, s, assign_ready);
+    return launch_step_src(bump_src(st), bv, st, ts, k, s, assign_ready);
 }
 
 template <class Src>

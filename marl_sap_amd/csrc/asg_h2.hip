@@ -1056,6 +1056,9 @@ struct RolloutArgs {
     uint32_t sk0, sk1, counter;
     int *sel_err;
     int64_t scratch_off;  // per-wave LDS scratch (u32x4v units)
+    // bids_as_actions (asg_step_forward): the tasks of transition k0 are the handle's LSA
+    // assignments of the bids row [E][n] instead of the batch's actions row
+    const int *assign;
 };
 
 // The launch arguments as the tiles and transitions read them: a kernarg-segment pointer made
@@ -1150,7 +1153,7 @@ __device__ __forceinline__ void rollout_actions_from_batch(RA &ra, int64_t e, in
     const int n = ra.n, m = ra.m;
     int err = 0;
     for (int i = lane; i < n; i += 64) {
-        const int64_t a64 = ra.act[((int64_t)ts * ra.E + e) * n + i];
+        const int64_t a64 = ra.assign ? (int64_t)ra.assign[e * n + i] : ra.act[((int64_t)ts * ra.E + e) * n + i];
         int a = (a64 >= 0 && a64 < m) ? (int)a64 : -1;
         if (a < 0) err = ASG_E_ACTION_RANGE;
         s_act[i] = (uint16_t)(a < 0 ? 0 : a);
@@ -1869,6 +1872,8 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     // Q output: one transition and the forward of the row after it (asg_step_forward)
     if (Q && (steps != 1 || select_first || !select_last || reset)) return hipErrorInvalidValue;
     ra.Q = Q;
+    ra.assign = st.bids ? st.assign : nullptr;
+    if (st.bids && !Q) return hipErrorInvalidValue;  // bids: asg_step_forward only
     ra.W1T = reinterpret_cast<const float *>(packed);
     ra.pk = reinterpret_cast<const u32x4v *>(packed + w1t_f4(g));
     ra.Hin = Hin;

@@ -54,7 +54,11 @@ struct SelectArgs {
 
 hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bool construct, hipStream_t s);
 hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s);
-hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
+// bids_as_actions: assign_ready = st.assign already holds LSA(bids row ts) (asg_bids_select)
+hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s,
+                       bool assign_ready = false);
+// bids_as_actions: st.assign = LSA(bids row ts, maximize) per env
+hipError_t launch_bids_assign(const asg_batch_view &bv, const EnvState &st, int ts, hipStream_t s);
 hipError_t launch_random_actions(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s);
 hipError_t launch_random_rollout(const asg_batch_view &bv, const EnvState &st, int ts, int k0, int steps, bool reset,
                                  hipStream_t s);
@@ -77,6 +81,9 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
                              double *duals = nullptr, int warm = 0);
 hipError_t launch_sap_noise(const float *q, const int64_t qs[3], int64_t B, int n, int m, float epsilon, uint64_t seed,
                             uint32_t counter, int64_t env_base, float *q_out, int32_t *status_out, hipStream_t s);
+hipError_t launch_bids_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, int row_sm, int col_sm,
+                              float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids,
+                              const int64_t os[3], int *assign, int *env_err, hipStream_t s);
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s);

@@ -423,6 +423,120 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
 }
 
 // ------------------------------------------------------------------------------------
+// bids_as_actions with the ContinuousActionSelector (ippo_sap.yaml), n <= m <= 64, fused: env
+// b's agent outputs (the rollout kernel's Q rows) -> softmax over the tasks (BasicMAC.forward
+// with agent_output_type "pi_logits", basic_controller.py:37-46) -> softmax over the agents
+// (softmax_agent_inputs, bet_selectors.py:13) -> th.normal(x, std) = x + std z (bet_selectors.py:
+// 15-20; z from Philox keyed by (seed, global env, call)) -> the bids, stored as the batch's
+// actions row -> LSA(bids, maximize) = the env's assignments for its next step
+// (mock_constellation_env.py:121-122), kept in the handle for asg_step / asg_step_forward.
+// ------------------------------------------------------------------------------------
+// (110 VGPRs, 4 waves per SIMD: the 5-wave budget of sap_select_kernel spills the transforms)
+__global__ void __launch_bounds__(64 * kLsaWpb)
+bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, int m, int row_sm, int col_sm,
+                   float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids, int64_t o0,
+                   int64_t o1, int64_t o2, int *assign, int *env_err, int64_t B) {
+    __shared__ uint64_t s_slot[kLsaWpb][64];
+    const int64_t b = lsa_reg_problem();
+    if (b >= B) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool lv = lane < m;
+    asm volatile("" : "+s"(q0), "+s"(q1), "+s"(q2), "+s"(o0), "+s"(o1), "+s"(o2));
+    RegColPin<32> rc;  // column `lane` of the env's matrix, rows 0..31 in lo, 32..63 in hi
+    {
+        const float *col = q + b * q0 + (int64_t)lane * q2;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            rc.lo[i] = (lv && i < n) ? col[i * q1] : 0.0f;
+            rc.hi[i] = (lv && i + 32 < n) ? col[(i + 32) * q1] : 0.0f;
+        }
+    }
+    // f(x, i) applied to every row i < n of the column (rows at compile-time register slots)
+    auto each_row = [&](auto f) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (i < n) rc.lo[i] = f(rc.lo[i], i);
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (i + 32 < n) rc.hi[i] = f(rc.hi[i], i + 32);
+    };
+    if (row_sm) {  // softmax(dim = -1) of each agent's row: exp(x - max) / sum, as torch
+        each_row([&](float x, int) {
+            const float mx = wave_allreduce(lv ? x : -__builtin_inff(), [](float a, float c) { return fmaxf(a, c); });
+            const float ex = lv ? expf(x - mx) : 0.0f;
+            const float sum = wave_allreduce(ex, [](float a, float c) { return a + c; });
+            return ex / sum;
+        });
+    }
+    if (col_sm) {  // softmax(dim = 1): over the agents, lane-local
+        float mx = -__builtin_inff(), sum = 0.0f;
+        each_row([&](float x, int) {
+            mx = fmaxf(mx, x);
+            return x;
+        });
+        each_row([&](float x, int) {
+            const float ex = expf(x - mx);
+            sum += ex;
+            return ex;
+        });
+        each_row([&](float x, int) { return x / sum; });
+    }
+    if (stdv > 0.0f) {  // th.normal(mean, std): mean + std * z (std = 0 keeps the means exactly)
+        const EnvKey key = env_key(seed, env_base + b);
+        constexpr float k2m24 = 5.9604644775390625e-08f;  // 2^-24
+        constexpr float k2pi = 6.283185307179586f;
+#pragma unroll
+        for (int i4 = 0; i4 < 16; ++i4) {  // rows 4 i4 .. 4 i4 + 3 of this column (rows >= n unused)
+            const u32x4 r = philox4x32_10(u32x4{(uint32_t)lane, (uint32_t)i4, kCtrBidsNoise, counter}, key.k0, key.k1);
+            const float u1a = (float)((r.x >> 8) + 1u) * k2m24, u2a = (float)(r.y >> 8) * k2m24;
+            const float u1b = (float)((r.z >> 8) + 1u) * k2m24, u2b = (float)(r.w >> 8) * k2m24;
+            const float ra = __builtin_sqrtf(-2.0f * __logf(u1a)), rb = __builtin_sqrtf(-2.0f * __logf(u1b));
+            const float z[4] = {ra * __cosf(k2pi * u2a), ra * __sinf(k2pi * u2a), rb * __cosf(k2pi * u2b),
+                                rb * __sinf(k2pi * u2b)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = 4 * i4 + k;
+                if (i < 32) rc.lo[i] = rc.lo[i] + stdv * z[k];
+                else rc.hi[i - 32] = rc.hi[i - 32] + stdv * z[k];
+            }
+        }
+    }
+    // the bids: the actions the batch stores (one 64-float row per store instruction); scipy
+    // maximize on the float64 bids: NaN or +inf (-inf once negated) is invalid
+    int bad = 0;
+    {
+        float *o = bids + b * o0 + (int64_t)lane * o2;
+        each_row([&](float x, int i) {
+            if (lv) o[i * o1] = x;
+            bad |= lv & ((x != x) | (x == __builtin_inff()));
+            return x;
+        });
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        rc.lo[i] = (lv && i < n) ? -rc.lo[i] : 0.0f;
+        rc.hi[i] = (lv && i + 32 < n) ? -rc.hi[i] : 0.0f;
+    }
+    int status = __builtin_amdgcn_readfirstlane(wave_or_i32(bad)) ? ASG_E_LSA_INVALID : ASG_OK;
+    int c4r[1] = {-1};
+    int nfast = 0, nsteps = 0;
+    bool done = false;
+    if (ASG_SAP_FAST && status == ASG_OK && n == m)
+        done = lsa_fast_reg64<decltype(rc), false>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
+    if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), false>(rc, n, m, c4r, &nsteps);
+    if (lane < n) assign[b * n + lane] = status == ASG_OK ? c4r[0] : -1;
+    if (status != ASG_OK && lane == 0) atomicCAS(env_err, 0, status);
+}
+
+hipError_t launch_bids_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, int row_sm, int col_sm,
+                              float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids,
+                              const int64_t os[3], int *assign, int *env_err, hipStream_t s) {
+    hipLaunchKernelGGL(bids_select_kernel, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n, m,
+                       row_sm, col_sm, stdv, seed, counter, env_base, bids, os[0], os[1], os[2], assign, env_err, B);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
 // beta_hat = beta - lambda * T_trans[prev_i, j] * (beta > 1e-12)   (mock :250-270)
 // ------------------------------------------------------------------------------------
 template <typename BT>

@@ -146,16 +146,18 @@ class AssignEnvBatch(MultiAgentEnv):
         self.k += 1
         return self.k >= self.T
 
-    def can_step_select(self, prefer=True, use_rnn=True):
+    def can_step_select(self, prefer=True, use_rnn=True, bids_ok=False):
         """Whether asg_rollout (env steps fused with the agent forward + epsilon-greedy
         selections, up to a whole episode per launch) takes this env: integer actions,
         16 <= m <= 256, n <= 256, L >= 1 -- with the GRU or the Linear RNNAgent -- and any
         benefit source: Philox bumps regenerated in the kernel, or the float32 table of the
         MT19937-compat / injected modes read for the lookahead rows.  `prefer` (kept for
         callers that ask whether it is also the faster schedule): measured on MI355X it is
-        wherever it applies."""
-        return (not self.bids_as_actions
-                and _lib.lib().asg_rollout_l2_slices(self.n, self.m, self.L, int(bool(use_rnn))) >= 0)
+        wherever it applies.  bids_ok: the caller's schedule is the bids one
+        (asg_step_forward + asg_bids_select), which takes bids_as_actions envs with m <= 64."""
+        if self.bids_as_actions and not (bids_ok and self.m <= 64):
+            return False
+        return _lib.lib().asg_rollout_l2_slices(self.n, self.m, self.L, int(bool(use_rnn))) >= 0
 
     @property
     def fused_reset_ok(self):
@@ -187,6 +189,21 @@ class AssignEnvBatch(MultiAgentEnv):
                    ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), _lib.stream_ptr(self.device))
         self.k += 1
         return q_out, h_out
+
+    def bids_select(self, q, out, row_softmax, col_softmax, std, seed, counter):
+        """asg_bids_select: the bids of every env from the agent outputs q ([E n, m] or [E, n, m]
+        float32) -- softmax over the tasks (row_softmax), over the agents (col_softmax), + N(0,
+        std) -- written to `out` [E, n, m] float32 (the batch's actions row), and their
+        LSA(maximize) assignments kept in the handle for the step on that row."""
+        E, n, m = self.num_envs, self.n, self.m
+        q = q.view(E, n, m)
+        if q.dtype != torch.float32 or out.dtype != torch.float32 or tuple(out.shape) != (E, n, m):
+            raise ValueError("bids_select: float32 q and out of shape [E, n, m]")
+        self._call("asg_bids_select", ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()),
+                   ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), int(bool(row_softmax)),
+                   int(bool(col_softmax)), float(std), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter),
+                   _lib.stream_ptr(self.device))
+        return out
 
     def rollout(self, batch, ts, steps, agent, hidden_state, epsilon, seed, counter, status, select_first=True,
                 select_last=False, reset=False):

@@ -128,7 +128,8 @@ class GpuVecRunner:
     def select_into_batch(self, t, test_mode=False):
         """mac.select_actions at t_ep = t, actions written into the batch row t (in place
         when the selector supports `out`, else through EpisodeBatch.update)."""
-        row = self.batch["actions"][:, t, :, 0] if not self.env.bids_as_actions else None
+        # the actions row: int64 [B, n]; bids_as_actions: the float32 bids [B, n, m]
+        row = self.batch["actions"][:, t] if self.env.bids_as_actions else self.batch["actions"][:, t, :, 0]
         actions = self.mac.select_actions(self.batch, t_ep=t, t_env=self.t_env, test_mode=test_mode, out=row)
         if row is None or actions is not row:
             self.batch.update({"actions": actions}, ts=t, mark_filled=False, preprocess=False)
