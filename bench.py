@@ -533,7 +533,9 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
                 state["mode"] = "random_episode" if fused_sched else None
             else:
                 state["mode"] = mac.fused_mode(env, runner.batch, runner.t_env)
-        state["fuse_reset"] = state["mode"] in ("episode", "random_episode") and bool(a.fuse_reset)
+        state["fuse_reset"] = bool(a.fuse_reset) and (
+            state["mode"] in ("episode", "random_episode")
+            or (state["mode"] == "step_q" and mac.fused_reset_ok(env)))  # asg_reset_forward
         if not state["fuse_reset"]:
             env.reset(runner.batch, ts=0)
 
@@ -570,6 +572,9 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
             fused = state["mode"] in ("step", "step_q")
             if selector == "random":
                 timed(sel_pairs, lambda: env.random_actions(runner.batch, ts=t))
+            elif t == 0 and state.pop("fuse_reset", False):
+                # step_q: the reset + the forward on its row (asg_reset_forward), then the selector
+                timed(sel_pairs, lambda: mac.fused_reset_select(env, runner.batch, runner.t_env))
             elif not state["selected"]:
                 timed(sel_pairs, lambda: runner.select_into_batch(t))
             if fused and t + 1 < a.T:
@@ -625,7 +630,9 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
             if state.get("mode") == "step_q":
                 if state["t"] + 1 >= a.T:
                     new_episode()
-                if not state["selected"]:
+                if state["t"] == 0 and state.pop("fuse_reset", False):
+                    mac.fused_reset_select(env, runner.batch, runner.t_env)
+                elif not state["selected"]:
                     runner.select_into_batch(state["t"])
                 sel_obj.count_steps = torch.zeros(E, dtype=torch.int32, device=dev)
                 mac.fused_step_select(env, runner.batch, state["t"], runner.t_env)

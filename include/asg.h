@@ -399,6 +399,15 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
 int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream);
+/* asg_reset then the agent forward on the reset row ts (Q to q_out, the hidden state to h_out), in
+ * one launch: the runner's env.reset() + mac.forward(0) of a selector acting on Q outside the
+ * kernel (runners/episode_runner.py:49-62 with sap_selectors.py:52-98 / bet_selectors.py).  The
+ * reset row is generated, stored and consumed on chip.  Philox bump / dense benefits and the
+ * MT19937 mode (its draw kernels first, as asg_reset_rollout); not an injected table under
+ * Philox (asg_reset).  Same batch, Q and hidden state as asg_reset + asg_rnn_agent_forward. */
+int asg_reset_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream);
 /* bids_as_actions with the ContinuousActionSelector (config/algs/ippo_sap.yaml), replacing the
  * per-env chain BasicMAC.forward's pi_logits softmax (controllers/basic_controller.py:37-46) ->
  * ContinuousActionSelector.select_action (action_selectors/bet_selectors.py:12-20: softmax over

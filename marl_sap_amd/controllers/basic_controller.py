@@ -131,28 +131,44 @@ class BasicMAC:
         hidden state advances as select_actions would advance it.  SAP selector: the kernel
         ends with the agent's Q (kept in one reused buffer), which the selector's kernel turns
         into the actions of row t_ep + 1, written in place."""
-        if self._fused_bids_ok():
+        if self._fused_bids_ok() or self._fused_q_ok():
             q, self.hidden_states = env.step_forward(ep_batch, t_ep, self.selector_agent, self.hidden_states,
                                                      q_out=getattr(self, "_q_buf", None))
-            self._q_buf = q
-            self.action_selector.fused_bids(q.view(ep_batch.batch_size, self.n, -1), ep_batch["actions"][:, t_ep + 1],
-                                            t_env, test_mode, row_softmax=self.agent_output_type == "pi_logits")
-            return
-        if self._fused_q_ok():
-            q, self.hidden_states = env.step_forward(ep_batch, t_ep, self.selector_agent, self.hidden_states,
-                                                     q_out=getattr(self, "_q_buf", None))
-            self._q_buf = q
-            row = ep_batch["actions"][:, t_ep + 1, :, 0]
-            acts = self.action_selector.select_action(q.view(ep_batch.batch_size, self.n, -1),
-                                                      ep_batch["avail_actions"][:, t_ep + 1], t_env,
-                                                      test_mode=test_mode, beta=ep_batch["beta"][:, t_ep + 1],
-                                                      out=row)
-            if acts is not row:
-                ep_batch.update({"actions": acts}, ts=t_ep + 1, mark_filled=False, preprocess=False)
+            self._select_on_q(q, ep_batch, t_ep + 1, t_env, test_mode)
             return
         eps, seed, counter, status, _base = self.action_selector.fused_params(t_env, test_mode, env.device)
         self.hidden_states = env.step_select(ep_batch, t_ep, self.selector_agent, self.hidden_states, eps, seed,
                                              counter, status)
+
+    def _select_on_q(self, q, ep_batch, t, t_env, test_mode):
+        """The step_q schedule's selection on the agent outputs q [B n, m] of row t (kept in one
+        reused buffer): SAP -- its noise + LSA kernel, actions into the batch row in place; bids --
+        asg_bids_select (the bids row and its LSA)."""
+        self._q_buf = q
+        B = ep_batch.batch_size
+        if self._fused_bids_ok():
+            self.action_selector.fused_bids(q.view(B, self.n, -1), ep_batch["actions"][:, t], t_env, test_mode,
+                                            row_softmax=self.agent_output_type == "pi_logits")
+            return
+        row = ep_batch["actions"][:, t, :, 0]
+        acts = self.action_selector.select_action(q.view(B, self.n, -1), ep_batch["avail_actions"][:, t], t_env,
+                                                  test_mode=test_mode, beta=ep_batch["beta"][:, t], out=row)
+        if acts is not row:
+            ep_batch.update({"actions": acts}, ts=t, mark_filled=False, preprocess=False)
+
+    def fused_reset_ok(self, env):
+        """The step_q schedule may fold env.reset() into the forward on the reset row
+        (asg_reset_forward): the env's reset runs inside a launch (Philox bump / dense, MT19937)."""
+        return (getattr(env, "fused_reset_ok", False) and hasattr(env, "reset_forward")
+                and (self._fused_bids_ok() or self._fused_q_ok()))
+
+    def fused_reset_select(self, env, ep_batch, t_env, test_mode=False):
+        """env.reset() + select_actions(0) on the step_q schedule: the reset and the agent forward
+        on the reset row in one launch (asg_reset_forward), then the selector's kernel on its Q --
+        the batch, hidden state and actions of the separate calls."""
+        q, self.hidden_states = env.reset_forward(ep_batch, 0, self.selector_agent, self.hidden_states,
+                                                  q_out=getattr(self, "_q_buf", None))
+        self._select_on_q(q, ep_batch, 0, t_env, test_mode)
 
     def fused_episode(self, env, ep_batch, t_env, test_mode=False, reset=False):
         """select_actions(0), then env.step(t) + select_actions(t + 1) for the whole episode

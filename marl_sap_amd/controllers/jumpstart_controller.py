@@ -76,6 +76,15 @@ class JumpstartMAC(BasicMAC):
         acts = self.jumpstart_action_selector.select_action(ep_batch[:, t_ep + 1])
         ep_batch.update({"actions": acts}, ts=t_ep + 1, mark_filled=False, preprocess=False)
 
+    def fused_reset_select(self, env, ep_batch, t_env, test_mode=False):
+        """env.reset() + select_actions(0): the fused reset + forward when the flip for row 0 picks
+        the RL branch, else env.reset then the jumpstart selector."""
+        if not self._coin(t_env, test_mode):
+            return super().fused_reset_select(env, ep_batch, t_env, test_mode)
+        env.reset(ep_batch, ts=0)
+        acts = self.jumpstart_action_selector.select_action(ep_batch[:, 0])
+        ep_batch.update({"actions": acts}, ts=0, mark_filled=False, preprocess=False)
+
     def forward(self, ep_batch, t, test_mode=False, action_selection_mode=False):
         agent_inputs = self._build_inputs(ep_batch, t)
         net = self.selector_agent if action_selection_mode else self.agent

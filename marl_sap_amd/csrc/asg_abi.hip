@@ -656,7 +656,9 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     if (reset && st.benefit_mode == ASG_BENEFIT_INJECTED && !h->table_ready)
         return fail(h, ASG_E_STATE, "benefit_mode=injected needs asg_set_benefits before reset");
     const int k0 = reset ? 0 : h->k;
-    if (steps < 1 || k0 + steps > st.T)
+    // steps = 0: asg_reset_forward (the reset and the forward on its row, Q out)
+    const bool reset_forward = steps == 0 && reset && q_out;
+    if ((steps < 1 && !reset_forward) || k0 + steps > st.T)
         return fail(h, ASG_E_STATE, "asg_rollout: steps must be >= 1 and stay within the episode (k + steps <= T)");
     if (select_first && k0 != 0)
         return fail(h, ASG_E_STATE, "asg_rollout: select_first selects on the reset row (k == 0 only)");
@@ -699,7 +701,7 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     // as asg_reset: a fresh Philox key per episode, committed once the launch succeeded
     asg::EnvState lst = h->st;
     if (reset && h->has_reset) lst.episode += 1;
-    if (st.bids && !bids_ready(h, b, ts)) {  // the bids of row ts not solved by asg_bids_select
+    if (st.bids && !reset && !bids_ready(h, b, ts)) {  // the bids of row ts not solved by asg_bids_select
         hipError_t e0 = asg::launch_bids_assign(*b, st, ts, s);
         if (e0 != hipSuccess) return hip_fail(h, e0, "asg_step_forward (bids LSA)");
     }
@@ -743,6 +745,14 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
                     int32_t *status, void *hip_stream) {
     return asg_rollout(h, b, ts, 1, 0, 1, packed, b1, b_ih, b_hh, b2, K, hidden, 1, h_in, h_stride, h_out, epsilon,
                        seed, counter, status, hip_stream);
+}
+
+int asg_reset_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream) {
+    if (!q_out) return fail(h, ASG_E_INVALID_ARG, "asg_reset_forward: NULL q_out");
+    return rollout_impl(h, b, ts, 0, 1, 1, 1, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in, h_stride, h_out,
+                        0.0, 0, 0, nullptr, hip_stream, q_out);
 }
 
 int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,

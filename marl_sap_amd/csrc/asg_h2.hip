@@ -1870,7 +1870,11 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.table32 = tab ? st.table32 : nullptr;
     // the table modes' reset in this launch: the MT19937 draws ran before it (asg_reset_rollout)
     // Q output: one transition and the forward of the row after it (asg_step_forward)
-    if (Q && (steps != 1 || select_first || !select_last || reset)) return hipErrorInvalidValue;
+    // or (asg_reset_forward) the envs' reset and the forward on the reset row, no transition
+    const bool q_step = steps == 1 && !select_first && select_last && !reset;
+    const bool q_reset = steps == 0 && select_first && select_last && reset;
+    if (Q && !q_step && !q_reset) return hipErrorInvalidValue;
+    if (!Q && steps < 1) return hipErrorInvalidValue;
     ra.Q = Q;
     ra.assign = st.bids ? st.assign : nullptr;
     if (st.bids && !Q) return hipErrorInvalidValue;  // bids: asg_step_forward only

@@ -175,16 +175,30 @@ class AssignEnvBatch(MultiAgentEnv):
         return self.rollout(batch, ts, 1, agent, hidden_state, epsilon, seed, counter, status, select_first=False,
                             select_last=True)
 
+    def reset_forward(self, batch, ts, agent, hidden_state, q_out=None):
+        """asg_reset_forward: reset() and the agent forward on the reset row ts in one kernel
+        (the row is written to the batch and consumed on chip) -- env.reset + mac.forward(0) for a
+        selector acting on Q outside the kernel.  Needs fused_reset_ok.  Returns (Q [E n, m]
+        float32, the new hidden state [E n, hidden])."""
+        q_out, h_out, args = self._forward_args(batch, agent, hidden_state, q_out)
+        self._call("asg_reset_forward", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
+                   ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), _lib.stream_ptr(self.device))
+        self.k = 0
+        return q_out, h_out
+
+    def _forward_args(self, batch, agent, hidden_state, q_out):
+        args = agent.step_select_args(hidden_state, batch["obs"].shape[-1], self.device, self.num_envs * self.n)
+        R = self.num_envs * self.n
+        if q_out is None or q_out.dtype != torch.float32 or q_out.numel() != R * self.m or not q_out.is_contiguous():
+            q_out = torch.empty((R, self.m), dtype=torch.float32, device=self.device)
+        return q_out, args[-1], args
+
     def step_forward(self, batch, ts, agent, hidden_state, q_out=None):
         """asg_step_forward: asg_step at row ts and the agent forward on row ts + 1 in one
         kernel (the observation row is written to the batch and consumed on chip) -- env.step
         + mac.forward for a selector that acts on Q outside the kernel (SAP).  Returns
         (Q [E n, m] float32, the new hidden state [E n, hidden])."""
-        args = agent.step_select_args(hidden_state, batch["obs"].shape[-1], self.device, self.num_envs * self.n)
-        h_out = args[-1]
-        R = self.num_envs * self.n
-        if q_out is None or q_out.dtype != torch.float32 or q_out.numel() != R * self.m or not q_out.is_contiguous():
-            q_out = torch.empty((R, self.m), dtype=torch.float32, device=self.device)
+        q_out, h_out, args = self._forward_args(batch, agent, hidden_state, q_out)
         self._call("asg_step_forward", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
                    ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), _lib.stream_ptr(self.device))
         self.k += 1

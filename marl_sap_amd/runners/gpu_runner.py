@@ -110,8 +110,12 @@ class GpuVecRunner:
             # the env reset runs in the episode's launch (asg_reset_rollout)
             self.mac.fused_episode(self.env, self.batch, self.t_env, test_mode, reset=True)
         else:
-            self.env.reset(self.batch, ts=0)
-            self.select_into_batch(0, test_mode)
+            if mode == "step_q" and self.mac.fused_reset_ok(self.env):
+                # the reset and the forward on its row in one launch, then the selector's kernel
+                self.mac.fused_reset_select(self.env, self.batch, self.t_env, test_mode)
+            else:
+                self.env.reset(self.batch, ts=0)
+                self.select_into_batch(0, test_mode)
             for t in range(self.T):
                 if mode in ("step", "step_q") and t + 1 < self.T:
                     self.mac.fused_step_select(self.env, self.batch, t, self.t_env, test_mode)

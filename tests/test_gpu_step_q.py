@@ -145,6 +145,48 @@ def test_step_forward_equals_step_then_forward():
         assert torch.equal(ra, rb)
 
 
+def test_reset_forward_equals_reset_then_forward():
+    """asg_reset_forward (the step_q schedule's reset + forward on the reset row, one launch):
+    the batch, Q rows and hidden state of asg_reset followed by the agent kernel, bitwise --
+    Philox bump / dense benefits and the MT19937 mode, two episodes (the second reset's key)."""
+    from marl_sap_amd.components import EpisodeBatch
+    from marl_sap_amd.envs import AssignEnvBatch
+    from marl_sap_amd.modules.agents import RNNFusedAgent
+    for n, m, L, use_rnn, benefits, rng in ((64, 64, 3, True, "bump", "philox"), (20, 25, 3, False, "bump", "philox"),
+                                            (32, 48, 2, True, "dense", "philox"), (20, 25, 3, False, "bump", "mt19937")):
+        T, E = 4, 6
+        outs = []
+        for fused in (True, False):
+            env = AssignEnvBatch(n, m, T, L, 0.5, seed=2, num_envs=E, device=DEV, benefits=benefits, rng=rng)
+            assert env.fused_reset_ok
+            b = EpisodeBatch(env.scheme, {"agents": n}, E, T + 1, preprocess=env.preprocess, device=DEV,
+                             time_major=True)
+            torch.manual_seed(4)
+            agent = RNNFusedAgent(m * (L + 1), SimpleNamespace(hidden_dim=64, use_rnn=use_rnn, m=m)).to(DEV)
+            rec = []
+            with torch.no_grad():
+                for ep in range(2):
+                    h = agent.init_hidden().unsqueeze(0).expand(E, n, -1)
+                    if fused:
+                        q, h = env.reset_forward(b, 0, agent, h)
+                    else:
+                        env.reset(b, ts=0)
+                        q, h = agent(b["obs"][:, 0].reshape(E * n, -1), h)
+                    rec.append((q.cpu().clone(), h.cpu().clone(),
+                                {k: v.cpu().clone() for k, v in b.data.transition_data.items()}))
+                    assert env.k == 0
+                    # one step so the handle advances, then a new episode
+                    b["actions"][:, 0, :, 0] = torch.arange(n, device=DEV).remainder(m).expand(E, n)
+                    env.step(b, ts=0)
+            env.sync()
+            outs.append(rec)
+            env.close()
+        for (qa, ha, fa), (qb, hb, fb) in zip(*outs):
+            assert torch.equal(qa, qb) and torch.equal(ha, hb), (n, m, benefits, rng)
+            for k in fa:
+                assert torch.equal(fa[k], fb[k]), (n, m, benefits, rng, k)
+
+
 def test_sap_select_into_equals_float_output():
     """asg_sap_select_into: the int64 ids of asg_sap_select's float output, -1 rows for a NaN
     env, and its per-env status word min-accumulated over calls."""
