@@ -744,21 +744,29 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
                 const int cend = min(n, c0 + kWave);
                 double2 mine = make_double2(0.0, 0.0);  // lane i - c0: agent i's bump on task j
                 // speculative reads: every remaining agent of the chunk tests its r as if no bump
-                // came before it (two words each); the first agent with r > 0.75 is exact, it
-                // consumes four more words, and the agents after it test again from there
+                // came before it (two words each) and reads the four words its center and spread
+                // would take (one LDS round trip for all six); the first agent with r > 0.75 is
+                // exact, its bump is broadcast from its lane, and the agents after it test again
+                // four words further on
                 for (int i = c0; i < cend;) {
                     const int rows = cend - i;
-                    const int w = 2 * lane;  // < 128 words ahead: inside the two blocks
-                    const double r = lane < rows ? MtWave2::dbl(mt.word(w), mt.word(w + 1)) : 0.0;
+                    const int w = 2 * lane;  // < 134 words ahead: inside the two blocks
+                    uint32_t wd[6];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) wd[q] = mt.word(w + q);
+                    const double r = lane < rows ? MtWave2::dbl(wd[0], wd[1]) : 0.0;
                     const uint64_t act = __ballot(lane < rows && r > 0.75);
                     if (act == 0) {
                         mt.advance(2 * rows);
                         break;
                     }
                     const int k = __builtin_amdgcn_readfirstlane(__builtin_ctzll(act));
-                    mt.advance(2 * k + 2);
-                    const double center = mt.uniform(0.0, (double)T);
-                    const double spread = mt.uniform(wmin, wmax);  // s2 = bump_s2(spread) in mt_table_kernel
+                    // numpy's uniform(lo, hi) = lo + (hi - lo) * random_sample(), as MtWave2::uniform
+                    const double center = 0.0 + ((double)T - 0.0) * MtWave2::dbl(
+                        __builtin_amdgcn_readlane(wd[2], k), __builtin_amdgcn_readlane(wd[3], k));
+                    const double spread = wmin + (wmax - wmin) * MtWave2::dbl(  // s2 = bump_s2(spread) in mt_table_kernel
+                        __builtin_amdgcn_readlane(wd[4], k), __builtin_amdgcn_readlane(wd[5], k));
+                    mt.advance(2 * k + 6);
                     if (lane == i + k - c0) mine = make_double2(center, scale == 10.0 ? -spread : spread);
                     i += k + 1;
                 }
