@@ -645,6 +645,15 @@ __device__ __forceinline__ void mt_temper(const uint32_t *k, uint32_t *o) {
 // shift / mask steps) -- so a draw wave holds only the two raw blocks, 5 KiB of LDS instead of
 // 10 (29 draw waves per CU instead of 16).  Measured slower (r5 A/B, compat leg): 0.946-0.954 vs
 // 0.892-0.900 ms/step -- the speculative reads temper every word they test; off
+// Timing-only switch (WRONG results; refused without -DASG_TIMING_EXPERIMENTS): ASG_MT_XSKIP bits
+// 1 = no twist of the next block at a shift (the tempered words go stale), 2 = no speculative
+// bump loop (each task's agents consumed as if none had a bump), 4 = no permutation
+#if defined(ASG_MT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
+#error "ASG_MT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
+#endif
+#ifndef ASG_MT_XSKIP
+#define ASG_MT_XSKIP 0
+#endif
 #ifndef ASG_MT_TEMPER_ON_READ
 #define ASG_MT_TEMPER_ON_READ 0
 #endif
@@ -676,8 +685,10 @@ struct MtWave2 {
             if (!ASG_MT_TEMPER_ON_READ) out[i] = out[kMtN + i];
         }
         wave_sync();
-        mt_twist_inplace(key2);
-        if (!ASG_MT_TEMPER_ON_READ) mt_temper(key2, out + kMtN);
+        if (!(ASG_MT_XSKIP & 1)) {
+            mt_twist_inplace(key2);
+            if (!ASG_MT_TEMPER_ON_READ) mt_temper(key2, out + kMtN);
+        }
         pos -= kMtN;
     }
     __device__ uint32_t word(int k) const {  // k < 624 (per lane: the speculative reads)
@@ -748,7 +759,8 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
                 // would take (one LDS round trip for all six); the first agent with r > 0.75 is
                 // exact, its bump is broadcast from its lane, and the agents after it test again
                 // four words further on
-                for (int i = c0; i < cend;) {
+                if (ASG_MT_XSKIP & 2) mt.advance(2 * (cend - c0));
+                for (int i = (ASG_MT_XSKIP & 2) ? cend : c0; i < cend;) {
                     const int rows = cend - i;
                     const int w = 2 * lane;  // < 134 words ahead: inside the two blocks
                     uint32_t wd[6];
@@ -777,7 +789,7 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
     // prev_assigns = choice(m, n, replace=False) = permutation(m)[:n]  (mock :105)
     for (int j = lane; j < m; j += kWave) perm[j] = j;
     wave_sync();
-    for (int i = m - 1; i >= 1; --i) {
+    for (int i = (ASG_MT_XSKIP & 4) ? 0 : m - 1; i >= 1; --i) {
         const int jj = (int)mt.interval((uint32_t)i);
         if (lane == 0) {
             const int t = perm[i];
