@@ -732,6 +732,17 @@ struct MtWave2 {
 // (0, 0) for no bump -- in par [E][m][n] (draw order: one coalesced 1 KiB store per 64 agents
 // of a task); mt_table_kernel then writes the table from them with whole-row stores.
 // construct: also replay the throwaway __init__ table draw (mock :34) first.
+// bumps resolved per LDS round trip of the draw loop's bump search
+#ifndef ASG_MT_BUMPS
+#define ASG_MT_BUMPS 8
+#endif
+constexpr int kMtBumps = ASG_MT_BUMPS;
+// numpy's random_sample() from words (a, b) is ((a >> 5) 2^26 + (b >> 6)) 2^-53 exactly: r > 0.75
+// (mock :283) is an integer test on the 53-bit numerator against 3 2^51
+__device__ __forceinline__ bool mt_r_above_075(uint32_t a, uint32_t b) {
+    const uint32_t hi = a >> 5, lo = b >> 6;
+    return hi > (3u << 25) || (hi == (3u << 25) && lo != 0u);
+}
 __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvState st, double2 *par, bool construct,
                                                        bool generate) {
     extern __shared__ uint32_t s_mt[];
@@ -750,38 +761,59 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
         const double wmin = pass == 0 ? st.wmin_init : st.wmin;
         const double wmax = pass == 0 ? st.wmax_init : st.wmax;
         for (int j = 0; j < m; ++j) {
-            const double scale = (mt.next() & 3u) == 3u ? 10.0 : 1.0;
+            // benefit_scale = choice([1, 1, 1, 10]): one word (randint(0, 4), mask 3), read with the
+            // first chunk's words (the chunk's offsets start after it: o0)
+            const double scale = (mt.word(0) & 3u) == 3u ? 10.0 : 1.0;
+            int o0 = 1;
             for (int c0 = 0; c0 < n; c0 += kWave) {
-                const int cend = min(n, c0 + kWave);
-                double2 mine = make_double2(0.0, 0.0);  // lane i - c0: agent i's bump on task j
-                // speculative reads: every remaining agent of the chunk tests its r as if no bump
-                // came before it (two words each) and reads the four words its center and spread
-                // would take (one LDS round trip for all six); the first agent with r > 0.75 is
-                // exact, its bump is broadcast from its lane, and the agents after it test again
-                // four words further on
-                if (ASG_MT_XSKIP & 2) mt.advance(2 * (cend - c0));
-                for (int i = (ASG_MT_XSKIP & 2) ? cend : c0; i < cend;) {
-                    const int rows = cend - i;
-                    const int w = 2 * lane;  // < 134 words ahead: inside the two blocks
-                    uint32_t wd[6];
+                const int rows = min(n, c0 + kWave) - c0;
+                // 1. which agents of the chunk have a bump (r > 0.75): lane l tests agent a0 + l with
+                //    its two r words at o + 2 l + 4 s, s = the bumps before it among a0.., s <
+                //    kMtBumps -- all read in one LDS round trip, the first hit at s = 0 is exact, the
+                //    first after it at s = 1, ... (integer tests, no float64); no stream advance yet
+                uint64_t bumps = 0;
+                int o = o0, a0 = 0;  // o0 + the words consumed by agents 0 .. a0 - 1 of the chunk
+                if (ASG_MT_XSKIP & 2) a0 = rows;
+                while (a0 < rows) {
+                    uint32_t rw[2 * kMtBumps];
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) wd[q] = mt.word(w + q);
-                    const double r = lane < rows ? MtWave2::dbl(wd[0], wd[1]) : 0.0;
-                    const uint64_t act = __ballot(lane < rows && r > 0.75);
-                    if (act == 0) {
-                        mt.advance(2 * rows);
-                        break;
+                    for (int q = 0; q < 2 * kMtBumps; ++q) rw[q] = mt.word(o + 2 * lane + 4 * (q >> 1) + (q & 1));
+                    int lo = 0, found = 0;
+                    bool done = false;
+#pragma unroll
+                    for (int sb = 0; sb < kMtBumps; ++sb) {
+                        const uint64_t act = __ballot(lane + a0 < rows && lane >= lo && mt_r_above_075(rw[2 * sb], rw[2 * sb + 1]));
+                        if (act == 0) {
+                            done = true;
+                            break;
+                        }
+                        const int k = __builtin_amdgcn_readfirstlane(__builtin_ctzll(act));
+                        bumps |= 1ull << (a0 + k);
+                        lo = k + 1;
+                        found = sb + 1;
                     }
-                    const int k = __builtin_amdgcn_readfirstlane(__builtin_ctzll(act));
-                    // numpy's uniform(lo, hi) = lo + (hi - lo) * random_sample(), as MtWave2::uniform
-                    const double center = 0.0 + ((double)T - 0.0) * MtWave2::dbl(
-                        __builtin_amdgcn_readlane(wd[2], k), __builtin_amdgcn_readlane(wd[3], k));
-                    const double spread = wmin + (wmax - wmin) * MtWave2::dbl(  // s2 = bump_s2(spread) in mt_table_kernel
-                        __builtin_amdgcn_readlane(wd[4], k), __builtin_amdgcn_readlane(wd[5], k));
-                    mt.advance(2 * k + 6);
-                    if (lane == i + k - c0) mine = make_double2(center, scale == 10.0 ? -spread : spread);
-                    i += k + 1;
+                    if (done) {  // agents a0 .. rows - 1: two words each, four more per bump
+                        o += 2 * (rows - a0) + 4 * found;
+                        a0 = rows;
+                    } else {
+                        o += 2 * lo + 4 * found;
+                        a0 += lo;
+                    }
                 }
+                // 2. every bump's center and spread read by its own lane: agent l's words start at
+                //    o0 + 2 l + 4 (bumps before l); center ~ U(0, T), spread ~ U(wmin, wmax) (numpy's
+                //    uniform(lo, hi) = lo + (hi - lo) * random_sample(), as MtWave2::uniform)
+                double2 mine = make_double2(0.0, 0.0);  // agent c0 + lane's bump on task j
+                if ((bumps >> lane) & 1) {
+                    const int sl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bumps >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bumps, 0u));
+                    const int w = o0 + 2 * lane + 4 * sl + 2;
+                    const double center = 0.0 + ((double)T - 0.0) * MtWave2::dbl(mt.word(w), mt.word(w + 1));
+                    const double spread = wmin + (wmax - wmin) * MtWave2::dbl(mt.word(w + 2), mt.word(w + 3));
+                    mine = make_double2(center, scale == 10.0 ? -spread : spread);  // s2 in mt_table_kernel
+                }
+                mt.advance(o);
+                o0 = 0;
                 if (pass == 1 && pe && c0 + lane < n) pe[(int64_t)j * n + c0 + lane] = mine;
             }
         }
@@ -852,12 +884,23 @@ __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvSt
                 for (int tt = 0; tt < tg; ++tt) s_tile[tt * ne + id] = (float)mt_par_value(p, t0 + tt);
             }
             __syncthreads();
-            // whole rows out; the tile is left zeroed for the next group
-            for (int tt = 0; tt < tg; ++tt)
-                for (int id = threadIdx.x; id < ne; id += blockDim.x) {
-                    o[(int64_t)(t0 + tt) * nm + id] = s_tile[tt * ne + id];
-                    s_tile[tt * ne + id] = 0.f;
+            // whole rows out (16 B per lane when the rows allow), the tile left zeroed for the next group
+            if ((ne & 3) == 0 && (nm & 3) == 0 && ((R * m) & 3) == 0) {  // (the tile sits at 20 R m bytes)
+                for (int tt = 0; tt < tg; ++tt) {
+                    float4 *o4 = reinterpret_cast<float4 *>(o + (int64_t)(t0 + tt) * nm);
+                    float4 *s4 = reinterpret_cast<float4 *>(s_tile + tt * ne);
+                    for (int id = threadIdx.x; id < (ne >> 2); id += blockDim.x) {
+                        o4[id] = s4[id];
+                        s4[id] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
+            } else {
+                for (int tt = 0; tt < tg; ++tt)
+                    for (int id = threadIdx.x; id < ne; id += blockDim.x) {
+                        o[(int64_t)(t0 + tt) * nm + id] = s_tile[tt * ne + id];
+                        s_tile[tt * ne + id] = 0.f;
+                    }
+            }
             __syncthreads();
         }
     }
