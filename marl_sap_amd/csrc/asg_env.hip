@@ -846,7 +846,13 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
 #define ASG_TABLE_TG 4
 #endif
 constexpr int kTableTG = ASG_TABLE_TG;
-static int mt_table_rows(int m) { return m >= 1024 ? 1 : (1024 / m < 16 ? 1024 / m : 16); }
+// agents per chunk of the table kernel (rows * m <= 1024 floats per time slice of the tile)
+#ifndef ASG_TABLE_ROWS
+#define ASG_TABLE_ROWS 16
+#endif
+static int mt_table_rows(int m) {
+    return m >= 1024 ? 1 : (1024 / m < ASG_TABLE_ROWS ? 1024 / m : ASG_TABLE_ROWS);
+}
 static size_t mt_table_lds(int R, int m) {
     return (sizeof(double2) + sizeof(int) + sizeof(float) * kTableTG) * (size_t)R * m;
 }
