@@ -773,7 +773,8 @@ def main():
     value = G * a.steps / res["elapsed"]
     kern_ms, sel_ms = res["kern_ms"], res["sel_ms"]
     if res.get("mode") == "step_q" and res.get("step_forward_ms"):
-        roof = fused_roofline(a, E, res["step_forward_ms"], use_rnn=a.use_rnn, q_out=True)
+        bids = a.selector == "bids"
+        roof = fused_roofline(a, E, res["step_forward_ms"], use_rnn=a.use_rnn and not bids, q_out=True, bids=bids)
     elif res.get("mode") == "random_episode" and res.get("fused_ms"):
         roof = random_roofline(a, E, res["fused_ms"], res_resets(res))
     elif res.get("fused_ms"):
@@ -980,7 +981,8 @@ def main():
         ra = agent_roofline(a, E, sel_ms, "asg::rnn_agent_h2_kernel (forward + eps-greedy)"
                             if a.agent in FUSED_AGENTS else "torch RNNAgent + asg_epsilon_greedy")
     if rank == 0:
-        sel_name = {"eps": "epsilon-greedy", "sap": "SAP", "random": "random"}[a.selector]
+        sel_name = {"eps": "epsilon-greedy", "sap": "SAP", "random": "random",
+                    "bids": "continuous (bids_as_actions, ippo_sap.yaml)"}[a.selector]
         line = {
             "metric": f"env steps/sec (whole node), {a.n}-agent assignment env, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": a.steps,
@@ -995,6 +997,11 @@ def main():
                        "parallelism": f"env-sharded x{world} (gather of returns per episode)"},
             "roofline": roof,
             "kernels_ms": {**(sap_kernels(res) if a.selector == "sap" else {
+                               "step_forward": round(res["step_forward_ms"], 4) if res.get("step_forward_ms") else None,
+                               "bids_select": round(res["lsa_ms"], 4) if res.get("lsa_ms") else None,
+                               "fused_step_total": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
+                               "env_step": round(kern_ms, 4) if kern_ms else None,
+                               "select": round(sel_ms, 4) if sel_ms else None} if a.selector == "bids" else {
                                "fused_rollout_per_step": round(res["fused_ms"], 4) if res.get("fused_ms") else None,
                                "env_step": round(kern_ms, 4) if kern_ms else None,
                                "select": round(sel_ms, 4) if sel_ms else None}),

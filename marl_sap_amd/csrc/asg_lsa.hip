@@ -289,8 +289,15 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
 // actions row -> LSA(bids, maximize) = the env's assignments for its next step
 // (mock_constellation_env.py:121-122), kept in the handle for asg_step / asg_step_forward.
 // ------------------------------------------------------------------------------------
-// (110 VGPRs, 4 waves per SIMD: the 5-wave budget of sap_select_kernel spills the transforms)
+// ASG_BIDS_WAVES: waves per SIMD the kernel is compiled for (0: the register allocator's choice,
+// 110 VGPRs at 4 waves; 5: 96 VGPRs with 26 spilled, 0.489 vs 0.498 ms, r5 A/B)
+#ifndef ASG_BIDS_WAVES
+#define ASG_BIDS_WAVES 5
+#endif
 __global__ void __launch_bounds__(64 * kLsaWpb)
+#if ASG_BIDS_WAVES
+__attribute__((amdgpu_waves_per_eu(ASG_BIDS_WAVES)))
+#endif
 bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, int m, int row_sm, int col_sm,
                    float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids, int64_t o0,
                    int64_t o1, int64_t o2, int *assign, int *env_err, int64_t B) {
@@ -318,10 +325,12 @@ bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, in
         for (int i = 0; i < 32; ++i)
             if (i + 32 < n) rc.hi[i] = f(rc.hi[i], i + 32);
     };
+    // exp as v_exp_f32 of x log2(e) (x = y - max <= 0: relative error <= |x| 2^-24 + 1 ulp; torch's
+    // expf is within 1 ulp): the accurate expf unrolled over the 64 rows spilled at any budget
     if (row_sm) {  // softmax(dim = -1) of each agent's row: exp(x - max) / sum, as torch
         each_row([&](float x, int) {
             const float mx = wave_allreduce(lv ? x : -__builtin_inff(), [](float a, float c) { return fmaxf(a, c); });
-            const float ex = lv ? expf(x - mx) : 0.0f;
+            const float ex = lv ? __expf(x - mx) : 0.0f;
             const float sum = wave_allreduce(ex, [](float a, float c) { return a + c; });
             return ex / sum;
         });
@@ -333,7 +342,7 @@ bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, in
             return x;
         });
         each_row([&](float x, int) {
-            const float ex = expf(x - mx);
+            const float ex = __expf(x - mx);
             sum += ex;
             return ex;
         });
