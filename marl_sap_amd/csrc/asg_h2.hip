@@ -197,7 +197,10 @@ constexpr int kH2SxInit = 11;                   // fc1 input scale of the first 
 // column gather (zeros); bit 4: fc1 slices that live in L2 read LDS slot 0 instead; bit 8:
 // h_t not loaded (constants); bit 16: h' not stored; bit 32: the tile's row stores go to a
 // small region that stays in L2 (env e & 7, batch row 1): same instructions, no HBM writes;
-// bit 64: the tiles' bump parameters from a cheap hash instead of Philox (VALU)
+// bit 64: the tiles' bump parameters from a cheap hash instead of Philox (VALU); bit 256: no env
+// transition between the steps (rewards, returns, the transition's rows); bit 512: the return
+// not summed in agent order (one readlane); bit 1024: the transition's rewards without the bump
+// (Philox + float64 exp: beta = 0)
 #if defined(ASG_ROLLOUT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
 #error "ASG_ROLLOUT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
 #endif
@@ -1083,9 +1086,23 @@ __host__ __device__ inline int rollout_scratch_bytes(int n, int m) {
     return (40 + 4 * rollout_mp(m) + 4 * rollout_np(n) + 15) / 16 * 16;
 }
 
+// Orders one wave's LDS scratch accesses across its lanes (the collision counts, the actions /
+// previous tasks, the env's return).  A wave's LDS instructions complete in issue order, so a
+// wavefront-scope fence (compiler ordering, no wait) is enough.  ASG_LDS_FENCE_WG=1: the
+// round-4 workgroup-scope fence, whose release also waited for every outstanding global store
+// (s_waitcnt vmcnt(0)) -- three drains of the previous tile's row stores per transition (A/B)
+#ifndef ASG_LDS_FENCE_WG
+#define ASG_LDS_FENCE_WG 0
+#endif
 __device__ __forceinline__ void wave_lds_fence() {
+#if ASG_LDS_FENCE_WG
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     __builtin_amdgcn_wave_barrier();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 }
 
 // 1: the n = m = 64 shape runs the compile-time-shape instances (0: the runtime-shape ones, A/B)
@@ -1196,6 +1213,8 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
                 if constexpr (TAB) {
                     beta = ra.par ? mt_par_value(ra.par[(e * m + j) * n + i], k)
                                   : ra.table[(((int64_t)e * ra.T + k) * n + i) * m + j];
+                } else if (ASG_ROLLOUT_XSKIP & 1024) {
+                    beta = (double)(j & 3) * 0.25;
                 } else {
                     const Bump32 b =
                         philox_bump32(key, ra.episode, i * m + j, task_scale(s_scl, j), bsh, ra.dense != 0);
@@ -1213,7 +1232,7 @@ __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int
             }
             const int lo = __double2loint(rr), hi = __double2hiint(rr);
             const int cnt = n - i0 < 64 ? n - i0 : 64;
-            for (int l2 = 0; l2 < cnt; ++l2)
+            for (int l2 = 0; l2 < ((ASG_ROLLOUT_XSKIP & 512) ? 1 : cnt); ++l2)
                 sum += __hiloint2double(__builtin_amdgcn_readlane(hi, l2), __builtin_amdgcn_readlane(lo, l2));
         }
     };
@@ -1738,7 +1757,7 @@ rollout_kernel(RolloutArgs ra) {
             const int k = ri.k0 + it - sf;  // k0 - 1 on the select_first iteration
             const int ts = ri.ts0 + (k - ri.k0);
             const bool first_sel = it < sf;
-            if (!first_sel)
+            if (!first_sel && !(ASG_ROLLOUT_XSKIP & 256))
                 rollout_transition<TAB, SQ>(RA_, e, k, ts, key, s_scl, s_cnt, s_act, s_prev, s_ret);
             const int kk = k + 1;
             if (has_agent(ri, it)) {
