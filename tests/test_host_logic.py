@@ -196,6 +196,26 @@ def test_bench_profile_order_and_reset_share(monkeypatch):
         assert roof["traffic"] / roof["bytes_per_launch"] == pytest.approx(1.02, abs=0.002)
 
 
+def test_bench_bids_and_q_accounting(monkeypatch):
+    """The step_q rooflines: the Q rows are reported beside the HBM bytes (q_buffer), and the
+    bids_as_actions env's step writes no int64 one-hot and reads the int32 assignments instead of
+    the int64 actions row; no PMC summary is matched for it."""
+    import types
+    import bench
+    monkeypatch.setattr(bench, "pmc_lookup", lambda pattern, **kw: None)
+    a = types.SimpleNamespace(n=64, m=64, L=3)
+    E = 16384
+    q = bench.fused_roofline(a, E, 0.5, use_rnn=False, q_out=True)
+    b = bench.fused_roofline(a, E, 0.5, use_rnn=False, q_out=True, bids=True)
+    base = bench.step_bytes(64, 64, 3) + 64 * (4 * 64 + 8)
+    assert q["bytes_per_launch"] == base * E
+    assert b["bytes_per_launch"] == (base - 8 * 64 * 64 - 4 * 64) * E
+    assert q["q_buffer"]["bytes_per_launch"] == 4 * 64 * 64 * E == b["q_buffer"]["bytes_per_launch"]
+    assert q["traffic"] is None and b["traffic"] is None
+    for r in (q, b):
+        assert 0 < r["frac"] <= 1 and r["store_ceiling"]["frac"] <= 1
+
+
 @pytest.mark.parametrize("time_major", [False, True])
 def test_replay_buffer_matches_reference(golden, time_major):
     """Ring inserts (a split insert included), counters and seeded sample() against the
