@@ -119,13 +119,13 @@ __device__ __forceinline__ float philox_task_scale(EnvKey key, uint32_t episode,
 // the bump-shape constants of one launch (T's center grid exponent q, the width range)
 struct BumpShape {
     int T, q;
-    float wmin, wspan;
+    float wmin, wspan14;  // wspan14 = (wmax - wmin) 2^-14 (exact: a power-of-two scale)
     float cscale;  // T * 2^-16: the center directly from the 16-bit draw when q >= 16 (T < 256)
 };
 __host__ __device__ inline BumpShape bump_shape(int T, float wmin, float wmax) {
     int bits = 0;
     for (unsigned t = (unsigned)(T > 0 ? T : 1); t; t >>= 1) ++bits;
-    return BumpShape{T, 24 - bits, wmin, wmax - wmin, (float)T * 0x1p-16f};
+    return BumpShape{T, 24 - bits, wmin, (wmax - wmin) * 0x1p-14f, (float)T * 0x1p-16f};
 }
 
 // Pair 4k + s takes word s of Philox call k (counter {k, 0, kCtrPair4, episode}):
@@ -145,7 +145,8 @@ __device__ __forceinline__ Bump32 bump_from_word(uint32_t w, float scale, const 
     else
         b.center = __builtin_ldexpf(
             (float)(uint32_t)((((uint64_t)(w >> 16) * (uint64_t)(uint32_t)bs.T) << bs.q) >> 16), -bs.q);
-    const float spread = bs.wmin + bs.wspan * ((float)((w >> 2) & 0x3fffu) * 0x1p-14f);
+    // wmin + wspan u14 2^-14: (wspan 2^-14) u14 is the same exact product, one multiply fewer
+    const float spread = bs.wmin + bs.wspan14 * (float)((w >> 2) & 0x3fffu);
     // log2(e) / (2 sigma_2), sigma_2 = sqrt(spread^2 / -8 / ln 0.05), is for spread > 0
     // log2(e) sqrt(-2 ln 0.05) / spread: one v_rcp_f32 (<= 1 ulp) and a multiply (within
     // 3e-7 relative of the float64 formula; parity checks use the exported parameters)

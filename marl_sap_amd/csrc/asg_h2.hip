@@ -1469,10 +1469,13 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                         for (int v = 0; v < 4; ++v)
                             bp[c][v][nt] = Bump32{1.0f, (float)((jw + v + ia[nt]) & 15), 0.25f};
                     } else if (!GEN) {
-                        // the lane's 4 pairs (j .. j + 3) are one Philox call (m % 4 == 0)
+                        // the lane's 4 pairs (j .. j + 3) are one Philox call (m % 4 == 0); their task
+                        // scales from one 4-bit field of the scale bits (jw % 4 == 0: no wrap), each
+                        // 1.0f or 10.0f as bits (0x3f800000 + b 0x01a00000)
                         float sv[4];
+                        const uint32_t nib = (uint32_t)(sbits >> (jw & 63)) & 15u;
 #pragma unroll
-                        for (int v = 0; v < 4; ++v) sv[v] = ((sbits >> ((jw + v) & 63)) & 1ull) ? 10.0f : 1.0f;
+                        for (int v = 0; v < 4; ++v) sv[v] = __builtin_bit_cast(float, 0x3f800000u + ((nib >> v) & 1u) * 0x01a00000u);
                         Bump32 b4[4];
                         philox_bump32x4(key, ra.episode, ia[nt] * m + jw, sv, bsh, ra.dense != 0, b4);
 #pragma unroll
