@@ -1282,7 +1282,10 @@ struct HNext {
 #ifndef ASG_TAB_PRELOAD
 #define ASG_TAB_PRELOAD 1
 #endif
-constexpr int kTabPre = 3;
+#ifndef ASG_TAB_PRE
+#define ASG_TAB_PRE 3
+#endif
+constexpr int kTabPre = ASG_TAB_PRE;  // lookahead blocks preloaded per chunk
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
