@@ -1283,7 +1283,7 @@ struct HNext {
 #define ASG_TAB_PRELOAD 1
 #endif
 #ifndef ASG_TAB_PRE
-#define ASG_TAB_PRE 3
+#define ASG_TAB_PRE 2
 #endif
 constexpr int kTabPre = ASG_TAB_PRE;  // lookahead blocks preloaded per chunk
 #ifndef ASG_ROLLOUT_LATE
