@@ -112,7 +112,8 @@ def agent_flops(n, m, L, hidden=64, use_rnn=True, onehot=True):
     """Algorithmic flops of one agent row: fc1 (m(L+1) -> hidden), GRUCell (two hidden x
     3*hidden products), fc2 (hidden -> m); 2 flops per multiply-add.  onehot: the obs
     one-hot block (the first m inputs) is a column gather of W1, not m*hidden products
-    (the fused kernel's one-hot prefix, ASG_AGENT_ONEHOT), so fc1 counts K - m inputs."""
+    (the fused kernel's one-hot prefix; a -DASG_AGENT_ONEHOT=0 build turns it off), so fc1
+    counts K - m inputs."""
     K = m * (L + 1) - (m if onehot else 0)
     rec = 2 * 3 * hidden * hidden if use_rnn else hidden * hidden
     return 2 * (K * hidden + rec + hidden * m)
@@ -131,7 +132,7 @@ def agent_roofline(a, E, agent_ms, kernel):
     if agent_ms is None or agent_ms <= 0:
         return None
     fused = a.agent in FUSED_AGENTS
-    onehot = fused and os.environ.get("ASG_AGENT_ONEHOT", "1") != "0"
+    onehot = fused
     flops = agent_flops(a.n, a.m, a.L, onehot=onehot) * E * a.n
     tfs = flops / (agent_ms * 1e-3) / 1e12
     from marl_sap_amd import _lib
@@ -533,8 +534,10 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
                 state["mode"] = "random_episode" if fused_sched else None
             else:
                 state["mode"] = mac.fused_mode(env, runner.batch, runner.t_env)
+        # (the random policy's launch folds the reset in the Philox mode only: the MT19937 reset
+        # is its draw kernels, run by random_rollout itself before the launch)
         state["fuse_reset"] = bool(a.fuse_reset) and (
-            state["mode"] in ("episode", "random_episode")
+            state["mode"] == "episode" or (state["mode"] == "random_episode" and env.rng == "philox")
             or (state["mode"] == "step_q" and mac.fused_reset_ok(env)))  # asg_reset_forward
         if not state["fuse_reset"]:
             env.reset(runner.batch, ts=0)

@@ -155,6 +155,14 @@ int asg_reset(asg_handle *h, const asg_batch_view *b, int ts);
  * accumulate per-env float64 returns.  Actions outside [0, m) set a sticky device
  * error reported by asg_sync_status. */
 int asg_step(asg_handle *h, const asg_batch_view *b, int ts);
+/* asg_step with flags.  ASG_STEP_USE_SELECTED_BIDS (bids_as_actions): the caller states that
+ * batch row ts still holds exactly the bids asg_bids_select wrote there (nothing wrote the row
+ * since), so the step takes the assignments that call solved instead of solving the row again;
+ * ASG_E_STATE when row ts is not the row asg_bids_select last wrote (a step or reset came in
+ * between, or another row / layout).  Without the flag (asg_step) the bids row is always
+ * solved as it is at the step (mock_constellation_env.py:121-122). */
+#define ASG_STEP_USE_SELECTED_BIDS 0x1
+int asg_step_ex(asg_handle *h, const asg_batch_view *b, int ts, int flags);
 /* Uniform random actions in [0, m) at row ts (Philox keyed (seed, env, episode, t)). */
 int asg_random_actions(asg_handle *h, const asg_batch_view *b, int ts);
 /* The random policy's episode in one launch: for the next `steps` steps of every env, the
@@ -395,10 +403,16 @@ int asg_step_select(asg_handle *h, const asg_batch_view *b, int ts, const void *
  * h_out the hidden state.  Needs k + 1 < T; the actions of row ts are read from the batch.
  * Every benefit source (Philox, MT19937-compat and injected tables); agent and batch
  * requirements as asg_rollout.  bids_as_actions: the tasks of row ts are LSA(bids row ts,
- * maximize) -- the assignments asg_bids_select left for that row, else solved first. */
+ * maximize), solved in the launch's stream order before the transition; asg_step_forward_ex
+ * with ASG_STEP_USE_SELECTED_BIDS takes the assignments asg_bids_select solved for that row
+ * instead (as asg_step_ex). */
 int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream);
+int asg_step_forward_ex(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                        const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                        const float *h_in, int64_t h_stride, float *h_out, float *q_out, int flags,
+                        void *hip_stream);
 /* asg_reset then the agent forward on the reset row ts (Q to q_out, the hidden state to h_out), in
  * one launch: the runner's env.reset() + mac.forward(0) of a selector acting on Q outside the
  * kernel (runners/episode_runner.py:49-62 with sap_selectors.py:52-98 / bet_selectors.py).  The
@@ -417,8 +431,9 @@ int asg_reset_forward(asg_handle *h, const asg_batch_view *b, int ts, const void
  * (agent_output_type "pi_logits"); col_softmax: softmax over the agents (softmax_agent_inputs);
  * noise_std >= 0: Gaussian noise N(0, noise_std) from Philox keyed by (seed, global env index, counter)
  * (0: the means exactly).  Writes the bids to bids_out [E][n][m] (element strides: the batch's
- * actions row) and their LSA(maximize) assignments into the handle, which the next asg_step /
- * asg_step_forward on that batch row uses instead of solving it again.  A NaN / +inf bid sets
+ * actions row) and their LSA(maximize) assignments into the handle, which asg_step_ex /
+ * asg_step_forward_ex with ASG_STEP_USE_SELECTED_BIDS on that batch row use instead of solving
+ * it again (the caller vouches that nothing rewrote the row in between).  A NaN / +inf bid sets
  * the env's sticky error (asg_sync_status: "matrix contains invalid numeric entries"). */
 int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
                     const int64_t out_strides[3], int row_softmax, int col_softmax, double noise_std, uint64_t seed,

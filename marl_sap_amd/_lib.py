@@ -26,6 +26,7 @@ ASG_BENEFIT_BUMP, ASG_BENEFIT_DENSE, ASG_BENEFIT_INJECTED = 0, 1, 2
 ASG_QUIRK_PREV_ASSIGNS_ZERO = 0x1
 ASG_QUIRK_PARALLEL_TERMINATED = 0x2
 ASG_QUIRK_REPLICATE_STREAM = 0x4
+ASG_STEP_USE_SELECTED_BIDS = 0x1
 
 _DTYPES = {torch.float32: ASG_F32, torch.float64: ASG_F64, torch.int64: ASG_I64,
            torch.int32: ASG_I32, torch.bool: ASG_BOOL, torch.float16: ASG_F16, torch.int16: ASG_I16}
@@ -43,7 +44,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_real_haal_num_sequences", "asg_step_select", "asg_step_select_l2_slices", "asg_rollout",
            "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward",
            "asg_sap_noise", "asg_random_rollout", "asg_sap_select_warm", "asg_bids_select",
-           "asg_reset_forward"]
+           "asg_reset_forward", "asg_step_ex", "asg_step_forward_ex"]
 
 
 class AsgField(ctypes.Structure):
@@ -173,6 +174,10 @@ def lib():
                                             vp, i64, vp, vp, vp]
         L.asg_step_forward.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, vp, vp, vp, vp, vp, i32, i32, i32, vp,
                                        i64, vp, vp, vp]
+        if hasattr(L, "asg_step_ex"):  # absent from older A/B builds
+            L.asg_step_ex.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, i32]
+            L.asg_step_forward_ex.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, vp, vp, vp, vp, vp, i32, i32,
+                                              i32, vp, i64, vp, vp, i32, vp]
         for f in EXPORTS:
             if f not in ("asg_last_error", "asg_real_destroy") and hasattr(L, f):
                 getattr(L, f).restype = i32

@@ -86,6 +86,19 @@ bool bids_ready(const asg_handle *h, const asg_batch_view *b, int ts) {
            t.s_task == f.stride[3];
 }
 
+// ASG_STEP_USE_SELECTED_BIDS: the caller states that batch row ts still holds the bids
+// asg_bids_select wrote (nothing wrote the row since); the handle checks that it is that row.
+// Without the flag every step solves the row it is given.
+int selected_bids_ok(asg_handle *h, const asg_batch_view *b, int ts, int flags) {
+    if (!(flags & ASG_STEP_USE_SELECTED_BIDS)) return ASG_OK;
+    if (!h->st.bids) return fail(h, ASG_E_INVALID_ARG, "ASG_STEP_USE_SELECTED_BIDS needs a bids_as_actions handle");
+    if (!bids_ready(h, b, ts))
+        return fail(h, ASG_E_STATE,
+                    "ASG_STEP_USE_SELECTED_BIDS: batch row ts is not the row asg_bids_select last wrote "
+                    "(or a step / reset came in between)");
+    return ASG_OK;
+}
+
 }  // namespace
 
 void asg::set_last_error(const std::string &msg) { g_err = msg; }
@@ -226,13 +239,17 @@ int asg_reset(asg_handle *h, const asg_batch_view *b, int ts) {
     return ASG_OK;
 }
 
-int asg_step(asg_handle *h, const asg_batch_view *b, int ts) {
+int asg_step(asg_handle *h, const asg_batch_view *b, int ts) { return asg_step_ex(h, b, ts, 0); }
+
+int asg_step_ex(asg_handle *h, const asg_batch_view *b, int ts, int flags) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (int rc = check_view(h, b, ts, true)) return rc;
     if (!h->has_reset) return fail(h, ASG_E_STATE, "step called before reset");
     if (h->k >= h->st.T) return fail(h, ASG_E_STATE, "episode already terminated (k >= T); reset first");
+    if (flags & ~ASG_STEP_USE_SELECTED_BIDS) return fail(h, ASG_E_INVALID_ARG, "asg_step_ex: unknown flags");
+    if (int rc = selected_bids_ok(h, b, ts, flags)) return rc;
     DeviceGuard g(h->device);
-    const bool ready = bids_ready(h, b, ts);
+    const bool ready = (flags & ASG_STEP_USE_SELECTED_BIDS) != 0;
     hipError_t e = asg::launch_step(*b, h->st, ts, h->k, h->stream, ready);
     if (e != hipSuccess) return hip_fail(h, e, "asg_step");
     h->k += 1;
@@ -639,9 +656,13 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
                         int reset, const void *packed, const float *b1, const float *b_r0, const float *b_r1,
                         const float *b2, int K, int hidden, int use_rnn, const float *h_in, int64_t h_stride,
                         float *h_out, double epsilon, uint64_t seed, uint64_t counter, int32_t *status,
-                        void *hip_stream, float *q_out = nullptr) {
+                        void *hip_stream, float *q_out = nullptr, int flags = 0) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     if (int rc = check_view(h, b, ts, true)) return rc;
+    if (flags & ~ASG_STEP_USE_SELECTED_BIDS) return fail(h, ASG_E_INVALID_ARG, "asg_step_forward_ex: unknown flags");
+    if (reset && (flags & ASG_STEP_USE_SELECTED_BIDS))
+        return fail(h, ASG_E_INVALID_ARG, "ASG_STEP_USE_SELECTED_BIDS: a reset has no bids row to step");
+    if (int rc = selected_bids_ok(h, b, ts, flags)) return rc;
     if (!packed || !b1 || !b_r0 || (use_rnn && !b_r1) || !b2 || !h_out || (!status && !q_out))
         return fail(h, ASG_E_INVALID_ARG, "asg_rollout: NULL agent argument");
     if (q_out && (reinterpret_cast<uintptr_t>(q_out) % 16) != 0)
@@ -701,7 +722,7 @@ static int rollout_impl(asg_handle *h, const asg_batch_view *b, int ts, int step
     // as asg_reset: a fresh Philox key per episode, committed once the launch succeeded
     asg::EnvState lst = h->st;
     if (reset && h->has_reset) lst.episode += 1;
-    if (st.bids && !reset && !bids_ready(h, b, ts)) {  // the bids of row ts not solved by asg_bids_select
+    if (st.bids && !reset && !(flags & ASG_STEP_USE_SELECTED_BIDS)) {  // solve the bids of row ts
         hipError_t e0 = asg::launch_bids_assign(*b, st, ts, s);
         if (e0 != hipSuccess) return hip_fail(h, e0, "asg_step_forward (bids LSA)");
     }
@@ -758,9 +779,17 @@ int asg_reset_forward(asg_handle *h, const asg_batch_view *b, int ts, const void
 int asg_step_forward(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
                      const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
                      const float *h_in, int64_t h_stride, float *h_out, float *q_out, void *hip_stream) {
+    return asg_step_forward_ex(h, b, ts, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in, h_stride, h_out, q_out,
+                               0, hip_stream);
+}
+
+int asg_step_forward_ex(asg_handle *h, const asg_batch_view *b, int ts, const void *packed, const float *b1,
+                        const float *b_r0, const float *b_r1, const float *b2, int K, int hidden, int use_rnn,
+                        const float *h_in, int64_t h_stride, float *h_out, float *q_out, int flags,
+                        void *hip_stream) {
     if (!q_out) return fail(h, ASG_E_INVALID_ARG, "asg_step_forward: NULL q_out");
     return rollout_impl(h, b, ts, 1, 0, 1, 0, packed, b1, b_r0, b_r1, b2, K, hidden, use_rnn, h_in, h_stride, h_out,
-                        0.0, 0, 0, nullptr, hip_stream, q_out);
+                        0.0, 0, 0, nullptr, hip_stream, q_out, flags);
 }
 
 int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,

@@ -937,23 +937,18 @@ int stream_cus(hipStream_t s) {
     return last_n < ncu ? last_n : ncu;
 }
 
-// ASG_AGENT_ONEHOT=0 disables the one-hot prefix shortcut (A/B experiments)
-bool onehot_prefix_enabled() {
-    static const int v = [] {
-        const char *e = getenv("ASG_AGENT_ONEHOT");
-        return e ? atoi(e) : 1;
-    }();
-    return v != 0;
-}
+// Build-time A/B switches (no runtime environment knobs in the shipped library):
+// -DASG_AGENT_ONEHOT=0 disables the one-hot prefix shortcut (and with it the episode kernel,
+// whose tiles rely on it); -DASG_AGENT_LDS_WEIGHTS=0 selects the L2-weight kernel.
+#ifndef ASG_AGENT_ONEHOT
+#define ASG_AGENT_ONEHOT 1
+#endif
+#ifndef ASG_AGENT_LDS_WEIGHTS
+#define ASG_AGENT_LDS_WEIGHTS 1
+#endif
+bool onehot_prefix_enabled() { return ASG_AGENT_ONEHOT != 0; }
 
-// ASG_AGENT_LDS_WEIGHTS=0 selects the L2-weight kernel (A/B experiments)
-static bool use_lds_weights() {
-    static const int v = [] {
-        const char *e = getenv("ASG_AGENT_LDS_WEIGHTS");
-        return e ? atoi(e) : 1;
-    }();
-    return v != 0;
-}
+static bool use_lds_weights() { return ASG_AGENT_LDS_WEIGHTS != 0; }
 
 hipError_t launch_rnn_agent_fwd(const float *X, int64_t xs, int64_t R, int K, const float *Hin, int64_t hs,
                                 const float4 *packed, const float *b1, const float *bih, const float *bhh,

@@ -107,7 +107,7 @@ hipError_t launch_filtered_soft_map(const int64_t *picked, const int64_t *topm, 
 
 int64_t rnn_agent_packed_f4(int K, int nout, int use_rnn);
 int stream_cus(hipStream_t s);        // CUs the stream may run on (persistent grids)
-bool onehot_prefix_enabled();         // ASG_AGENT_ONEHOT (default on)
+bool onehot_prefix_enabled();         // -DASG_AGENT_ONEHOT (build time, default on)
 hipError_t launch_w1t_pack(const float *W1, int K, int P, float *out, hipStream_t s);
 
 // split-f16 agent path (asg_h2.hip): input geometry -- NB blocks of P inputs, each padded to

@@ -156,7 +156,10 @@ __device__ __forceinline__ void sap_select_one(const float *q, int64_t q0, int64
         double vnew = __builtin_nan("");
         if (ASG_SAP_FAST && status == ASG_OK && n == m)
             done = lsa_fast_reg64<decltype(rc), kCount, true>(rc, n, c4r, &nfast, slot, vin, &vnew) == ASG_OK;
-        *dp = vnew;
+        // only certified duals carry over: an env whose fast path ended uncertified (ties, NaN)
+        // or did not run stores NaN and starts cold next call (lsa_fast_reg64 fills vnew before
+        // its certificate)
+        *dp = done ? vnew : __builtin_nan("");
     } else if (ASG_SAP_FAST && status == ASG_OK && n == m) {
         done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, slot) == ASG_OK;
     }

@@ -138,13 +138,27 @@ class AssignEnvBatch(MultiAgentEnv):
         """New episode for every env; writes the pre-transition row `ts` of `batch`."""
         self._call("asg_reset", ctypes.byref(batch_view(batch)), int(ts))
         self.k = 0
+        self._bids_token = None
 
     def step(self, batch, ts):
         """Reads actions at row ts; writes rewards/terminated/actions_onehot at ts and the
         next pre-transition row ts+1.  Returns the `done` flag (identical for all envs)."""
-        self._call("asg_step", ctypes.byref(batch_view(batch)), int(ts))
+        self._call("asg_step_ex", ctypes.byref(batch_view(batch)), int(ts), self._bids_flags(batch, ts))
         self.k += 1
         return self.k >= self.T
+
+    def _bids_flags(self, batch, ts):
+        """ASG_STEP_USE_SELECTED_BIDS when batch row ts holds exactly the bids bids_select wrote:
+        the same row (pointer, strides) and the actions tensor's version counter unchanged since
+        (torch bumps it on every in-place write -- EpisodeBatch.update, slice assignment, copy_ --
+        to any view of the tensor; the kernel's own write does not touch it).  Otherwise 0: the
+        step solves the row as it is.  The token is spent by the step."""
+        tok, self._bids_token = getattr(self, "_bids_token", None), None
+        if not self.bids_as_actions or tok is None:
+            return 0
+        td = batch.data.transition_data if hasattr(batch, "data") else batch
+        row = td["actions"][:, int(ts)]
+        return _lib.ASG_STEP_USE_SELECTED_BIDS if tok == (row.data_ptr(), tuple(row.stride()), row._version) else 0
 
     def can_step_select(self, prefer=True, use_rnn=True, bids_ok=False):
         """Whether asg_rollout (env steps fused with the agent forward + epsilon-greedy
@@ -184,6 +198,7 @@ class AssignEnvBatch(MultiAgentEnv):
         self._call("asg_reset_forward", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
                    ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), _lib.stream_ptr(self.device))
         self.k = 0
+        self._bids_token = None
         return q_out, h_out
 
     def _forward_args(self, batch, agent, hidden_state, q_out):
@@ -199,8 +214,9 @@ class AssignEnvBatch(MultiAgentEnv):
         + mac.forward for a selector that acts on Q outside the kernel (SAP).  Returns
         (Q [E n, m] float32, the new hidden state [E n, hidden])."""
         q_out, h_out, args = self._forward_args(batch, agent, hidden_state, q_out)
-        self._call("asg_step_forward", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
-                   ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), _lib.stream_ptr(self.device))
+        self._call("asg_step_forward_ex", ctypes.byref(batch_view(batch)), int(ts), *args[:-1],
+                   ctypes.c_void_p(h_out.data_ptr()), ctypes.c_void_p(q_out.data_ptr()), self._bids_flags(batch, ts),
+                   _lib.stream_ptr(self.device))
         self.k += 1
         return q_out, h_out
 
@@ -217,6 +233,7 @@ class AssignEnvBatch(MultiAgentEnv):
                    ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), int(bool(row_softmax)),
                    int(bool(col_softmax)), float(std), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter),
                    _lib.stream_ptr(self.device))
+        self._bids_token = (out.data_ptr(), tuple(out.stride()), out._version)
         return out
 
     def rollout(self, batch, ts, steps, agent, hidden_state, epsilon, seed, counter, status, select_first=True,
@@ -233,6 +250,7 @@ class AssignEnvBatch(MultiAgentEnv):
         h_out = args[-1]
         tail = (*args[:-1], ctypes.c_void_p(h_out.data_ptr()), float(epsilon), seed & 0xFFFFFFFFFFFFFFFF, int(counter),
                 ctypes.c_void_p(status.data_ptr()), _lib.stream_ptr(self.device))
+        self._bids_token = None
         if reset and not self.fused_reset_ok:
             self.reset(batch, ts)  # table modes: asg_reset, then the episode from the reset row
             reset, select_first = False, True
@@ -252,7 +270,12 @@ class AssignEnvBatch(MultiAgentEnv):
     def random_rollout(self, batch, ts, steps, reset=False):
         """The uniform random policy's next `steps` steps in one launch (asg_random_rollout):
         random_actions(ts + s) + step(ts + s) for s < steps, after reset(ts) when `reset` --
-        bit-identical to those separate calls."""
+        bit-identical to those separate calls.  The MT19937 mode's reset is asg_reset (its stream's
+        draw kernels) followed by the launch."""
+        self._bids_token = None
+        if reset and self.rng == "mt19937":
+            self.reset(batch, ts)
+            reset = False
         self._call("asg_random_rollout", ctypes.byref(batch_view(batch)), int(ts), int(steps), int(bool(reset)))
         self.k = (0 if reset else self.k) + int(steps)
         return self.k >= self.T

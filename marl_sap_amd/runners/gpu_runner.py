@@ -162,14 +162,30 @@ class GpuVecRunner:
         """Host side of the finished episodes: selector status, device errors, logging.
         The selectors' status goes first: an env whose noisy Q was invalid gets -1 in its actions
         row (asg_sap_select_into) and the next transition then sets the env's sticky action-range
-        error -- the LSA's "invalid numeric entries" is the cause and is the error raised."""
-        for sel in (getattr(self.mac, "action_selector", None), getattr(self.mac, "jumpstart_action_selector", None)):
-            if hasattr(sel, "flush"):
-                sel.flush()
-            st = getattr(sel, "status", None)
-            if hasattr(st, "flush"):
-                st.flush()
-        self.env.sync()
+        error -- the LSA's "invalid numeric entries" is the cause and is the error raised.  Whatever
+        raises, the env's sticky device error word is read and cleared (its action-range error
+        chained under the selector's) and the pending episodes are dropped, so a caller that
+        catches the exception and continues sees no stale error on the next flush."""
+        try:
+            try:
+                for sel in (getattr(self.mac, "action_selector", None),
+                            getattr(self.mac, "jumpstart_action_selector", None)):
+                    if hasattr(sel, "flush"):
+                        sel.flush()
+                    st = getattr(sel, "status", None)
+                    if hasattr(st, "flush"):
+                        st.flush()
+            except BaseException as sel_err:
+                try:
+                    self.env.sync()
+                except Exception as env_err:  # the consequence (-1 actions), not the cause
+                    raise sel_err from env_err
+                raise
+            self.env.sync()
+        except BaseException:
+            self._pending.clear()
+            self._pending_steps.clear()
+            raise
         for (returns, test_mode), steps in zip(self._pending, self._pending_steps):
             self.last_returns = returns
             cur_stats = self.test_stats if test_mode else self.train_stats

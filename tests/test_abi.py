@@ -77,6 +77,7 @@ def test_kernel_entry_points_validate_without_gpu(L):
         _lib.ASG_E_INVALID_ARG
     assert L.asg_reset(None, None, 0) == _lib.ASG_E_INVALID_ARG
     assert L.asg_step(None, None, 0) == _lib.ASG_E_INVALID_ARG
+    assert L.asg_step_ex(None, None, 0, _lib.ASG_STEP_USE_SELECTED_BIDS) == _lib.ASG_E_INVALID_ARG
     assert L.asg_random_rollout(None, None, 0, 20, 1) == _lib.ASG_E_INVALID_ARG
     assert L.asg_bids_select(None, None, None, None, None, 1, 1, 0.1, 0, 1, None) == _lib.ASG_E_INVALID_ARG
     agent = [None] * 5 + [256, 64, 1, None, 0, None, 0.05, 0, 1, None, None]

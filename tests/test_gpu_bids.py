@@ -93,6 +93,44 @@ def test_bids_tagged_step_equals_solving_the_row():
     b_env.close()
 
 
+def test_bids_row_rewritten_after_select_is_solved_again():
+    """a bids row rewritten after asg_bids_select (EpisodeBatch.update, a slice
+    assignment, ...) must be solved as it is at the step, not stepped on the stale assignments.
+    The env passes ASG_STEP_USE_SELECTED_BIDS only while the actions tensor's version is the one
+    bids_select recorded; the raw C-ABI refuses the flag for a row bids_select did not write."""
+    import ctypes
+
+    from marl_sap_amd import _lib
+    from marl_sap_amd.envs.assign_env import batch_view
+    n, m, E = 16, 24, 32
+    env, batch = _env(n, m, E=E, seed=5)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    q = (torch.randn(E, n, m, generator=g) * 3.0).to(DEV)
+    new_bids = (torch.randn(E, n, m, generator=g)).to(DEV)
+    row = batch["actions"][:, 0]
+    env.bids_select(q, row, 1, 1, 0.0, SEED, 1)
+    assert env._bids_flags(batch, 0) == _lib.ASG_STEP_USE_SELECTED_BIDS
+    env._bids_token = (row.data_ptr(), tuple(row.stride()), row._version)  # _bids_flags spent it
+    batch.update({"actions": new_bids}, ts=0, mark_filled=False)  # rewrites the row in place
+    assert env._bids_flags(batch, 0) == 0
+    env._bids_token = None
+    env.step(batch, 0)
+    got = batch["prev_assigns"][:, 1].cpu().numpy()
+    nb = batch["actions"][:, 0].cpu().double().numpy()
+    assert np.array_equal(nb, new_bids.cpu().double().numpy())
+    for e in range(E):
+        _, col = ora.lsa(nb[e], maximize=True)
+        assert np.array_equal(got[e], col), e
+    env.sync()
+    # the raw ABI: the flag on a row asg_bids_select did not write is refused (no silent reuse)
+    L = _lib.lib()
+    env.bids_select(q, batch["actions"][:, 1], 1, 1, 0.0, SEED, 2)
+    with torch.cuda.device(env.device):
+        rc = L.asg_step_ex(env._h, ctypes.byref(batch_view(batch)), 2, _lib.ASG_STEP_USE_SELECTED_BIDS)
+    assert rc == _lib.ASG_E_STATE and "not the row" in _lib.last_error(env._h)
+    env.close()
+
+
 def test_bids_noise_distribution_determinism_sharding():
     n = m = 64
     E, std = 256, 0.3

@@ -416,6 +416,14 @@ def test_native_bump_precision_vs_float64():
             got = h["obs"][:, t, :, m * (l + 1):m * (l + 2)].astype(np.float64)
             err = np.abs(got - want)
             assert (err <= bound + 2.0 ** -24 * np.abs(want)).all(), f"obs t={t} l={l}: {float((err - bound).max())}"
+            # relative bound over the whole range: value = scale 2^-y, y = x^2 a2 rounded
+            # twice in float32 (|dy| <= y 2^-23) and one v_exp_f32 + the scale product (<= 2 ulp), so
+            # err <= (y ln2 + 2) 2^-23 want; values that flush below FLT_MIN keep the absolute term
+            pos = (want > 0) & (scale > 0)
+            y = np.log2(np.where(pos, scale, 1.0) / np.where(pos, want, 1.0))
+            rel_bound = (y * np.log(2.0) + 2.0) * 2.0 ** -23 * want + 10.0 * float(np.finfo(np.float32).tiny)
+            assert (err[pos] <= rel_bound[pos]).all(), \
+                f"obs t={t} l={l}: relative {float(np.max((err[pos] - rel_bound[pos]) / want[pos]))}"
             worst_abs = max(worst_abs, float((err / np.maximum(scale, 1.0)).max()))
             big = want >= scale * 2.0 ** -12
             if (big & (scale > 0)).any():

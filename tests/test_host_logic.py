@@ -279,3 +279,41 @@ def test_jumpstart_flips_keep_reference_stream_order(selector):
     flips = [mac._coin(0, False) for _ in range(3)]
     np.random.seed(7)
     assert flips == list(np.random.rand(3) < 0.5)
+
+
+def test_runner_flush_clears_env_error_when_selector_raises():
+    """when a selector's status raises in flush_pending, the env's sticky device error
+    is still read and cleared (chained as the cause) and the pending episodes are dropped, so the
+    next flush sees neither a stale error nor duplicate episodes."""
+    from marl_sap_amd.runners.gpu_runner import GpuVecRunner
+
+    class Sel:
+        def __init__(self):
+            self.fail = True
+
+        def flush(self):
+            if self.fail:
+                self.fail = False
+                raise ValueError("matrix contains invalid numeric entries")
+
+    class Env:
+        def __init__(self):
+            self.err, self.syncs = True, 0
+
+        def sync(self):
+            self.syncs += 1
+            if self.err:
+                self.err = False
+                raise ValueError("an action outside [0, m) was passed to step")
+
+    r = object.__new__(GpuVecRunner)
+    r.mac = SimpleNamespace(action_selector=Sel())
+    r.env = Env()
+    r._pending, r._pending_steps = [("returns", False)], [20]
+    with pytest.raises(ValueError, match="invalid numeric entries") as ei:
+        r.flush_pending()
+    assert isinstance(ei.value.__cause__, ValueError) and "outside" in str(ei.value.__cause__)
+    assert r.env.syncs == 1 and not r.env.err
+    assert r._pending == [] and r._pending_steps == []
+    r.flush_pending()  # nothing stale left: no error, nothing logged twice
+    assert r.env.syncs == 2
