@@ -473,7 +473,9 @@ typedef struct {
     const double *T_trans;     /* host [m][m] or NULL (= 1 - I) */
     const double *task_prios;  /* host [m] or NULL (= ones) */
     int32_t variant;           /* asg_real_variant */
-    int32_t pad_;
+    int32_t bids_as_actions;   /* actions are float32 bids [B,T+1,n,m]; the step's assignments are
+                                  LSA(bids, maximize) (real_constellation_env.py:110-112, :140-142;
+                                  real_power :112, :142; interference :121, :159); no one-hot */
     uint64_t seed;             /* power variants: Philox key of the reset assignments ... */
     int64_t env_index_base;    /* ... per global env index (choice(m, n, replace=False)) */
     const int32_t *sat_freq_bands;   /* host [n] (interference) */

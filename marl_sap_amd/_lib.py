@@ -74,7 +74,7 @@ class AsgRealConfig(ctypes.Structure):
                 ("T", ctypes.c_int32), ("L", ctypes.c_int32), ("N", ctypes.c_int32), ("M", ctypes.c_int32),
                 ("lambda_", ctypes.c_double), ("T_trans", ctypes.POINTER(ctypes.c_double)),
                 ("task_prios", ctypes.POINTER(ctypes.c_double)), ("variant", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("seed", ctypes.c_uint64), ("env_index_base", ctypes.c_int64),
+                ("bids_as_actions", ctypes.c_int32), ("seed", ctypes.c_uint64), ("env_index_base", ctypes.c_int64),
                 ("sat_freq_bands", ctypes.POINTER(ctypes.c_int32)),
                 ("neighbor_matrix", ctypes.POINTER(ctypes.c_double))]
 

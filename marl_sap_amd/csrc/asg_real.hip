@@ -61,6 +61,9 @@ struct RealState {
     uint64_t seed;
     int64_t env_base;
     uint32_t episode;
+    int bids;                     // bids_as_actions: actions are float32 [n][m] bids
+    const int64_t *assign;        // bids: LSA(bids row, maximize) assignments [E][n] of this step
+    const int32_t *assign_status; // bids: their LSA status [E] (0, ASG_E_LSA_INVALID / _INFEASIBLE)
 };
 
 __device__ __forceinline__ void store_real(const asg_field &f, int64_t off, double v) {
@@ -237,8 +240,12 @@ __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv,
     double *srew = reinterpret_cast<double *>(scnt + m + (((n + m) & 1) ? 1 : 0));  // [n], 8-B aligned
     const double *tab = st.table + e * st.table_env_stride;
     int *prev = st.prev + e * n;
+    const int lsa_st = st.assign ? st.assign_status[e] : 0;
+    if (lsa_st != 0 && threadIdx.x == 0) atomicCAS(st.err, 0, lsa_st);  // scipy's ValueError
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        int64_t a = load_int(bv.actions, foff(bv.actions, e, ts, i, 0));
+        // bids_as_actions: the assignments of LSA(bids, maximize) (real_constellation_env.py:
+        // 140-142, real_power_constellation_env.py:142, interference_constellation_env.py:159)
+        int64_t a = st.assign ? (lsa_st != 0 ? 0 : st.assign[e * n + i]) : load_int(bv.actions, foff(bv.actions, e, ts, i, 0));
         if (a < 0 || a >= m) {
             atomicCAS(st.err, 0, ASG_E_ACTION_RANGE);
             a = a < 0 ? 0 : m - 1;
@@ -381,9 +388,10 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
     // are computed once; the scheme's own dtypes (f16 beta, bool avail, i16 one-hot) take
     // typed stores, anything else the generic ones
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    // (bids_as_actions: no actions_onehot field -- the scheme has no preprocess, :110-112)
     const bool fast = bv.beta.dtype == ASG_F16 && bv.avail_actions.dtype == ASG_BOOL &&
-                      (!step || bv.actions_onehot.dtype == ASG_I16) && bv.beta.ptr && bv.avail_actions.ptr &&
-                      (!step || bv.actions_onehot.ptr);
+                      (!step || !bv.actions_onehot.ptr || bv.actions_onehot.dtype == ASG_I16) && bv.beta.ptr &&
+                      bv.avail_actions.ptr;
     for (int r = wave; r < rows; r += waves) {
         const int i = i0 + r;
         const double *t0 = tab + ((int64_t)knew * n + i) * m;  // slice knew, row i
@@ -395,10 +403,11 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
         if (fast) {
             __half *bb = reinterpret_cast<__half *>(bv.beta.ptr) + foff(bv.beta, e, row, i, 0);
             uint8_t *ab = reinterpret_cast<uint8_t *>(bv.avail_actions.ptr) + foff(bv.avail_actions, e, row, i, 0);
-            int16_t *ob = step ? reinterpret_cast<int16_t *>(bv.actions_onehot.ptr) + foff(bv.actions_onehot, e, ts, i, 0)
-                               : nullptr;
+            int16_t *ob = step && bv.actions_onehot.ptr
+                              ? reinterpret_cast<int16_t *>(bv.actions_onehot.ptr) + foff(bv.actions_onehot, e, ts, i, 0)
+                              : nullptr;
             const int64_t bs3 = bv.beta.stride[3], as3 = bv.avail_actions.stride[3];
-            const int64_t os3 = step ? bv.actions_onehot.stride[3] : 0;
+            const int64_t os3 = ob ? bv.actions_onehot.stride[3] : 0;
             for (int j = lane; j < m; j += 64) {
                 const double pr = st.prios[j];
                 double sum = 0.0;
@@ -410,7 +419,7 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
                 trow[j] = sum;
                 if (!(ASG_REAL_PROF_SKIP & 2)) {
                     ab[j * as3] = 1;
-                    if (step) ob[j * os3] = (int16_t)(pa == j);
+                    if (ob) ob[j * os3] = (int16_t)(pa == j);
                 }
             }
         } else {
@@ -738,6 +747,8 @@ struct asg_real_handle {
     double *table_buf = nullptr;
     void *haal_ws = nullptr;  // HAAL workspace (grown on demand)
     size_t haal_ws_bytes = 0;
+    int64_t *bids_assign = nullptr;   // bids_as_actions: [E][n] assignments of the step's LSA
+    int32_t *bids_status = nullptr;   // [E] its status
     std::string err;
 };
 
@@ -780,7 +791,9 @@ int rcheck_view(asg_real_handle *h, const asg_batch_view *b, bool step) {
                     rfield_ok(b->prev_assigns, {ASG_I16, ASG_I32, ASG_I64}) &&
                     rfield_ok(b->actions_onehot, {ASG_I16, ASG_I32, ASG_I64}) && rfield_ok(b->filled, {ASG_I64});
     if (!ok) return rfail(h, ASG_E_INVALID_ARG, "batch field dtype does not match the real-env scheme");
-    if (step && (!b->actions.ptr || !rfield_ok(b->actions, {ASG_I16, ASG_I32, ASG_I64})))
+    if (step && h->st.bids && (!b->actions.ptr || !rfield_ok(b->actions, {ASG_F32})))
+        return rfail(h, ASG_E_INVALID_ARG, "bids_as_actions expects float32 actions [B, T+1, n, m]");
+    if (step && !h->st.bids && (!b->actions.ptr || !rfield_ok(b->actions, {ASG_I16, ASG_I32, ASG_I64})))
         return rfail(h, ASG_E_INVALID_ARG, "step needs integer actions");
     return ASG_OK;
 }
@@ -804,8 +817,20 @@ hipError_t launch_real(asg_real_handle *h, const asg_real_batch_view &v, int ts,
     const int knew = step ? h->k + 1 : 0;
     const int row = step ? ts + 1 : ts;
     if (step) {
+        RealState tst = st;
+        if (st.bids) {
+            // the step's LSA(bids row ts, maximize) for every env in one batched launch (the
+            // scipy-exact solver, rectangular n <= m, float32 bids read in place; asg_lsa.hip)
+            const float *row0 = static_cast<const float *>(bv.actions.ptr) + (int64_t)ts * bv.actions.stride[1];
+            const int64_t str[3] = {bv.actions.stride[0], bv.actions.stride[2], bv.actions.stride[3]};
+            hipError_t e0 = asg::launch_lsa_batched(row0, ASG_F32, str, st.E, st.n, st.m, 1, nullptr, h->bids_assign,
+                                                    h->bids_status, h->stream);
+            if (e0 != hipSuccess) return e0;
+            tst.assign = h->bids_assign;
+            tst.assign_status = h->bids_status;
+        }
         hipLaunchKernelGGL(asg::real_transition_kernel, dim3((unsigned)st.E), dim3(256), asg::transition_lds(st.n, st.m),
-                           h->stream, bv, st, ts, h->k);
+                           h->stream, bv, tst, ts, h->k);
     } else {
         hipLaunchKernelGGL(asg::real_reset_kernel, dim3((unsigned)st.E), dim3(256), sizeof(int) * (size_t)st.m,
                            h->stream, st);
@@ -894,6 +919,7 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
     st.variant = cfg->variant;
     st.seed = cfg->seed;
     st.env_base = cfg->env_index_base;
+    st.bids = cfg->bids_as_actions ? 1 : 0;
     std::vector<double> hp(m, 1.0), ht((size_t)m * m), hn((size_t)m * m, 0.0);
     std::vector<int> hb(n, 0);
     if (cfg->task_prios) std::memcpy(hp.data(), cfg->task_prios, sizeof(double) * m);
@@ -917,6 +943,8 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
     if (e == hipSuccess) e = hipMalloc(&st.err, sizeof(int));
     if (e == hipSuccess) e = hipMemset(st.err, 0, sizeof(int));
     if (e == hipSuccess) e = hipMemset(st.returns, 0, sizeof(double) * (size_t)st.E);
+    if (e == hipSuccess && st.bids) e = hipMalloc(&h->bids_assign, sizeof(int64_t) * (size_t)st.E * n);
+    if (e == hipSuccess && st.bids) e = hipMalloc(&h->bids_status, sizeof(int32_t) * (size_t)st.E);
     if (e != hipSuccess) {
         asg_real_destroy(h);
         return rhip(nullptr, e, "asg_real_create");
@@ -942,6 +970,8 @@ void asg_real_destroy(asg_real_handle *h) {
     hipFree(h->st.err);
     hipFree(h->table_buf);
     hipFree(h->haal_ws);
+    hipFree(h->bids_assign);
+    hipFree(h->bids_status);
     delete h;
 }
 
@@ -1054,10 +1084,10 @@ int asg_real_sync_status(asg_real_handle *h) {
     hipError_t e = hipMemcpyAsync(&code, h->st.err, sizeof(int), hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return rhip(h, e, "asg_real_sync_status");
-    if (code == ASG_E_ACTION_RANGE) {
-        (void)hipMemsetAsync(h->st.err, 0, sizeof(int), h->stream);
-        return rfail(h, code, "action out of range [0, m)");
-    }
+    if (code != 0) (void)hipMemsetAsync(h->st.err, 0, sizeof(int), h->stream);
+    if (code == ASG_E_ACTION_RANGE) return rfail(h, code, "action out of range [0, m)");
+    if (code == ASG_E_LSA_INVALID) return rfail(h, code, "matrix contains invalid numeric entries");
+    if (code == ASG_E_LSA_INFEASIBLE) return rfail(h, code, "cost matrix is infeasible");
     return code ? rfail(h, code, "device error") : ASG_OK;
 }
 

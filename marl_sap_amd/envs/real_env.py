@@ -31,9 +31,10 @@ def obs_size(N, M, L, power=False):
     return M * L + N * M * L + (N * M // 2) * L + M + ((N + 1) if power else 0)
 
 
-def make_real_scheme(n, m, L, N, M, power=False):
+def make_real_scheme(n, m, L, N, M, power=False, bids_as_actions=False):
     """Scheme + preprocess (real_constellation_env.py:74-97, real_power_constellation_env.py:
-    95-116): half precision; the power variants add power_states."""
+    95-116): half precision; the power variants add power_states; bids_as_actions: float32
+    bids [m] per agent and no one-hot preprocess (real_constellation_env.py:110-112)."""
     scheme = {
         "obs": {"vshape": obs_size(N, M, L, power), "group": "agents", "dtype": torch.float16},
         "actions": {"vshape": (1,), "group": "agents", "dtype": torch.int16},
@@ -46,6 +47,9 @@ def make_real_scheme(n, m, L, N, M, power=False):
     if power:
         scheme["power_states"] = {"vshape": (n,), "dtype": torch.float16, "part_of_state": True}
     preprocess = {"actions": ("actions_onehot", [OneHot(out_dim=m)])}
+    if bids_as_actions:
+        scheme["actions"] = {"vshape": (m,), "group": "agents", "dtype": torch.float32}
+        preprocess = {}
     return scheme, preprocess
 
 
@@ -72,8 +76,6 @@ class RealAssignEnvBatch(MultiAgentEnv):
         if sat_prox_mat is None:
             raise ValueError("RealAssignEnvBatch needs sat_prox_mat (constant-benefit path); the orbital "
                              "simulator is not part of this build")
-        if bids_as_actions:
-            raise ValueError("bids_as_actions is not supported by the batched RealConstellationEnv")
         table = torch.as_tensor(np.asarray(sat_prox_mat, dtype=np.float64) if not torch.is_tensor(sat_prox_mat)
                                 else sat_prox_mat, dtype=torch.float64)
         if table.dim() == 3:
@@ -85,7 +87,9 @@ class RealAssignEnvBatch(MultiAgentEnv):
         self.n, self.m, self.T = int(table.shape[1]), int(table.shape[2]), int(table.shape[3])
         self.N, self.M, self.L = int(N), int(M), min(int(L), int(T))
         self.lambda_ = float(lambda_)
-        self.bids_as_actions = False
+        # bids_as_actions: each step solves LSA(bids, maximize) per env on the GPU (asg_lsa_batched's
+        # scipy-exact solver inside asg_real_step) -- real_constellation_env.py:140-142
+        self.bids_as_actions = bool(bids_as_actions)
         self.env_index_base = int(env_index_base)
         self._seed = seed
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
@@ -101,7 +105,8 @@ class RealAssignEnvBatch(MultiAgentEnv):
         self.neighbor_matrix = (None if neighbor_matrix is None
                                 else np.ascontiguousarray(neighbor_matrix, dtype=np.float64))
         self.obs_space_size = obs_size(self.N, self.M, self.L, power)
-        self.scheme, self.preprocess = make_real_scheme(self.n, self.m, self.L, self.N, self.M, power)
+        self.scheme, self.preprocess = make_real_scheme(self.n, self.m, self.L, self.N, self.M, power,
+                                                        self.bids_as_actions)
         self.k = 0
         cfg = _lib.AsgRealConfig()
         cfg.num_envs, cfg.n, cfg.m, cfg.T, cfg.L = self.num_envs, self.n, self.m, self.T, int(L)
@@ -110,6 +115,7 @@ class RealAssignEnvBatch(MultiAgentEnv):
         cfg.T_trans = self.T_trans.ctypes.data_as(dp)
         cfg.task_prios = self.task_prios.ctypes.data_as(dp)
         cfg.variant = self.VARIANT
+        cfg.bids_as_actions = int(self.bids_as_actions)
         cfg.seed = (0 if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF
         cfg.env_index_base = self.env_index_base
         if self.sat_freq_bands is not None:
@@ -162,7 +168,9 @@ class RealAssignEnvBatch(MultiAgentEnv):
 
     def step(self, batch, ts):
         """Reads actions at row ts; writes rewards / terminated / actions_onehot at ts and
-        the next pre-transition row (obs, beta, avail, prev_assigns, filled) at ts + 1."""
+        the next pre-transition row (obs, beta, avail, prev_assigns, filled) at ts + 1.
+        bids_as_actions: the actions row holds float32 bids [E, n, m] and the step's tasks are
+        LSA(bids, maximize) per env (a NaN / -inf bid raises scipy's ValueError at sync())."""
         self._call("asg_real_step", ctypes.byref(real_batch_view(batch)), int(ts))
         self.k += 1
         return self.k >= self.T

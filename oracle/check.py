@@ -78,3 +78,86 @@ def _cmp(got, want, what, atol=0.0, rtol=0.0):
             raise AssertionError(f"{what}: {len(bad)} mismatches, first at {i}: {got[i]!r} vs {want[i]!r}")
     else:
         np.testing.assert_allclose(got, want, rtol=rtol, atol=atol, err_msg=what)
+
+
+# ---- exhaustive replay (oracle/asg_check.c): every env of a GPU batch -------------------------
+import ctypes  # noqa: E402
+
+
+class _CheckCfg(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("m", ctypes.c_int), ("T", ctypes.c_int), ("L", ctypes.c_int),
+                ("lambda_", ctypes.c_double), ("quirks", ctypes.c_int), ("obs_atol", ctypes.c_double),
+                ("obs_rtol", ctypes.c_double), ("reward_rtol", ctypes.c_double), ("env_index0", ctypes.c_int64),
+                ("seed_check", ctypes.c_int), ("seed", ctypes.c_uint32), ("seed_rtol", ctypes.c_double)]
+
+
+def _check_lib():
+    L = ora.lib()
+    if not hasattr(L, "_chk_ready"):
+        vp = ctypes.c_void_p
+        L.ora_check_rollout.argtypes = [ctypes.POINTER(_CheckCfg), ctypes.c_int] + [vp] * 12 + \
+            [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong)]
+        L.ora_check_rollout.restype = ctypes.c_int
+        L._chk_ready = True
+    return L
+
+
+def check_threads():
+    """Worker threads for the checker: the box's CPU share (16 per GPU), not os.cpu_count()."""
+    import os
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(16, avail))
+
+
+def replay_all(n, m, T, L, lam, td, table, prev0, returns, quirks=(), philox=False, rtol_reward=0.0,
+               seed=None, env_chunk=None, threads=None):
+    """Replay EVERY env of a GPU batch on the oracle in C (asg_check.c), chunk by chunk.
+
+    td: the batch's transition tensors ({name: torch tensor [E, T+1, ...]} on the GPU, any layout);
+    table: torch float64 [E, n, m, T] (asg_export_benefits: the values the kernel used; in the Philox
+    mode its float64 evaluation of the bump parameters); prev0 [E, n] int64; returns [E] float64.
+    philox: obs / beta within the Philox float32 bump tolerance (PHILOX_ATOL / RTOL), else exact.
+    seed: the MT19937 same-seed mode -- every env's table (rtol 1e-12) and reset permutation are
+    also rebuilt from np.random.seed(seed + env).  Returns (envs checked, values compared); raises
+    AssertionError naming the first mismatch."""
+    import numpy as _np
+    E = int(table.shape[0])
+    W = m * (L + 1)
+    if env_chunk is None:  # ~3 GiB of float32 obs per chunk
+        env_chunk = max(1, min(E, (3 << 30) // (4 * (T + 1) * n * W)))
+    cfg = _CheckCfg(n, m, T, L, float(lam),
+                    (1 if "prev_assigns_zero" in quirks else 0) | (2 if "parallel_terminated" in quirks else 0),
+                    PHILOX_ATOL if philox else 0.0, PHILOX_RTOL if philox else 0.0, float(rtol_reward), 0,
+                    1 if seed is not None else 0, 0 if seed is None else int(seed) & 0xFFFFFFFF, 1e-12)
+    lib_ = _check_lib()
+    threads = threads or check_threads()
+    compared = 0
+
+    def host(t, dtype):
+        return _np.ascontiguousarray(t.contiguous().cpu().numpy(), dtype=dtype)
+
+    for e0 in range(0, E, env_chunk):
+        e1 = min(E, e0 + env_chunk)
+        cfg.env_index0 = e0
+        arr = {
+            "table": host(table[e0:e1], _np.float64), "prev0": host(prev0[e0:e1], _np.int64),
+            "obs": host(td["obs"][e0:e1], _np.float32), "beta": host(td["beta"][e0:e1], _np.float32),
+            "actions": host(td["actions"][e0:e1], _np.int64), "rewards": host(td["rewards"][e0:e1], _np.float32),
+            "onehot": host(td["actions_onehot"][e0:e1], _np.int64) if "actions_onehot" in td else None,
+            "term": host(td["terminated"][e0:e1], _np.uint8), "prevb": host(td["prev_assigns"][e0:e1], _np.int64),
+            "avail": host(td["avail_actions"][e0:e1], _np.uint8), "filled": host(td["filled"][e0:e1], _np.int64),
+            "returns": host(returns[e0:e1], _np.float64)}
+        msg = ctypes.create_string_buffer(512)
+        cnt = ctypes.c_longlong(0)
+        ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        fails = lib_.ora_check_rollout(
+            ctypes.byref(cfg), e1 - e0, ptr(arr["table"]), ptr(arr["prev0"]), ptr(arr["obs"]), ptr(arr["beta"]),
+            ptr(arr["actions"]), ptr(arr["rewards"]), ptr(arr["onehot"]), ptr(arr["term"]), ptr(arr["prevb"]),
+            ptr(arr["avail"]), ptr(arr["filled"]), ptr(arr["returns"]), threads, msg, 512, ctypes.byref(cnt))
+        assert fails == 0, f"{fails} of envs {e0}..{e1 - 1} differ from the oracle replay; first: {msg.value.decode()}"
+        compared += cnt.value
+        del arr
+    return E, compared

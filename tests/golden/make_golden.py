@@ -21,6 +21,7 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   runner_dumps.npz    EpisodeRunner / ParallelRunner EpisodeBatch dumps (layout + quirks)
   real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
   real_variants.npz   RealPowerConstellationEnv / InterferenceConstellationEnv reset/step
+  real_bids.npz       the real-env family with bids_as_actions (float32 bids -> scipy LSA) reset/step
   real_runner_dumps.npz  EpisodeRunner + BasicMAC EpisodeBatch dumps over RealConstellationEnv
   filtered_selectors.npz the filtered selectors' actions with their recorded random draws
   haal.npz            HAALSelector actions + every time-interval sequence's value
@@ -373,6 +374,90 @@ def gen_real_variants():
         out[f"v{idx}_power"] = np.stack(powers)
     out["n_cases"] = np.array(len(specs))
     np.savez_compressed(os.path.join(OUT, "real_variants.npz"), **out)
+
+
+def gen_real_bids():
+    """bids_as_actions on the real-env family (VERDICT r5 "Next" item 4): RealConstellationEnv,
+    RealPowerConstellationEnv and InterferenceConstellationEnv constructed with bids_as_actions
+    (the latter without the orbital simulator, as gen_real_variants), stepped with float32 bid
+    matrices -- the batch's float32 actions row -- so each step is scipy's
+    linear_sum_assignment(bids, maximize=True) (real_constellation_env.py:140-142,
+    real_power_constellation_env.py:142, interference_constellation_env.py:159).  Continuous
+    random bids (tie-free LSA) and strictly positive tables (tie-free argsort orders)."""
+    from collections import defaultdict
+    from envs.real_constellation_env import RealConstellationEnv
+    from envs.real_power_constellation_env import RealPowerConstellationEnv
+    from envs.interference_constellation_env import InterferenceConstellationEnv
+    rng = np.random.RandomState(2468)
+    out = {}
+    specs = [  # (variant, n, m, T, L, N, M, lambda)
+        ("real", 7, 12, 6, 3, 2, 4, 0.5), ("real", 12, 20, 5, 2, 3, 4, 0.3),
+        ("power", 8, 14, 9, 3, 3, 4, 0.5), ("interference", 9, 15, 8, 3, 3, 4, 0.4)]
+    for idx, (kind, n, m, T, L, N, M, lam) in enumerate(specs):
+        table = rng.uniform(0.01, 1.0, size=(n, m, T))
+        prios = rng.choice([1.0, 1.0, 1.0, 5.0], size=m) if kind != "real" else np.ones(m)
+        np.random.seed(700 + idx)
+        bands = np.zeros(n, dtype=np.int64)
+        nbr = np.eye(m, dtype=np.int64)
+        if kind == "real":
+            env = RealConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(), graphs=[None] * T,
+                                       bids_as_actions=True)
+        elif kind == "power":
+            env = RealPowerConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(), graphs=[None] * T,
+                                            task_prios=prios.copy(), bids_as_actions=True)
+        else:
+            env = object.__new__(InterferenceConstellationEnv)
+            env.n, env.m, env.T, env.N, env.M, env.L = n, m, T, N, M, min(L, T)
+            env.lambda_, env.beam_types, env.bids_as_actions = lam, 7, True
+            env.k, env.done, env.constant_setup = 0, False, True
+            env.sat_prox_mat = table.copy()
+            nbr = (rng.uniform(size=(m, m)) > 0.7).astype(np.int64)
+            nbr = np.maximum(nbr, nbr.T)
+            np.fill_diagonal(nbr, 1)
+            env.neighbor_matrix = nbr
+            bands = rng.randint(0, 3, size=n)
+            env.sat_freq_bands = bands
+            env.sat_freq_band_dict = defaultdict(list)
+            for i, b in enumerate(bands):
+                env.sat_freq_band_dict[b].append(i)
+            env.task_prios = np.repeat(np.tile(prios, (n, 1))[:, :, np.newaxis], env.L, axis=-1)
+            env.power_states = np.ones(n)
+        env.reset()
+        obs0, beta0 = np.array(env._obs), np.asarray(env.beta).copy()
+        prev0 = np.asarray(env.prev_assigns, dtype=np.int64).copy()
+        bids_l, rews, obs, betas, dones, prevs, powers = [], [], [], [], [], [], []
+        for t in range(T):
+            bids = rng.uniform(0.0, 1.0, size=(n, m)).astype(np.float32)
+            if t % 3 == 1:  # a few columns everyone wants: contested LSA rows
+                bids[:, :2] += 1.0
+            r, d, info = env.step(bids)
+            bids_l.append(bids)
+            rews.append(np.asarray(r, dtype=np.float64))
+            obs.append(np.array(env._obs))
+            betas.append(np.asarray(env.beta).copy())
+            dones.append(bool(d))
+            prevs.append(np.asarray(env.prev_assigns, dtype=np.int64))
+            powers.append(np.asarray(getattr(env, "power_states", np.ones(n)), dtype=np.float64).copy())
+        out[f"b{idx}_kind"] = np.array(kind)
+        out[f"b{idx}_spec"] = np.array([n, m, T, env.L, N, M])
+        out[f"b{idx}_lambda"] = np.array(lam)
+        out[f"b{idx}_table"] = table
+        out[f"b{idx}_prios"] = prios
+        out[f"b{idx}_bands"] = np.asarray(bands, dtype=np.int64)
+        out[f"b{idx}_nbr"] = np.asarray(nbr, dtype=np.float64)
+        out[f"b{idx}_obs_size"] = np.array(env.get_obs_size())
+        out[f"b{idx}_obs0"] = obs0
+        out[f"b{idx}_beta0"] = beta0
+        out[f"b{idx}_prev0"] = prev0
+        out[f"b{idx}_bids"] = np.stack(bids_l)
+        out[f"b{idx}_rewards"] = np.stack(rews)
+        out[f"b{idx}_obs"] = np.stack(obs)
+        out[f"b{idx}_beta"] = np.stack(betas)
+        out[f"b{idx}_done"] = np.array(dones)
+        out[f"b{idx}_prev"] = np.stack(prevs)
+        out[f"b{idx}_power"] = np.stack(powers)
+    out["n_cases"] = np.array(len(specs))
+    np.savez_compressed(os.path.join(OUT, "real_bids.npz"), **out)
 
 
 def gen_lsa():
@@ -853,6 +938,9 @@ if __name__ == "__main__":
         gen_real_variants()
         gen_real_runner_dumps()
         sys.exit(0)
+    if sys.argv[1:] == ["round6"]:  # bids_as_actions on the real-env family (round 6)
+        gen_real_bids()
+        sys.exit(0)
     if sys.argv[1:] == ["yaml"]:  # the reference's unchanged mock algorithm configs (round 4)
         gen_yaml_runner_dumps()
         sys.exit(0)
@@ -863,6 +951,7 @@ if __name__ == "__main__":
         sys.exit(0)
     gen_real_env()
     gen_real_variants()
+    gen_real_bids()
     gen_mt_words()
     gen_mock_reset()
     gen_mock_step()

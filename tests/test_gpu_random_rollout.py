@@ -17,7 +17,7 @@ if not torch.cuda.is_available():  # collected on CPU, but never run there
 
 from marl_sap_amd.components import EpisodeBatch  # noqa: E402
 from marl_sap_amd.envs import AssignEnvBatch  # noqa: E402
-from oracle.check import replay_and_compare  # noqa: E402
+from oracle.check import replay_all, replay_and_compare  # noqa: E402
 
 DEV = torch.device("cuda", 0)
 
@@ -129,3 +129,8 @@ def test_random_rollout_full_size_configs1():
     table = env.export_benefits()[idx].cpu().numpy()
     td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
     replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy(), philox=True)
+    # and every env on the C replay (oracle/asg_check.c)
+    envs, compared = replay_all(n, m, T, L, 0.5, b.data.transition_data, env.export_benefits(), prev0, r,
+                                philox=True)
+    assert envs == E
+    print(f"exhaustive oracle replay: {envs} envs, {compared} values compared")

@@ -11,7 +11,9 @@ as bench.make_args does, run one whole episode through runner.run(), and check:
     filled / terminated / prev_assigns, returns == sum of rewards);
   * sampled envs (first, last, one inside each wave stride): a full replay of the env on
     the C oracle (mock_constellation_env.py:116-162 semantics: rewards, obs, beta, one-hots,
-    returns) from the episode's exported bump parameters;
+    returns) from the episode's exported bump parameters (numpy float64);
+  * EVERY env: the same replay in C over all envs (oracle/asg_check.c, multi-threaded, env
+    chunks) from the handle's float64 export of those parameters;
   * the same sampled envs' actions: the PyTorch RNNAgent module (the reference's
     rnn_agent.py:23-31, fp32, same weights) replayed over the batch's observation rows gives
     Q_t; rows whose Philox draw explores (oracle/philox.py, the kernel's draw restated) must
@@ -40,7 +42,7 @@ import bench  # noqa: E402
 from marl_sap_amd.controllers import REGISTRY as MAC  # noqa: E402
 from marl_sap_amd.modules.agents import RNNAgent  # noqa: E402
 from marl_sap_amd.runners import REGISTRY as RUN  # noqa: E402
-from oracle.check import bump_table_from_params, replay_and_compare  # noqa: E402
+from oracle.check import bump_table_from_params, replay_all, replay_and_compare  # noqa: E402
 from oracle.philox import eps_greedy_draws  # noqa: E402
 
 DEV = torch.device("cuda", 0)
@@ -153,6 +155,14 @@ def test_bench_workload_episode_vs_oracle(config):
         td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
         replay_and_compare(n, m, T, L, 0.5, table, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy(),
                            philox=True, rtol_reward=2e-7 if m > 64 else 0.0)
+        # the sampled envs' float64 tables from their bump parameters (numpy) equal the handle's
+        # own export; then EVERY env replayed on the C oracle from that export (asg_check.c)
+        full = env.export_benefits()
+        np.testing.assert_allclose(full[torch.as_tensor(idx, device=DEV)].cpu().numpy(), table, rtol=4e-16, atol=0)
+        envs, compared = replay_all(n, m, T, L, 0.5, b.data.transition_data, full, prev0, r, philox=True,
+                                    rtol_reward=2e-7 if m > 64 else 0.0)
+        print(f"exhaustive oracle replay: {envs} envs, {compared} values compared")
+        del full
         sel = mac.action_selector
         _check_actions(b, mac, idx, n, m, T, float(sel.epsilon), sel.seed, sel.calls - T)
     finally:
@@ -204,6 +214,11 @@ def test_compat_mode_configs2_episode_vs_oracle():
         np.testing.assert_allclose(dev_tab, np.stack(tables), rtol=1e-12, atol=0)
         td = {k: v[idx].cpu().numpy() for k, v in b.data.transition_data.items()}
         replay_and_compare(n, m, T, L, 0.5, dev_tab, prev0[idx].cpu().numpy(), td, r[idx].cpu().numpy())
+        # EVERY env: its table and permutation rebuilt from np.random.seed(seed + e) alone, and
+        # every batch row replayed exactly (asg_check.c)
+        envs, compared = replay_all(n, m, T, L, 0.5, b.data.transition_data, env.export_benefits(), prev0, r,
+                                    seed=a.seed)
+        print(f"exhaustive same-seed replay: {envs} envs, {compared} values compared")
         sel = mac.action_selector
         _check_actions(b, mac, idx, n, m, T, float(sel.epsilon), sel.seed, sel.calls - T)
     finally:
