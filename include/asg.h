@@ -506,12 +506,15 @@ int asg_real_get_step(const asg_real_handle *h, int *k_out);
 /* get_obs_size (real_constellation_env.py:251-253): M*L + N*M*L + (N*M//2)*L + M; the
  * power variants add N + 1 (real_power_constellation_env.py:286-290) */
 int asg_real_obs_size(int N, int M, int L);
-/* HAALSelector (non_rl_selectors.py:54-118) on every env of a plain-variant handle at its
+/* HAALSelector (non_rl_selectors.py:54-118) on every env of the handle (any variant) at its
  * current step k: for each time-interval sequence of the window eff = min(L, T - k)
  * (build_time_interval_sequences, utils/methods.py:309-349; S = 2^(eff-1) sequences in the
  * reference's order, eff <= 6) the env is forked, and per interval LSA(maximize) of
  * beta_hat summed over L (float64, numpy's order) is stepped interval-length times; a
- * sequence's value is the sum of the steps' sum(rewards).  The action is the first
+ * sequence's value is the sum of the steps' sum(rewards).  Power / interference variants: the
+ * fork carries the power states (drained / recharged by its own steps,
+ * real_power_constellation_env.py:170-178), beta_hat rows below 1e-12 power are zero (:343-347)
+ * and each step pays the variant's reward (interference_constellation_env.py:309-353).  The action is the first
  * interval's assignment of the first best sequence (col_out [E][n] float32 task ids, the
  * selector's float picked_actions).  values_out [E][S] float64, best_out [E] int32 (index of
  * the winning sequence) and status_out [E] int32 (0 or the scipy error code of any LSA of

@@ -225,6 +225,83 @@ __device__ __forceinline__ void wave_topk(const double *vals, int len, int K, in
     wave_sync();
 }
 
+// ---- one step's rewards and power update of one env (block-wide; every thread calls) -----
+// The variants' reward rules, shared by the transition kernel and HAAL's sequence values:
+//   plain / power  beta_hat[i, a_i, 0] / count(a_i), or the full penalty when beta_hat <= 0
+//                  (real_constellation_env.py:145-160); power: 0 for a dead satellite, beta_hat
+//                  zeroed below 1e-12 power (real_power_constellation_env.py:150-165, :343-347)
+//   interference   beta[i, a_i, 0] * 0.5 ** conflicts / count over applicable agents, minus
+//                  lambda on a handover (interference_constellation_env.py:309-353)
+// sa [n] this step's tasks, prevp(i) the previous task of agent i, pw [n] power (power
+// variants), LDS scnt [m], sapp [n]; rewards into srew [n].
+template <class PrevF>
+__device__ __forceinline__ void real_step_rewards(const RealState &st, const double *tab, int k, const int *sa,
+                                                  PrevF prevp, const double *pw, int *scnt, int *sapp,
+                                                  double *srew) {
+    const int n = st.n, m = st.m, L = st.L;
+    for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
+    __syncthreads();
+    if (st.variant == ASG_REAL_INTERFERENCE) {
+        // applicable = alive and on a meaningful task; counts over applicable agents only
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            sapp[i] = (pw[i] <= 0 ? 0 : 1) * (real_beta(st, tab, k, i, sa[i], 0) < 1e-12 ? 0 : 1);
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            if (sapp[i]) atomicAdd(&scnt[sa[i]], 1);
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[sa[i]], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int c = sa[i];
+        const int pv = prevp(i);
+        double r;
+        if (st.variant == ASG_REAL_INTERFERENCE) {
+            // conflicts = sum over the agents of i's band of nbr[a_i, a_j] * applicable_j - 1
+            // (interference_constellation_env.py:327-331), then 0.5 ** conflicts
+            double conf = 0.0;
+            const int band = st.bands[i];
+            for (int a = 0; a < n; ++a)
+                if (st.bands[a] == band) conf = conf + st.nbr[(int64_t)c * m + sa[a]] * (double)sapp[a];
+            conf = conf - 1.0;
+            r = real_beta(st, tab, k, i, c, 0) * pow(0.5, conf);
+            if (scnt[c] > 0) r = r / (double)scnt[c];
+            if (sapp[i] && pv != c) r = r - st.lambda_;
+        } else if (st.variant == ASG_REAL_POWER && !(pw[i] > 0)) {
+            r = 0.0;  // dead satellite (real_power_constellation_env.py:161-162)
+        } else {
+            double bh;
+            if (st.variant == ASG_REAL_POWER && pw[i] < 1e-12) {
+                bh = 0.0;  // beta_hat zeroed below 1e-12 power (:343-347)
+            } else {
+                double s = real_beta(st, tab, k, i, c, 0);
+                const double b0 = s;
+                for (int l = 1; l < L; ++l) s = s + real_beta(st, tab, k, i, c, l);
+                const double cond = s > 1e-12 ? 1.0 : 0.0;
+                const double pen = st.T_trans[(int64_t)pv * m + c] * cond;
+                bh = b0 - st.lambda_ * pen;
+            }
+            r = bh > 0 ? bh / (double)scnt[c] : bh;
+        }
+        srew[i] = r;
+    }
+}
+
+// power update on the pre-step beta (real_power_constellation_env.py:170-178); the caller
+// syncs before (every reader of the old power is done)
+__device__ __forceinline__ void real_power_update(const RealState &st, const double *tab, int k, const int *sa,
+                                                  double *pw) {
+    for (int i = threadIdx.x; i < st.n; i += blockDim.x)
+        if (pw[i] > 0) {
+            if (real_beta(st, tab, k, i, sa[i], 0) > 1e-12) {
+                pw[i] -= 0.2;
+            } else {
+                const double p = pw[i] + 0.1;
+                pw[i] = p < 1.0 ? p : 1.0;
+            }
+        }
+}
+
 // ---- kernel 1: the transition of each env (step only), one workgroup per env ---------------
 // LDS: actions [n] int, counts [m] int, rewards [n] f64, applicable [n] int
 __host__ __device__ __forceinline__ size_t transition_lds(int n, int m) {
@@ -234,7 +311,7 @@ __host__ __device__ __forceinline__ size_t transition_lds(int n, int m) {
 __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv, RealState st, int ts, int k) {
     extern __shared__ unsigned char s_raw[];
     const int64_t e = blockIdx.x;
-    const int n = st.n, m = st.m, L = st.L;
+    const int n = st.n, m = st.m;
     int *sa = reinterpret_cast<int *>(s_raw);                                        // [n]
     int *scnt = sa + n;                                                              // [m]
     double *srew = reinterpret_cast<double *>(scnt + m + (((n + m) & 1) ? 1 : 0));  // [n], 8-B aligned
@@ -252,66 +329,14 @@ __global__ void __launch_bounds__(256) real_transition_kernel(asg_batch_view bv,
         }
         sa[i] = (int)a;
     }
-    for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
-    __syncthreads();
     double *pw = st.power + e * n;
     int *sapp = reinterpret_cast<int *>(srew + n);  // [n] applicable (interference)
-    if (st.variant == ASG_REAL_INTERFERENCE) {
-        // applicable = alive and on a meaningful task; counts over applicable agents only
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            sapp[i] = (pw[i] <= 0 ? 0 : 1) * (real_beta(st, tab, k, i, sa[i], 0) < 1e-12 ? 0 : 1);
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            if (sapp[i]) atomicAdd(&scnt[sa[i]], 1);
-    } else {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&scnt[sa[i]], 1);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int c = sa[i];
-        double r;
-        if (st.variant == ASG_REAL_INTERFERENCE) {
-            // conflicts = sum over the agents of i's band of nbr[a_i, a_j] * applicable_j - 1
-            // (interference_constellation_env.py:327-331), then 0.5 ** conflicts
-            double conf = 0.0;
-            const int band = st.bands[i];
-            for (int a = 0; a < n; ++a)
-                if (st.bands[a] == band) conf = conf + st.nbr[(int64_t)c * m + sa[a]] * (double)sapp[a];
-            conf = conf - 1.0;
-            r = real_beta(st, tab, k, i, c, 0) * pow(0.5, conf);
-            if (scnt[c] > 0) r = r / (double)scnt[c];
-            if (sapp[i] && prev[i] != c) r = r - st.lambda_;
-        } else if (st.variant == ASG_REAL_POWER && !(pw[i] > 0)) {
-            r = 0.0;  // dead satellite (real_power_constellation_env.py:161-162)
-        } else {
-            double bh;
-            if (st.variant == ASG_REAL_POWER && pw[i] < 1e-12) {
-                bh = 0.0;  // beta_hat zeroed below 1e-12 power (:343-347)
-            } else {
-                double s = real_beta(st, tab, k, i, c, 0);
-                const double b0 = s;
-                for (int l = 1; l < L; ++l) s = s + real_beta(st, tab, k, i, c, l);
-                const double cond = s > 1e-12 ? 1.0 : 0.0;
-                const double pen = st.T_trans[(int64_t)prev[i] * m + c] * cond;
-                bh = b0 - st.lambda_ * pen;
-            }
-            r = bh > 0 ? bh / (double)scnt[c] : bh;
-        }
-        srew[i] = r;
-        if (bv.rewards.ptr) store_real(bv.rewards, foff(bv.rewards, e, ts, i, 0), r);
-    }
+    real_step_rewards(st, tab, k, sa, [&](int i) { return prev[i]; }, pw, scnt, sapp, srew);
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (bv.rewards.ptr) store_real(bv.rewards, foff(bv.rewards, e, ts, i, 0), srew[i]);
     if (st.variant != ASG_REAL_PLAIN) {
         __syncthreads();  // every reader of the old power is done
-        // power update on the pre-step beta (real_power_constellation_env.py:170-178)
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            if (pw[i] > 0) {
-                if (real_beta(st, tab, k, i, sa[i], 0) > 1e-12) {
-                    pw[i] -= 0.2;
-                } else {
-                    const double p = pw[i] + 0.1;
-                    pw[i] = p < 1.0 ? p : 1.0;
-                }
-            }
+        real_power_update(st, tab, k, sa, pw);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -598,11 +623,14 @@ __global__ void real_table_transpose_kernel(const double *src, double *dst, int6
 // ---- HAALSelector (action_selectors/non_rl_selectors.py:54-118) ---------------------------
 // The reference forks (deepcopy) every env once per time-interval sequence of the lookahead
 // window, and per interval solves scipy's LSA on beta_hat summed over L and steps the fork
-// interval-length times.  A fork's state is (step, previous assignment): the benefits are the
-// constant table.  Sequences share prefixes, so the distinct LSA states form a tree of
-// decision nodes (decision time t, the assignment in force before it = the parent node's):
-// 2^(eff-1) nodes, solved level by level as batched LSAs over all envs, then every
-// sequence's value is the reference's sum of per-step reward sums.
+// interval-length times.  A fork's state is (step, previous assignment, and in the power /
+// interference variants the power states, drained or recharged by every step the fork takes:
+// real_power_constellation_env.py:137-191): the benefits are the constant table.  Sequences
+// share prefixes, so the distinct LSA states form a tree of decision nodes (decision time t,
+// the assignment in force before it = the parent node's, the power replayed along the
+// ancestors' steps): 2^(eff-1) nodes, solved level by level as batched LSAs over all envs,
+// then every sequence's value is the reference's sum of per-step reward sums (each variant's
+// own reward rule, real_step_rewards).
 constexpr int kHaalMaxL = 6;                     // 2^(6-1) = 32 nodes / sequences
 struct HaalPlan {
     int nodes, seqs, eff;
@@ -613,7 +641,11 @@ struct HaalPlan {
 };
 
 // total beta_hat of one (node, env, agent) row: ((b0 - lambda * pen) + b1) + ... in numpy's
-// order (real_constellation_env.py:309-326, then .sum(axis=-1) left to right)
+// order (real_constellation_env.py:309-326, then .sum(axis=-1) left to right).  Power variants
+// (real_power_constellation_env.py:310-352, interference_constellation_env.py:355-406): the
+// agent's power at the node's decision time, replayed from the env's along the ancestors'
+// assignments; a row below 1e-12 power is all zeros; the interference variant's penalty mask is
+// 1 - I whatever T_trans (interference_constellation_env.py:384).
 __global__ void __launch_bounds__(256) haal_matrix_kernel(RealState st, int k, HaalPlan plan, int node0, int nodes,
                                                           const int64_t *assign, double *mats) {
     const int lane = threadIdx.x & 63;
@@ -628,18 +660,48 @@ __global__ void __launch_bounds__(256) haal_matrix_kernel(RealState st, int k, H
     const int prev = par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i];
     const double *tab = st.table + e * st.table_env_stride;
     double *row = mats + gr * m;
-    if (prev < 0 || prev >= m) {
+    bool poison = prev < 0 || prev >= m;
+    bool dead = false;
+    if (!poison && st.variant != ASG_REAL_PLAIN) {
+        // the power this fork reaches at time t: the env's, then every step of the ancestors'
+        // intervals (node chain root .. parent, each in force until its child's decision time)
+        int chain[kHaalMaxL];
+        int d = 0;
+        for (int x = node; x >= 0 && d < kHaalMaxL; x = plan.node_parent[x]) chain[d++] = x;
+        double p = st.power[e * n + i];
+        for (int c = d - 1; c >= 1 && !poison; --c) {
+            const int anc = chain[c];
+            const int ai = (int)assign[((int64_t)anc * st.E + e) * n + i];
+            if (ai < 0 || ai >= m) { poison = true; break; }
+            for (int s2 = plan.node_t[anc]; s2 < plan.node_t[chain[c - 1]]; ++s2)
+                if (p > 0) {  // real_power_update
+                    if (real_beta(st, tab, k + s2, i, ai, 0) > 1e-12) {
+                        p -= 0.2;
+                    } else {
+                        const double q = p + 0.1;
+                        p = q < 1.0 ? q : 1.0;
+                    }
+                }
+        }
+        dead = p < 1e-12;  // np.where(sats_out_of_power, 0, beta_hat)
+    }
+    if (poison) {
         // the parent node's LSA failed (its assignment is -1 rows): poison this row so the
         // node's LSA reports invalid entries too, never index T_trans with it
         for (int j = lane; j < m; j += 64) row[j] = __builtin_nan("");
         return;
     }
+    if (dead) {
+        for (int j = lane; j < m; j += 64) row[j] = 0.0;
+        return;
+    }
+    const bool eye = st.variant == ASG_REAL_INTERFERENCE;
     for (int j = lane; j < m; j += 64) {
         double s = real_beta(st, tab, k + t, i, j, 0);
         const double b0 = s;
         for (int l = 1; l < st.L; ++l) s = s + real_beta(st, tab, k + t, i, j, l);
         const double cond = s > 1e-12 ? 1.0 : 0.0;
-        const double pen = st.T_trans[(int64_t)prev * m + j] * cond;
+        const double pen = (eye ? (prev != j ? 1.0 : 0.0) : st.T_trans[(int64_t)prev * m + j]) * cond;
         double tot = b0 - st.lambda_ * pen;
         for (int l = 1; l < st.L; ++l) tot = tot + real_beta(st, tab, k + t, i, j, l);
         row[j] = tot;
@@ -647,59 +709,64 @@ __global__ void __launch_bounds__(256) haal_matrix_kernel(RealState st, int k, H
 }
 
 // value of every (env, sequence): sum over its steps of Python's sum(rewards) (agent order,
-// float64), one workgroup per (sequence, env); then (sequence 0's workgroup, after all are
-// done in a second launch) the best sequence per env
+// float64), one workgroup per (sequence, env), each step by the variant's own reward rule and,
+// in the power variants, the fork's power carried from step to step; then (a second launch)
+// the best sequence per env
+__host__ __device__ __forceinline__ size_t haal_values_lds(int n, int m) {
+    return (size_t)16 * n + (size_t)4 * (3 * n + m) + 16;  // rewards, power | tasks, prev, applicable, counts, flag
+}
+
 __global__ void __launch_bounds__(256) haal_values_kernel(RealState st, int k, HaalPlan plan, const int64_t *assign,
                                                           double *values) {
-    extern __shared__ double s_rew[];  // [n] rewards, then [m] int counts
-    int *scnt = reinterpret_cast<int *>(s_rew + st.n);
+    extern __shared__ double s_rew[];  // [n] rewards, [n] power, then ints: [n] tasks, [n] prev, [n] applicable, [m] counts
+    const int n = st.n, m = st.m;
+    double *spw = s_rew + n;
+    int *sa = reinterpret_cast<int *>(spw + n);
+    int *sp = sa + n, *sapp = sp + n, *scnt = sapp + n;
+    int *sbad = scnt + m;
     const int s = blockIdx.x % plan.seqs;
     const int64_t e = blockIdx.x / plan.seqs;
-    const int n = st.n, m = st.m;
     const double *tab = st.table + e * st.table_env_stride;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) spw[i] = st.variant != ASG_REAL_PLAIN ? st.power[e * n + i] : 1.0;
     double tot = 0.0;
-    for (int iv = 0; iv < plan.seq_len[s]; ++iv) {
+    bool bad = false;
+    for (int iv = 0; iv < plan.seq_len[s] && !bad; ++iv) {
         const int node = plan.seq_node[s][iv];
         const int t0 = plan.node_t[node];
         const int t1 = iv + 1 < plan.seq_len[s] ? plan.node_t[plan.seq_node[s][iv + 1]] - 1 : plan.eff - 1;
         const int64_t *A = assign + ((int64_t)node * st.E + e) * n;
         const int par = plan.node_parent[node];
         for (int t = t0; t <= t1; ++t) {
-            for (int j = threadIdx.x; j < m; j += blockDim.x) scnt[j] = 0;
-            __syncthreads();
-            for (int i = threadIdx.x; i < n; i += blockDim.x) {
-                const int c = (int)A[i];
-                if (c >= 0 && c < m) atomicAdd(&scnt[c], 1);
-            }
+            if (threadIdx.x == 0) *sbad = 0;
             __syncthreads();
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
                 // the previous assignment: the parent's on the interval's first step, then A
                 const int p = t > t0 ? (int)A[i]
                                      : (par < 0 ? st.prev[e * n + i] : (int)assign[((int64_t)par * st.E + e) * n + i]);
                 const int c = (int)A[i];
-                if (c < 0 || c >= m || p < 0 || p >= m) {
-                    // a failed LSA upstream (-1 assignment rows): the sequence's value is NaN
-                    // and the env's status carries the LSA error
-                    s_rew[i] = __builtin_nan("");
-                    continue;
-                }
-                double sum = real_beta(st, tab, k + t, i, c, 0);
-                const double b0 = sum;
-                for (int l = 1; l < st.L; ++l) sum = sum + real_beta(st, tab, k + t, i, c, l);
-                const double cond = sum > 1e-12 ? 1.0 : 0.0;
-                const double bh = b0 - st.lambda_ * (st.T_trans[(int64_t)p * m + c] * cond);
-                s_rew[i] = bh > 0 ? bh / (double)scnt[c] : bh;
+                sa[i] = c;
+                sp[i] = p;
+                if (c < 0 || c >= m || p < 0 || p >= m) *sbad = 1;
             }
+            __syncthreads();
+            if (*sbad) {
+                // a failed LSA upstream (-1 assignment rows): the sequence's value is NaN and
+                // the env's status carries the LSA error
+                bad = true;
+                break;
+            }
+            real_step_rewards(st, tab, k + t, sa, [&](int i) { return sp[i]; }, spw, scnt, sapp, s_rew);
             __syncthreads();
             if (threadIdx.x == 0) {
                 double r = 0.0;
                 for (int i = 0; i < n; ++i) r += s_rew[i];  // sum(rewards), left to right
                 tot += r;                                   // total_tis_value += sum(rewards)
             }
+            if (st.variant != ASG_REAL_PLAIN) real_power_update(st, tab, k + t, sa, spw);
             __syncthreads();
         }
     }
-    if (threadIdx.x == 0) values[e * plan.seqs + s] = tot;
+    if (threadIdx.x == 0) values[e * plan.seqs + s] = bad ? __builtin_nan("") : tot;
 }
 
 // per env: the first sequence with the largest value (strict >), its first-interval
@@ -1160,8 +1227,6 @@ int asg_real_haal_select(asg_real_handle *h, float *col_out, double *values_out,
     if (!h || !col_out) return rfail(h, ASG_E_INVALID_ARG, "NULL handle or output");
     if (!h->has_reset) return rfail(h, ASG_E_STATE, "asg_real_haal_select before asg_real_reset");
     const asg::RealState &st = h->st;
-    if (st.variant != ASG_REAL_PLAIN)
-        return rfail(h, ASG_E_INVALID_ARG, "asg_real_haal_select: RealConstellationEnv (plain variant) only");
     const int eff = std::min(st.L, st.T - h->k);
     if (eff <= 0) return rfail(h, ASG_E_STATE, "asg_real_haal_select: the episode is done");
     if (eff > asg::kHaalMaxL) return rfail(h, ASG_E_INVALID_ARG, "asg_real_haal_select: lookahead window > 6");
@@ -1227,7 +1292,7 @@ int asg_real_haal_select(asg_real_handle *h, float *col_out, double *values_out,
     }
     if (e == hipSuccess) {
         hipLaunchKernelGGL(asg::haal_values_kernel, dim3((unsigned)(E * plan.seqs)), dim3(256),
-                           sizeof(double) * n + sizeof(int) * m, h->stream, st, h->k, plan, assign, values);
+                           asg::haal_values_lds(n, m), h->stream, st, h->k, plan, assign, values);
         e = hipGetLastError();
     }
     int32_t *st_env = lsa_st;  // reduced in place into the first E words (row e is env e of level 0)

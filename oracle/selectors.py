@@ -148,3 +148,92 @@ def haal(table, prios, T_trans, lam, k, prev, L, T):
         if tot > best:
             best, best_a = tot, first
     return best_a, np.array(vals)
+
+
+def variant_beta_hat(kind, beta, prev, lam, T_trans, power):
+    """RealPowerConstellationEnv.beta_hat (real_power_constellation_env.py:310-352) /
+    InterferenceConstellationEnv.beta_hat (interference_constellation_env.py:355-406, its penalty
+    mask is 1 - I whatever T_trans) for one state: the plain beta_hat, rows of satellites below
+    1e-12 power zeroed."""
+    n, m, _ = beta.shape
+    tt = np.ones((m, m)) - np.eye(m) if kind == "interference" else T_trans
+    bh = real_beta_hat(beta, prev, lam, tt)
+    dead = np.asarray(power) < 1e-12
+    bh[dead] = 0.0
+    return bh
+
+
+def variant_rewards(kind, beta, prev, a, lam, T_trans, power, bands=None, nbr=None):
+    """One step's rewards: RealPowerConstellationEnv.step (:145-165) or
+    InterferenceConstellationEnv.interference_reward_function (:309-353)."""
+    n, m, _ = beta.shape
+    power = np.asarray(power)
+    if kind == "power":
+        cnt = np.zeros(m)
+        for i in range(n):
+            cnt[a[i]] += 1
+        bh = variant_beta_hat(kind, beta, prev, lam, T_trans, power)
+        r = []
+        for i in range(n):
+            if power[i] > 0:
+                v = bh[i, a[i], 0]
+                r.append(v / cnt[a[i]] if v > 0 else v)
+            else:
+                r.append(0)
+        return r
+    app = np.where(power <= 0, 0, 1) * np.where(beta[:, :, 0][np.arange(n), a] < 1e-12, 0, 1)
+    cnt = np.zeros(m)
+    for i in range(n):
+        if app[i] == 1:
+            cnt[a[i]] += 1
+    r = []
+    for i in range(n):
+        same = [j for j in range(n) if bands[j] == bands[i]]
+        conflicts = np.sum(nbr[a[i], a[same]] * app[same]) - 1
+        v = beta[i, a[i], 0] * 0.5 ** conflicts
+        if cnt[a[i]] > 0:
+            v /= cnt[a[i]]
+        if app[i] and prev[i] != a[i]:
+            v -= lam
+        r.append(v)
+    return r
+
+
+def power_update(beta, a, power):
+    """The power drain / recharge of one step (real_power_constellation_env.py:170-178)."""
+    p = np.array(power, dtype=np.float64)
+    for i in range(len(p)):
+        if p[i] > 0:
+            if beta[i, a[i], 0] > 1e-12:
+                p[i] -= 0.2
+            else:
+                p[i] = min(p[i] + 0.1, 1)
+    return p
+
+
+def haal_variant(kind, table, prios, T_trans, lam, k, prev, power, L, T, bands=None, nbr=None):
+    """HAALSelector (non_rl_selectors.py:54-118) over a power / interference env at step k with
+    previous assignments `prev` and power states `power`: each sequence forks the env (power
+    included), per interval LSA(maximize) of beta_hat (power-zeroed) summed over L, stepped
+    interval-length times with the variant's rewards and power updates.  Returns (action,
+    values per sequence)."""
+    eff = min(L, T - k)
+    seqs = time_interval_sequences(eff)
+    best, best_a, vals = -np.inf, None, []
+    for tis in seqs:
+        kk, pv, pw, tot, first = k, np.asarray(prev), np.array(power, dtype=np.float64), 0, None
+        for ti in tis:
+            beta = real_beta(table, prios, kk, L, T)
+            bh = variant_beta_hat(kind, beta, pv, lam, T_trans, pw)
+            a = ora.lsa(bh.sum(axis=-1), maximize=True)[1]
+            if first is None:
+                first = a
+            for _ in range(ti[1] - ti[0] + 1):
+                beta = real_beta(table, prios, kk, L, T)
+                tot += sum(variant_rewards(kind, beta, pv, a, lam, T_trans, pw, bands, nbr))
+                pw = power_update(beta, a, pw)
+                kk, pv = kk + 1, a
+        vals.append(tot)
+        if tot > best:
+            best, best_a = tot, first
+    return best_a, np.array(vals)

@@ -22,6 +22,7 @@ Fixture files (all arrays, loaded with numpy.load(allow_pickle=False)):
   real_env.npz        RealConstellationEnv (injected benefits) reset/step: obs, beta, rewards
   real_variants.npz   RealPowerConstellationEnv / InterferenceConstellationEnv reset/step
   real_bids.npz       the real-env family with bids_as_actions (float32 bids -> scipy LSA) reset/step
+  haal_variants.npz   HAALSelector over the power / interference envs (forks carry power states)
   real_runner_dumps.npz  EpisodeRunner + BasicMAC EpisodeBatch dumps over RealConstellationEnv
   filtered_selectors.npz the filtered selectors' actions with their recorded random draws
   haal.npz            HAALSelector actions + every time-interval sequence's value
@@ -880,6 +881,108 @@ def gen_haal():
     np.savez_compressed(os.path.join(OUT, "haal.npz"), **out)
 
 
+def gen_haal_variants():
+    """HAALSelector (non_rl_selectors.py:54-118) over RealPowerConstellationEnv and
+    InterferenceConstellationEnv (VERDICT r5 "Next" item 8): the selector deep-copies the env --
+    power states included -- and steps the copies, so forks drain / recharge power
+    (real_power_constellation_env.py:170-178) and see power-zeroed beta_hat rows (:343-347).
+    The reference's own selector after `pre` steps (some satellites dead or below 1e-12 power),
+    plus every sequence's value by the selector's own deepcopy + get_state + step loop."""
+    import copy
+    from collections import defaultdict
+    import torch as th
+    from envs.real_power_constellation_env import RealPowerConstellationEnv
+    from envs.interference_constellation_env import InterferenceConstellationEnv
+    from action_selectors.non_rl_selectors import HAALSelector
+    from utils.methods import generate_all_time_intervals, build_time_interval_sequences
+    import scipy.optimize as so
+    rng = np.random.RandomState(1357)
+    out = {}
+    # (variant, n, m, T, L, N, M, lambda, steps before the selection)
+    specs = [("power", 7, 12, 10, 3, 2, 4, 0.5, 5), ("power", 8, 14, 10, 4, 2, 4, 0.3, 4),
+             ("power", 6, 10, 9, 3, 2, 4, 0.5, 0), ("interference", 8, 13, 9, 3, 2, 4, 0.4, 5),
+             ("interference", 9, 15, 8, 4, 3, 4, 0.5, 2)]
+    for idx, (kind, n, m, T, L, N, M, lam, pre) in enumerate(specs):
+        B = 3
+        prios = rng.choice([1.0, 1.0, 1.0, 5.0], size=m)
+        nbr = (rng.uniform(size=(m, m)) > 0.7).astype(np.int64)
+        nbr = np.maximum(nbr, nbr.T)
+        np.fill_diagonal(nbr, 1)
+        bands = rng.randint(0, 3, size=n)
+        envs, tables, prev0_l, prev_l, power_l, acts_pre = [], [], [], [], [], []
+        for b in range(B):
+            table = rng.uniform(0.01, 1.0, size=(n, m, T))
+            table[rng.uniform(size=table.shape) < 0.3] = 0.0  # invisible pairs: no drain, no penalty
+            np.random.seed(900 + 10 * idx + b)
+            if kind == "power":
+                env = RealPowerConstellationEnv(1, n, m, T, N, M, L, lam, sat_prox_mat=table.copy(),
+                                                graphs=[None] * T, task_prios=prios.copy())
+            else:
+                env = object.__new__(InterferenceConstellationEnv)
+                env.n, env.m, env.T, env.N, env.M, env.L = n, m, T, N, M, min(L, T)
+                env.lambda_, env.beam_types, env.bids_as_actions = lam, 7, False
+                env.k, env.done, env.constant_setup = 0, False, True
+                env.sat_prox_mat = table.copy()
+                env.neighbor_matrix = nbr
+                env.sat_freq_bands = bands
+                env.sat_freq_band_dict = defaultdict(list)
+                for i, bd in enumerate(bands):
+                    env.sat_freq_band_dict[bd].append(i)
+                env.task_prios = np.repeat(np.tile(prios, (n, 1))[:, :, np.newaxis], env.L, axis=-1)
+                env.power_states = np.ones(n)
+            env.reset()
+            prev0_l.append(np.asarray(env.prev_assigns, dtype=np.int64).copy())
+            ap = []
+            for t in range(pre):
+                a = rng.randint(0, m, size=n)
+                env.step(list(a))
+                ap.append(a)
+            envs.append(env)
+            tables.append(table)
+            prev_l.append(np.asarray(env.prev_assigns, dtype=np.int64))
+            power_l.append(np.asarray(env.power_states, dtype=np.float64).copy())
+            acts_pre.append(np.stack(ap) if pre else np.zeros((0, n), np.int64))
+        args = SimpleNamespace(runner="episode", use_mps_action_selection=False, device="cpu")
+        sel = HAALSelector(args)
+        sel.envs = envs
+        scheme = {"beta": {"vshape": (n, m, L), "part_of_state": True},
+                  "prev_assigns": {"vshape": (n,), "part_of_state": True},
+                  "power_states": {"vshape": (n,), "part_of_state": True}}
+        beta5 = th.zeros((B, 1, n, m, envs[0].L))
+        batch_get = {"beta": beta5}
+        batch = type("B", (), {"scheme": scheme, "__getitem__": lambda self, k: batch_get[k]})()
+        acts = sel.select_action(batch).numpy()
+        eff = min(envs[0].L, envs[0].T - envs[0].k)
+        seqs = build_time_interval_sequences(generate_all_time_intervals(eff), eff)
+        vals = np.zeros((B, len(seqs)))
+        for b in range(B):
+            for s_, tis in enumerate(seqs):
+                e = copy.deepcopy(envs[b])
+                tot = 0
+                for ti in tis:
+                    bh = e.beta_hat(e.beta, e.prev_assigns, e.power_states)
+                    _, a = so.linear_sum_assignment(bh.sum(axis=-1), maximize=True)
+                    for _ in range(ti[1] - ti[0] + 1):
+                        r, _, _ = e.step(a)
+                        tot += sum(r)
+                vals[b, s_] = tot
+        out[f"h{idx}_kind"] = np.array(kind)
+        out[f"h{idx}_spec"] = np.array([B, n, m, T, envs[0].L, N, M, pre, envs[0].k])
+        out[f"h{idx}_lambda"] = np.array(lam)
+        out[f"h{idx}_tables"] = np.stack(tables)
+        out[f"h{idx}_prios"] = prios
+        out[f"h{idx}_bands"] = np.asarray(bands, dtype=np.int64)
+        out[f"h{idx}_nbr"] = np.asarray(nbr, dtype=np.float64)
+        out[f"h{idx}_prev0"] = np.stack(prev0_l)
+        out[f"h{idx}_pre_actions"] = np.stack(acts_pre)
+        out[f"h{idx}_prev"] = np.stack(prev_l)
+        out[f"h{idx}_power"] = np.stack(power_l)
+        out[f"h{idx}_actions"] = acts
+        out[f"h{idx}_values"] = vals
+    out["n_cases"] = np.array(len(specs))
+    np.savez_compressed(os.path.join(OUT, "haal_variants.npz"), **out)
+
+
 def gen_replay_buffer():
     """ReplayBuffer (components/episode_buffer.py:237-277): ring inserts of EpisodeBatches
     of 2, 2 and 3 episodes into a 5-episode buffer (the last one wraps: split insert), the
@@ -940,6 +1043,7 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["round6"]:  # bids_as_actions on the real-env family (round 6)
         gen_real_bids()
+        gen_haal_variants()
         sys.exit(0)
     if sys.argv[1:] == ["yaml"]:  # the reference's unchanged mock algorithm configs (round 4)
         gen_yaml_runner_dumps()
@@ -960,6 +1064,7 @@ if __name__ == "__main__":
     gen_real_runner_dumps()
     gen_filtered_selectors()
     gen_haal()
+    gen_haal_variants()
     gen_replay_buffer()
     gen_yaml_runner_dumps()
     for f in sorted(os.listdir(OUT)):

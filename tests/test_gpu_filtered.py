@@ -188,6 +188,87 @@ def test_haal_matches_reference(golden):
         env.close()
 
 
+def _variant_env(kind, tables, N, M, L, lam, prios, E, bands, nbr, prev0=None, seed=0):
+    from marl_sap_amd.envs import InterferenceAssignEnvBatch, RealPowerAssignEnvBatch
+    n, m, T = tables.shape[-3:]
+    if kind == "power":
+        return RealPowerAssignEnvBatch(1, n, m, T, N, M, L, lam, sat_prox_mat=tables, graphs=[None] * T,
+                                       task_prios=prios, num_envs=E, initial_assignments=prev0, seed=seed, device=DEV)
+    return InterferenceAssignEnvBatch(1, n, None, T, N, M, L, lam, task_prios=prios, sat_freq_bands=bands,
+                                      sat_prox_mat=tables, neighbor_matrix=nbr, num_envs=E, initial_assignments=prev0,
+                                      seed=seed, device=DEV)
+
+
+def test_haal_variants_match_reference(golden):
+    """HAAL over the power / interference envs: the forks carry the power
+    states (drained by their own steps, dead / below-1e-12 rows zeroed in beta_hat) -- actions,
+    every sequence's value and the winning sequence bit-exact against the reference's selector
+    (tests/golden/haal_variants.npz), after the fixture's own pre-selection steps."""
+    g = golden("haal_variants")
+    for c in range(int(g["n_cases"])):
+        kind = str(g[f"h{c}_kind"])
+        B, n, m, T, L, N, M, pre, k = [int(x) for x in g[f"h{c}_spec"]]
+        env = _variant_env(kind, g[f"h{c}_tables"], N, M, L, float(g[f"h{c}_lambda"]), g[f"h{c}_prios"], B,
+                           g[f"h{c}_bands"], g[f"h{c}_nbr"], prev0=g[f"h{c}_prev0"])
+        batch = EpisodeBatch(env.scheme, {"agents": n}, B, T + 1, preprocess=env.preprocess, device=DEV,
+                             time_major=True)
+        env.reset(batch, 0)
+        for t in range(pre):
+            _step_real(env, batch, t, g[f"h{c}_pre_actions"][:, t])
+        np.testing.assert_array_equal(batch["prev_assigns"][:, pre].cpu().numpy(), g[f"h{c}_prev"])
+        assert torch.equal(batch["power_states"][:, pre].cpu(), torch.from_numpy(g[f"h{c}_power"]).to(torch.float16))
+        sel = NONRL["haal_selector"](SimpleNamespace())
+        sel.envs = env
+        out = sel.select_action(batch)
+        sel.status.flush()
+        np.testing.assert_array_equal(out.cpu().numpy(), g[f"h{c}_actions"], err_msg=f"{kind} case {c}")
+        np.testing.assert_array_equal(sel.last_values.cpu().numpy(), g[f"h{c}_values"], err_msg=f"{kind} case {c}")
+        best = np.array([int(np.argmax(v)) for v in g[f"h{c}_values"]])
+        np.testing.assert_array_equal(sel.last_best.cpu().numpy(), best)
+        env.close()
+
+
+@pytest.mark.parametrize("kind,n,m,T,L", [("power", 12, 20, 10, 4), ("power", 30, 45, 8, 3),
+                                          ("interference", 14, 24, 9, 3)])
+def test_haal_variants_vs_oracle_through_an_episode(oracle, kind, n, m, T, L):
+    """HAAL on the power variants at every step of an episode driven by HAAL itself (satellites
+    drain and die along the way), against the oracle restatement (pinned by the fixture above)."""
+    from oracle.selectors import haal_variant
+    E = 4
+    rng = np.random.RandomState(n + m + T + len(kind))
+    tables = rng.uniform(0.0, 1.0, size=(E, n, m, T))
+    tables[rng.uniform(size=tables.shape) < 0.4] = 0.0
+    prios = rng.choice([1.0, 1.0, 1.0, 5.0], size=m)
+    bands = rng.randint(0, 3, size=n)
+    nbr = (rng.uniform(size=(m, m)) > 0.75).astype(np.float64)
+    nbr = np.maximum(nbr, nbr.T)
+    np.fill_diagonal(nbr, 1.0)
+    env = _variant_env(kind, tables, 2, 2, L, 0.4, prios, E, bands, nbr, seed=3)
+    batch = EpisodeBatch(env.scheme, {"agents": n}, E, T + 1, preprocess=env.preprocess, device=DEV,
+                         time_major=True)
+    env.reset(batch, 0)
+    prev = batch["prev_assigns"][:, 0].cpu().numpy().astype(np.int64)
+    power = np.ones((E, n))
+    tt = np.ones((m, m)) - np.eye(m)
+    from oracle.selectors import power_update, real_beta
+    dead_seen = 0
+    for t in range(T):
+        out, values, best, status = env.haal_select(return_values=True)
+        assert int(status.abs().max()) == 0
+        acts = out.cpu().numpy().astype(np.int64)
+        for e in range(E):
+            a, vals = haal_variant(kind, tables[e], prios, tt, 0.4, t, prev[e], power[e], env.L, T, bands=bands,
+                                   nbr=nbr)
+            np.testing.assert_array_equal(acts[e], a, err_msg=f"t={t} env {e}")
+            np.testing.assert_array_equal(values[e].cpu().numpy(), vals, err_msg=f"t={t} env {e}")
+            power[e] = power_update(real_beta(tables[e], prios, t, env.L, T), acts[e], power[e])
+        _step_real(env, batch, t, acts)
+        prev = acts
+        dead_seen += int((power < 1e-12).sum())
+    assert dead_seen > 0  # the episode exercised dead / drained satellites
+    env.close()
+
+
 @pytest.mark.parametrize("n,m,T,L", [(12, 20, 8, 4), (30, 45, 6, 3), (5, 8, 9, 5)])
 def test_haal_vs_oracle_through_an_episode(oracle, n, m, T, L):
     """Sparse per-env tables (many zero benefits -> masked penalties, exact ties in the LSA),

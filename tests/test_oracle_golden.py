@@ -180,3 +180,19 @@ def test_haal_oracle(golden, oracle):
         seqs = osel.time_interval_sequences(min(L, T - k))
         flat = [[t for ti in s for t in ti] for s in seqs]
         assert [list(r[r >= 0]) for r in g[f"h{c}_seqs"]] == flat
+
+
+def test_haal_variants_oracle(golden, oracle):
+    """The HAAL restatement over the power / interference envs (forks carry power states) against
+    the reference selector's actions and every sequence's value (tests/golden/haal_variants.npz)."""
+    from oracle import selectors as osel
+    g = golden("haal_variants")
+    for c in range(int(g["n_cases"])):
+        kind = str(g[f"h{c}_kind"])
+        B, n, m, T, L, N, M, pre, k = [int(x) for x in g[f"h{c}_spec"]]
+        for b in range(B):
+            a, vals = osel.haal_variant(kind, g[f"h{c}_tables"][b], g[f"h{c}_prios"], np.ones((m, m)) - np.eye(m),
+                                        float(g[f"h{c}_lambda"]), k, g[f"h{c}_prev"][b], g[f"h{c}_power"][b], L, T,
+                                        bands=g[f"h{c}_bands"], nbr=g[f"h{c}_nbr"])
+            np.testing.assert_array_equal(a, g[f"h{c}_actions"][b], err_msg=f"{kind} case {c} env {b}")
+            np.testing.assert_array_equal(vals, g[f"h{c}_values"][b], err_msg=f"{kind} case {c} env {b}")
