@@ -362,6 +362,9 @@ def parse(argv=None):
     p.add_argument("--use-rnn", type=int, default=1, help="0: the Linear + ReLU RNNAgent (use_rnn: False)")
     p.add_argument("--sap-warm", type=int, default=1,
                    help="1 (default): the SAP selector's fast path warm-started from the previous step's duals")
+    p.add_argument("--real-envs", type=int, default=512,
+                   help="envs of the secondary real-env leg (324 x 450, T = 100; ~280 MB of tables + batch per env); "
+                        "0: skip it")
     p.add_argument("--fuse-reset", type=int, default=1,
                    help="1 (default, the runner's): on the episode schedule the env reset runs in the episode's "
                         "first launch (asg_reset_rollout); 0: asg_reset as its own launch")
@@ -693,6 +696,84 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
     return res
 
 
+def real_step_bytes(n, m, L, N, M):
+    """Algorithmic HBM bytes of one RealConstellationEnv env-step (per-env
+    tables): the L float64 benefit slices read (8nmL) + the int16 actions (2n) read; the float16
+    obs rows (2 obs n) and beta (2nmL), bool avail (nm), int16 one-hot (2nm), float16 rewards (2n),
+    int16 prev_assigns (2n) written, terminated + filled (9).  The task-major totals and the ranked
+    task lists the strip kernel hands the observation kernel are working state, not counted."""
+    obs = M * L + N * M * L + (N * M // 2) * L + M
+    return 8 * n * m * L + 2 * n + 2 * obs * n + 2 * n * m * L + n * m + 2 * n * m + 2 * n + 2 * n + 9
+
+
+def real_leg(a, dev, E, steps, warmup, n=324, m=450, T=100, L=3, N=10, M=10):
+    """The real-env family's rollout on one GPU: RealConstellationEnv at the
+    reference's real_constellation_env.yaml shape (18 x 18 satellites, 450 tasks, T = 100, L = 3,
+    N = M = 10), E envs with their own injected benefit tables (sparse, like proximities), random
+    policy written into the int16 actions row; `steps` env steps timed after `warmup`, each step =
+    the transition + strip + observation kernels (HIP events on the stream)."""
+    from marl_sap_amd.components import EpisodeBatch
+    from marl_sap_amd.envs import RealAssignEnvBatch
+    g = torch.Generator(device=dev).manual_seed(a.seed)
+    tables = torch.rand((E, n, m, T), generator=g, device=dev, dtype=torch.float64)
+    tables *= torch.rand((E, n, m, 1), generator=g, device=dev, dtype=torch.float64) > 0.8
+    env = RealAssignEnvBatch(18, 18, m, T, N, M, L, 0.5, sat_prox_mat=tables, num_envs=E, device=dev)
+    del tables
+    b = EpisodeBatch(env.scheme, {"agents": n}, E, T + 1, preprocess=env.preprocess, device=dev, time_major=True)
+    env.reset(b, 0)
+    acts = torch.randint(0, m, (warmup + steps, E, n), generator=g, device=dev, dtype=torch.int64).to(torch.int16)
+    for t in range(warmup):
+        b["actions"][:, t, :, 0] = acts[t]
+        env.step(b, t)
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for t in range(warmup, warmup + steps):
+        b["actions"][:, t, :, 0] = acts[t]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        env.step(b, t)
+        e1.record()
+        ev.append((e0, e1))
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    env.sync()
+    step_ms = sum(x.elapsed_time(y) for x, y in ev) / len(ev)
+    per = real_step_bytes(n, m, L, N, M) * E
+    gbs = per / (step_ms * 1e-3) / 1e9
+    pm = pmc_lookup("*pmc_real_step*.json", n=n, m=m, E=E)
+    traffic = pm.get("hbm_bytes_per_step") if pm else None
+    leg = {"value": round(E * steps / secs, 1), "unit": "env-steps/s", "ms_per_step": round(secs / steps * 1e3, 4),
+           "steps": steps, "warmup": warmup, "schedule": "asg_real_step (transition + strip + observation kernels)",
+           "workload": f"RealConstellationEnv (real_constellation_env.yaml shape) n={n} satellites, m={m} tasks, T={T}, "
+                       f"L={L}, N={N}, M={M}; {E} envs with their own injected float64 tables (80 % of pairs zero), "
+                       "random policy, float16 / int16 scheme",
+           "envs_per_gpu": E, "kernels_ms": {"real_step": round(step_ms, 4)},
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_over_algorithmic": round(traffic / per, 4) if traffic else None,
+                        "kernel": "asg::real_transition_kernel + real_strip_kernel + real_obs_kernel",
+                        "bytes_per_launch": per, "bytes_per_env_step": real_step_bytes(n, m, L, N, M),
+                        "pmc_source": os.path.basename(pm["_path"]) if pm else None}}
+    if a.cpu_baseline:
+        # the C oracle env (oracle/asg_real_oracle.c, one thread) on a bounded sample, as a CPU figure
+        import numpy as np
+        from oracle import oracle as ora
+        rs = np.random.RandomState(0)
+        tab = rs.uniform(size=(n, m, T)) * (rs.uniform(size=(n, m, 1)) > 0.8)
+        r = ora.OracleRealEnv(tab, N, M, L, 0.5)
+        r.reset()
+        t1, k = time.perf_counter(), 0
+        while time.perf_counter() - t1 < 3.0 and k < T:
+            r.step(rs.randint(0, m, size=n))
+            k += 1
+        leg["cpu_baseline"] = {"value": round(k / (time.perf_counter() - t1), 2), "unit": "env-steps/s", "cores": 1,
+                               "kind": "port", "sample": f"{k} steps of one env on the C oracle (3 s bound)"}
+    env.close()
+    del b, env, acts
+    return leg
+
+
 def leg_memory(dev):
     """Device memory at a leg's edges (GB): torch's allocated / reserved, and free per hipMemGetInfo."""
     free, total = torch.cuda.mem_get_info(dev)
@@ -969,6 +1050,13 @@ def main():
                 croof.pop("issue", None)
                 leg["roofline"] = croof
             extra["compat"] = leg
+        if a.config == 2 and world == 1 and a.real_envs > 0:
+            # the real-env family at its reference shape; last, with the
+            # allocator's cache released first (its per-env tables and 101-row batch are the largest
+            # allocation of the run)
+            gc.collect()
+            torch.cuda.empty_cache()
+            extra["real"] = real_leg(a, dev, a.real_envs, 20, 5)
 
     if a.selector == "random":
         ra = None

@@ -29,6 +29,15 @@ for st in "$@"; do
       done
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_compat" -o run -- python3 $B --rng mt19937 --steps 40 --warmup 20 > "$OUT/kt_compat.log" 2>&1
       rc=$?; echo "kt compat rc=$rc"; fatal $rc kt_compat ;;
+    real_pmc)
+      RE=${REAL_ENVS:-512}
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_real_$c" -o run -- python3 tools/bench_real_env.py --envs $RE --steps 3 --cpu 0 > "$OUT/pmc_real_$c.log" 2>&1
+        rc=$?; echo "pmc real $c rc=$rc"; fatal $rc pmc_real_$c
+      done
+      python3 tools/pmc_real_summary.py "$OUT/pmc_real_FETCH_SIZE" "$OUT/pmc_real_WRITE_SIZE" "$OUT/pmc_real_step.json" --E $RE
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_real" -o run -- python3 tools/bench_real_env.py --envs $RE --steps 20 --cpu 0 > "$OUT/kt_real.log" 2>&1
+      rc=$?; echo "kt real rc=$rc"; fatal $rc kt_real ;;
     *) echo "unknown step $st" ;;
   esac
 done
