@@ -303,6 +303,15 @@ def fused_roofline(a, E, fused_ms, use_rnn=True, resets_per_step=0.0, q_out=Fals
                                "replaced by this window's resets_per_step (same accounting as bytes_per_launch)")
     if issue:
         out["issue"] = issue
+    # SURVEY §8(d)'s own accounting beside the one above: B_batch = B_env + the fused int64 one-hot
+    # (8nm) + the actions written (8n) per env-step, + the reset row per reset -- no hidden state
+    # (the agent's h round trip is design traffic of this kernel, not the path's)
+    b_env = a.n * a.m * (4 * a.L + 13) + 20 * a.n + 9
+    b_batch = int(round((b_env + 8 * a.n * a.m + 8 * a.n + resets_per_step * reset_bytes(a.n, a.m, a.L)) * E))
+    sv = b_batch / (fused_ms * 1e-3) / 1e9
+    out["survey_b_batch"] = {"bytes_per_launch": b_batch, "achieved": round(sv, 1), "frac": round(sv / HBM_PEAK_GBS, 4),
+                             "note": "SURVEY §8(d) B_batch = nm(4L+13) + 20n + 9 + 8nm + 8n per env-step (+ the reset "
+                                     "row amortised), against the 8 TB/s peak"}
     return out
 
 
@@ -628,7 +637,7 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
            "fused_launches": len(fused_pairs), "fused_steps": sum(p[2] for p in fused_pairs),
            "fused_resets": state.get("fused_resets", 0),
            "gather_ms": mean(gather_pairs) if gather_pairs else None, "gathers": len(gather_pairs)}
-    if count_lsa and selector == "sap" and a.n <= a.m <= 64:
+    if count_lsa and selector in ("sap", "bids") and a.n <= a.m <= 64:
         # one more selection with the step-counting kernel instance.  On the step_q schedule it
         # is a genuine next step (env step t + agent forward + the selection of row t + 1, warm-
         # started from row t's duals, as in the timed window); else a selection on the current row
@@ -797,7 +806,7 @@ def sap_kernels(r):
             "first_select": r4(r.get("sel_ms")), "schedule": r.get("mode") or "split"}
 
 
-def lsa_roofline(a, E, res):
+def lsa_roofline(a, E, res, kernel="asg::sap_select_kernel", pmc="*pmc_sap_kernel*.json"):
     """SAP selector efficiency: augmenting-path steps (scipy's inner-loop iterations, counted
     by the instrumented kernel instance on one selection) per second of the fused
     noise + LSA kernel, as cycles per step per SIMD.  With a PMC summary of the kernel in
@@ -811,7 +820,7 @@ def lsa_roofline(a, E, res):
         return None
     per_s = steps / (lsa_ms * 1e-3)
     cyc = SIMDS * CLOCK_HZ * lsa_ms * 1e-3 / steps
-    out = {"bound": None, "kernel": "asg::sap_select_kernel", "kernel_ms": round(lsa_ms, 4),
+    out = {"bound": None, "kernel": kernel, "kernel_ms": round(lsa_ms, 4),
            "path_steps_per_launch": steps, "path_steps_per_s": round(per_s, 1),
            "path_steps_fast": res.get("path_steps_fast"), "path_steps_exact": res.get("path_steps_exact"),
            "problems_on_exact_solver": res.get("exact_problems"), "problems": E,
@@ -819,7 +828,7 @@ def lsa_roofline(a, E, res):
                          "paths, square problems) and of the scipy-exact solver (uncertified / rectangular problems)",
            "cycles_per_step_per_simd": round(cyc, 1), "achieved": None, "peak": None, "frac": None,
            "unit": "wave-VALU-instr/s", "traffic": None}
-    pm = pmc_lookup("*pmc_sap_kernel*.json", n=a.n, m=a.m, E=E)
+    pm = pmc_lookup(pmc, n=a.n, m=a.m, E=E)
     if pm and pm.get("valu_insts_per_path_step"):
         vps = pm["valu_insts_per_path_step"]
         sps = pm.get("salu_insts_per_path_step") or 0.0
@@ -925,7 +934,7 @@ def main():
             # asg_bids_select (pi_logits softmax, softmax over the agents, noise, the bids row, its LSA);
             # the same with separate launches beside it
             for name, fz in (("ippo_sap", None), ("ippo_sap_split", 0)):
-                rb = run_leg(a, dev, world, E, sk, sw, selector="bids", agent="rnn", fused=fz)
+                rb = run_leg(a, dev, world, E, sk, sw, selector="bids", agent="rnn", fused=fz, count_lsa=fz is None)
                 extra[name] = {
                     **leg_base(rb, sk, sw),
                     "what": "ippo_sap.yaml env path: bids_as_actions, ContinuousActionSelector (softmax_agent_inputs, "
@@ -940,6 +949,12 @@ def main():
                 if rb.get("mode") == "step_q" and rb.get("step_forward_ms"):
                     extra[name]["roofline_step_forward"] = fused_roofline(a, E, rb["step_forward_ms"], use_rnn=False,
                                                                           q_out=True, bids=True)
+                if fz is None:
+                    # bids_select_kernel: the two softmaxes (2n wave reductions), the noise, the bids row
+                    # store, then the LSA of the negated bids -- augmenting-path steps counted by its
+                    # instrumented instance on one more step of the same schedule
+                    extra[name]["roofline_lsa"] = lsa_roofline(a, E, rb, kernel="asg::bids_select_kernel",
+                                                               pmc="*pmc_bids_kernel*.json")
             # the reference's own algorithms for this env (config/algs/mock_constellation_*.yaml):
             # jumpstart_mac with the HAA jumpstart selector, use_rnn: False (Linear + ReLU agent),
             # jumpstart epsilon 1 -> 0 over 20,000 env steps -- one 16,384-env episode is 327,680
@@ -1048,8 +1063,50 @@ def main():
                 croof.pop("traffic_over_algorithmic", None)
                 croof.pop("traffic_note", None)
                 croof.pop("issue", None)
+                croof.pop("survey_b_batch", None)
+                # PMC bytes of the same launches (tools/gpu_r6.sh compat_pmc: separate FETCH / WRITE
+                # passes over one whole same-seed episode: the draw kernel, the table kernel, the episode
+                # kernel with its reset row), per step with this window's reset share
+                pm = pmc_lookup("*pmc_rollout_tab*.json", n=a.n, m=a.m, E=E, L=a.L)
+                if pm:
+                    ks = pm.get("kernels", {})
+                    col = "hbm_bytes_fetch_doubled"
+                    roll = next((v[col] for k, v in ks.items() if "rollout_kernel" in k), None)
+                    draw = sum(v[col] for k, v in ks.items() if "mt_reset_kernel" in k or "mt_table_kernel" in k)
+                    if roll:
+                        spl = pm.get("steps_per_launch", a.T)
+                        rb = reset_bytes(a.n, a.m, a.L) * E
+                        rps = res_resets(rc)
+                        tr = round((roll - rb) / spl + rps * (rb + draw))
+                        table_read = next((v for k, v in pm.get("table_reads", {}).items()), None)
+                        croof.update({"traffic": tr, "traffic_over_algorithmic": round(tr / per, 4),
+                                      "traffic_pmc": os.path.basename(pm["_path"]),
+                                      "traffic_note": "(2 FETCH_SIZE + WRITE_SIZE) of the episode kernel per step, its "
+                                                      "reset row replaced by this window's share, + the draw and table "
+                                                      "kernels' bytes per reset amortised the same way",
+                                      "episode_kernel_bytes_per_step": round((roll - rb) / spl)})
+                        if table_read:
+                            croof["table_read_over_algorithmic"] = table_read
                 leg["roofline"] = croof
             extra["compat"] = leg
+        if a.config == 2 and world == 1:
+            # SURVEY §8(f) rows 1 and 3 on this GPU (tools/bench_aux.py): the SAP learner's B x (T-1)
+            # target LSAs as one asg_lsa_batched launch (the reference: a serial scipy loop,
+            # sap_q_learner.py:98-108, timed beside it on the host), and the device ReplayBuffer's
+            # insert of a 4,096-episode rollout batch + a 32-episode sample (episode_buffer.py:237-277)
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import bench_aux
+            lt = bench_aux.bench_sap_targets(32, a.T + 1, a.n, a.m, dev)
+            extra["learner_lsa_targets"] = {
+                **lt, "what": "sap_q_learner.py:98-108's per-(episode, t) scipy LSA on the target Q-values: "
+                              "marl_sap_amd.learners.sap_target_max_qvals (one asg_lsa_batched launch + gather), "
+                              "32 episodes x (T-1) problems of n x m; scipy_loop_ms = the reference's loop on the host"}
+            rp = bench_aux.bench_replay(4096, 8192, a.n, a.m, a.T, a.L, 32, dev)
+            rp["insert_frac"] = round(rp["insert_GBps"] / HBM_PEAK_GBS, 4)
+            rp["what"] = ("device ReplayBuffer (episode_buffer.py:237-277 layout): insert_episode_batch of one "
+                          "4,096-env time-major rollout batch into an 8,192-episode ring (bytes read + written), "
+                          "sample(32)")
+            extra["replay_buffer"] = rp
         if a.config == 2 and world == 1 and a.real_envs > 0:
             # the real-env family at its reference shape; last, with the
             # allocator's cache released first (its per-env tables and 101-row batch are the largest

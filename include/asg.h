@@ -438,6 +438,12 @@ int asg_reset_forward(asg_handle *h, const asg_batch_view *b, int ts, const void
 int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
                     const int64_t out_strides[3], int row_softmax, int col_softmax, double noise_std, uint64_t seed,
                     uint64_t counter, void *hip_stream);
+/* asg_bids_select on the instrumented kernel instance: path_steps_out [E] int32 (device) receives
+ * every env's augmenting-path steps (the certified fast path's in bits 0..15, the scipy-exact
+ * solver's above, as asg_sap_select); same bids and assignments (bench.py's efficiency figure). */
+int asg_bids_select_count(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
+                          const int64_t out_strides[3], int row_softmax, int col_softmax, double noise_std,
+                          uint64_t seed, uint64_t counter, int32_t *path_steps_out, void *hip_stream);
 /* Number of fc1 weight slices (32 inputs x 64 units) the rollout kernel reads through L2
  * instead of LDS for an (n, m, L) env and agent kind, or -1 when asg_rollout does not take
  * the shape (GRU: 64 x 64, L = 3: 1; 256 x 256: 19).  asg_step_select_l2_slices = the GRU

@@ -44,7 +44,7 @@ EXPORTS = ["asg_abi_version", "asg_last_error", "asg_create", "asg_destroy", "as
            "asg_real_haal_num_sequences", "asg_step_select", "asg_step_select_l2_slices", "asg_rollout",
            "asg_rollout_l2_slices", "asg_reset_rollout", "asg_sap_select_into", "asg_step_forward",
            "asg_sap_noise", "asg_random_rollout", "asg_sap_select_warm", "asg_bids_select",
-           "asg_reset_forward", "asg_step_ex", "asg_step_forward_ex"]
+           "asg_reset_forward", "asg_step_ex", "asg_step_forward_ex", "asg_bids_select_count"]
 
 
 class AsgField(ctypes.Structure):
@@ -169,6 +169,8 @@ def lib():
             L.asg_sap_select_warm.argtypes = [vp, i64p, i64, i32, i32, dbl, u64, u64, i64, vp, vp, vp, vp, i32, vp]
         if hasattr(L, "asg_bids_select"):  # absent from older A/B builds
             L.asg_bids_select.argtypes = [vp, vp, i64p, vp, i64p, i32, i32, dbl, u64, u64, vp]
+        if hasattr(L, "asg_bids_select_count"):
+            L.asg_bids_select_count.argtypes = [vp, vp, i64p, vp, i64p, i32, i32, dbl, u64, u64, vp, vp]
         if hasattr(L, "asg_reset_forward"):
             L.asg_reset_forward.argtypes = [vp, ctypes.POINTER(AsgBatchView), i32, vp, vp, vp, vp, vp, i32, i32, i32,
                                             vp, i64, vp, vp, vp]

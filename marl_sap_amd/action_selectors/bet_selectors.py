@@ -26,6 +26,9 @@ class ContinuousActionSelector:
         self.seed = selector_seed(args)
         self.calls = 0
         self.envs = None  # set by the runner (the batched env: fused_bids)
+        # instrumentation (bench.py): an int32 [B] device tensor receives every env's augmenting-path
+        # steps of the next fused_bids call (the counting kernel instance), then is left as is
+        self.count_steps = None
 
     def fused_bids(self, q, out, t_env, test_mode=False, row_softmax=False):
         """The bids of every env from the agent's raw outputs q [B, n, m] (row_softmax: the
@@ -35,7 +38,7 @@ class ContinuousActionSelector:
         self.variance = self.args.evaluation_epsilon if test_mode else self.schedule.eval(t_env)
         self.calls += 1
         self.envs.bids_select(q, out, row_softmax, bool(getattr(self.args, "softmax_agent_inputs", False)),
-                              float(self.variance), self.seed, self.calls)
+                              float(self.variance), self.seed, self.calls, count_steps=self.count_steps)
         return out
 
     def select_action(self, agent_inputs, avail_actions, t_env, test_mode=False, state=None, beta=None):

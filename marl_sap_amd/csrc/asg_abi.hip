@@ -795,6 +795,13 @@ int asg_step_forward_ex(asg_handle *h, const asg_batch_view *b, int ts, const vo
 int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
                     const int64_t out_strides[3], int row_softmax, int col_softmax, double stdv, uint64_t seed,
                     uint64_t counter, void *hip_stream) {
+    return asg_bids_select_count(h, q, q_strides, bids_out, out_strides, row_softmax, col_softmax, stdv, seed, counter,
+                                 nullptr, hip_stream);
+}
+
+int asg_bids_select_count(asg_handle *h, const float *q, const int64_t q_strides[3], float *bids_out,
+                          const int64_t out_strides[3], int row_softmax, int col_softmax, double stdv, uint64_t seed,
+                          uint64_t counter, int32_t *path_steps_out, void *hip_stream) {
     if (!h) return fail(nullptr, ASG_E_INVALID_ARG, "NULL handle");
     const EnvState &st = h->st;
     if (!st.bids) return fail(h, ASG_E_INVALID_ARG, "asg_bids_select: the handle was not created with bids_as_actions");
@@ -805,7 +812,7 @@ int asg_bids_select(asg_handle *h, const float *q, const int64_t q_strides[3], f
     hipStream_t s = static_cast<hipStream_t>(hip_stream ? hip_stream : h->stream);
     hipError_t e = asg::launch_bids_select(q, q_strides, st.E, st.n, st.m, row_softmax != 0, col_softmax != 0,
                                            (float)stdv, seed, (uint32_t)counter, st.env_base, bids_out, out_strides,
-                                           st.assign, st.err, s);
+                                           st.assign, st.err, s, path_steps_out);
     if (e != hipSuccess) return hip_fail(h, e, "asg_bids_select");
     h->bids_tag.row = bids_out;
     h->bids_tag.s_env = out_strides[0];

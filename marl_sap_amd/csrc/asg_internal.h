@@ -83,7 +83,7 @@ hipError_t launch_sap_noise(const float *q, const int64_t qs[3], int64_t B, int 
                             uint32_t counter, int64_t env_base, float *q_out, int32_t *status_out, hipStream_t s);
 hipError_t launch_bids_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, int row_sm, int col_sm,
                               float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids,
-                              const int64_t os[3], int *assign, int *env_err, hipStream_t s);
+                              const int64_t os[3], int *assign, int *env_err, hipStream_t s, int32_t *steps_out = nullptr);
 hipError_t launch_haa_select(const float *beta, const int64_t bs[3], const int64_t *prev, const int64_t ps[2],
                              int64_t B, int n, int m, const double *T_trans, double lambda_, float *col_out,
                              int32_t *status_out, hipStream_t s);

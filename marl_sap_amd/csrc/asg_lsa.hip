@@ -294,13 +294,16 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
 #ifndef ASG_BIDS_WAVES
 #define ASG_BIDS_WAVES 5
 #endif
+// kCount: the instrumented instance (bench.py's efficiency figure): steps_out[b] = the env's
+// augmenting-path steps, fast path in bits 0..15, scipy-exact solver above (as asg_sap_select)
+template <bool kCount>
 __global__ void __launch_bounds__(64 * kLsaWpb)
 #if ASG_BIDS_WAVES
 __attribute__((amdgpu_waves_per_eu(ASG_BIDS_WAVES)))
 #endif
 bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, int m, int row_sm, int col_sm,
                    float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids, int64_t o0,
-                   int64_t o1, int64_t o2, int *assign, int *env_err, int64_t B) {
+                   int64_t o1, int64_t o2, int *assign, int *env_err, int64_t B, int32_t *steps_out = nullptr) {
     __shared__ uint64_t s_slot[kLsaWpb][64];
     const int64_t b = lsa_reg_problem();
     if (b >= B) return;
@@ -389,17 +392,24 @@ bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, in
     int nfast = 0, nsteps = 0;
     bool done = false;
     if (ASG_SAP_FAST && status == ASG_OK && n == m)
-        done = lsa_fast_reg64<decltype(rc), false>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
-    if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), false>(rc, n, m, c4r, &nsteps);
+        done = lsa_fast_reg64<decltype(rc), kCount>(rc, n, c4r, &nfast, s_slot[threadIdx.x >> 6]) == ASG_OK;
+    if (status == ASG_OK && !done) status = lsa_solve_reg64<decltype(rc), kCount>(rc, n, m, c4r, &nsteps);
     if (lane < n) assign[b * n + lane] = status == ASG_OK ? c4r[0] : -1;
     if (status != ASG_OK && lane == 0) atomicCAS(env_err, 0, status);
+    if (kCount && lane == 0 && steps_out) steps_out[b] = nfast | (nsteps << 16);
 }
 
 hipError_t launch_bids_select(const float *q, const int64_t qs[3], int64_t B, int n, int m, int row_sm, int col_sm,
                               float stdv, uint64_t seed, uint32_t counter, int64_t env_base, float *bids,
-                              const int64_t os[3], int *assign, int *env_err, hipStream_t s) {
-    hipLaunchKernelGGL(bids_select_kernel, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2], n, m,
-                       row_sm, col_sm, stdv, seed, counter, env_base, bids, os[0], os[1], os[2], assign, env_err, B);
+                              const int64_t os[3], int *assign, int *env_err, hipStream_t s, int32_t *steps_out) {
+    if (steps_out)
+        hipLaunchKernelGGL(bids_select_kernel<true>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1], qs[2],
+                           n, m, row_sm, col_sm, stdv, seed, counter, env_base, bids, os[0], os[1], os[2], assign,
+                           env_err, B, steps_out);
+    else
+        hipLaunchKernelGGL(bids_select_kernel<false>, lsa_reg_grid(B), dim3(64 * kLsaWpb), 0, s, q, qs[0], qs[1],
+                           qs[2], n, m, row_sm, col_sm, stdv, seed, counter, env_base, bids, os[0], os[1], os[2],
+                           assign, env_err, B, nullptr);
     return hipGetLastError();
 }
 

@@ -220,7 +220,7 @@ class AssignEnvBatch(MultiAgentEnv):
         self.k += 1
         return q_out, h_out
 
-    def bids_select(self, q, out, row_softmax, col_softmax, std, seed, counter):
+    def bids_select(self, q, out, row_softmax, col_softmax, std, seed, counter, count_steps=None):
         """asg_bids_select: the bids of every env from the agent outputs q ([E n, m] or [E, n, m]
         float32) -- softmax over the tasks (row_softmax), over the agents (col_softmax), + N(0,
         std) -- written to `out` [E, n, m] float32 (the batch's actions row), and their
@@ -229,10 +229,16 @@ class AssignEnvBatch(MultiAgentEnv):
         q = q.view(E, n, m)
         if q.dtype != torch.float32 or out.dtype != torch.float32 or tuple(out.shape) != (E, n, m):
             raise ValueError("bids_select: float32 q and out of shape [E, n, m]")
-        self._call("asg_bids_select", ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()),
-                   ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), int(bool(row_softmax)),
-                   int(bool(col_softmax)), float(std), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter),
-                   _lib.stream_ptr(self.device))
+        if count_steps is not None:  # instrumentation (bench.py): int32 [E] augmenting-path steps
+            self._call("asg_bids_select_count", ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()),
+                       ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), int(bool(row_softmax)),
+                       int(bool(col_softmax)), float(std), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter),
+                       ctypes.c_void_p(count_steps.data_ptr()), _lib.stream_ptr(self.device))
+        else:
+            self._call("asg_bids_select", ctypes.c_void_p(q.data_ptr()), _lib.i64arr(q.stride()),
+                       ctypes.c_void_p(out.data_ptr()), _lib.i64arr(out.stride()), int(bool(row_softmax)),
+                       int(bool(col_softmax)), float(std), int(seed) & 0xFFFFFFFFFFFFFFFF, int(counter),
+                       _lib.stream_ptr(self.device))
         self._bids_token = (out.data_ptr(), tuple(out.stride()), out._version)
         return out
 
