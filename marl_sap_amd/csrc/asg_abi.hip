@@ -170,8 +170,17 @@ int asg_create(const asg_config *cfg, int device, void *hip_stream, asg_handle *
         if ((e = hipMemsetAsync(st.table, 0, sizeof(double) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
     }
     if (st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED) {
-        if ((e = hipMalloc(&st.table32, sizeof(float) * E * T * n * m)) != hipSuccess) goto oom;
-        if ((e = hipMemsetAsync(st.table32, 0, sizeof(float) * E * T * n * m, h->stream)) != hipSuccess) goto oom;
+        // + 16 floats: the compact table's 16-byte quad reads may run 12 bytes past a slice's pairs
+        if ((e = hipMalloc(&st.table32, sizeof(float) * (E * T * n * m + 16))) != hipSuccess) goto oom;
+        if ((e = hipMemsetAsync(st.table32, 0, sizeof(float) * (E * T * n * m + 16), h->stream)) != hipSuccess) goto oom;
+    }
+    if (st.rng_mode == ASG_RNG_MT19937 && st.benefit_mode != ASG_BENEFIT_INJECTED) {
+        // the compact table's pair masks / offsets (all zero = no bumps, the zero table before a reset)
+        const size_t W = (m + 63) / 64;
+        if ((e = hipMalloc(&st.tmask, sizeof(uint64_t) * E * n * W)) != hipSuccess) goto oom;
+        if ((e = hipMemsetAsync(st.tmask, 0, sizeof(uint64_t) * E * n * W, h->stream)) != hipSuccess) goto oom;
+        if ((e = hipMalloc(&st.toff, sizeof(int) * E * n * W)) != hipSuccess) goto oom;
+        if ((e = hipMemsetAsync(st.toff, 0, sizeof(int) * E * n * W, h->stream)) != hipSuccess) goto oom;
     }
     if (st.bids) {
         if ((e = hipMalloc(&st.assign, sizeof(int) * E * n)) != hipSuccess) goto oom;
@@ -206,6 +215,8 @@ int asg_destroy(asg_handle *h) {
     (void)hipFree(const_cast<double *>(st.T_trans));
     (void)hipFree(st.table);
     (void)hipFree(st.table32);
+    (void)hipFree(st.tmask);
+    (void)hipFree(st.toff);
     (void)hipFree(st.mt);
     (void)hipFree(st.mtpar);
     (void)hipFree(st.assign);

@@ -16,6 +16,8 @@
 #include "asg_internal.h"
 #include "lsa_wave.h"
 
+#include <mutex>
+
 namespace asg {
 
 // ------------------------------------------------------------------------------------
@@ -98,28 +100,41 @@ struct TableSrc {  // float64 table [E][T][n][m] (injected)
     }
 };
 
-// MT19937 compat mode: the rows' float32 benefits from the reset's float32 table, the float64
-// ones (rewards, export) evaluated from the recorded draws par [E][m][n] (mt_par_value, the
-// function the table was written with): no float64 table in HBM
+// MT19937 compat mode: the rows' float32 benefits from the reset's compact float32 table (per
+// (env, t) slice only the bump pairs, in (agent, task) order: tmask marks them, toff gives each
+// mask word's first compact index -- every other pair is exactly 0), the float64 ones (rewards,
+// export) evaluated from the recorded draws par [E][m][n] (mt_par_value, the function the table
+// was written with): no float64 table in HBM
 struct ParSrc {
     const float *tab32;
     const double2 *par;
+    const uint64_t *tmask;
+    const int *toff;
     int n, m, T;
 
     static constexpr bool kNeedsScale = false;
     struct Env {
-        const float *p;  // &tab32[e][0][0][0]
+        const float *p;  // &tab32[e][0][0] (slice 0; slices are n m floats apart)
         const double2 *q;  // &par[e][0][0]
-        int n, m;
+        const uint64_t *mk;  // &tmask[e][0][0]
+        const int *of;       // &toff[e][0][0]
+        int n, m, W;
         int64_t nm;
         struct Pair {
-            const float *p;
+            const float *p;  // the pair's slice-0 compact value, or nullptr: no bump (0 at every t)
             const double2 *q;
             int64_t tstride;
-            __device__ float at(int t) const { return p[t * tstride]; }
+            __device__ float at(int t) const { return p ? p[t * tstride] : 0.0f; }
             __device__ double at64(int t) const { return mt_par_value(*q, t); }
         };
-        __device__ Pair pair(int i, int j) const { return Pair{p + (int64_t)i * m + j, q + (int64_t)j * n + i, nm}; }
+        __device__ Pair pair(int i, int j) const {
+            const int w = j >> 6, b = j & 63;
+            const uint64_t mw = mk[(int64_t)i * W + w];
+            const float *v = nullptr;
+            if ((mw >> b) & 1ull)
+                v = p + of[(int64_t)i * W + w] + __popcll(mw & ((1ull << b) - 1ull));
+            return Pair{v, q + (int64_t)j * n + i, nm};
+        }
         __device__ void pair4(int i, int j, Pair (&P)[4]) const {
 #pragma unroll
             for (int k = 0; k < 4; ++k) P[k] = pair(i, j + k);
@@ -128,7 +143,8 @@ struct ParSrc {
     __device__ void fill_scale(int64_t, float *) const {}
     __device__ Env bind(int64_t e, const float *) const {
         const int64_t nm = (int64_t)n * m;
-        return Env{tab32 + e * (int64_t)T * nm, par + e * nm, n, m, nm};
+        const int W = (m + 63) >> 6;
+        return Env{tab32 + e * (int64_t)T * nm, par + e * nm, tmask + e * n * W, toff + e * n * W, n, m, W, nm};
     }
 };
 
@@ -744,11 +760,11 @@ __device__ __forceinline__ bool mt_r_above_075(uint32_t a, uint32_t b) {
     return hi > (3u << 25) || (hi == (3u << 25) && lo != 0u);
 }
 __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvState st, double2 *par, bool construct,
-                                                       bool generate) {
+                                                       bool generate, int64_t e0 = 0) {
     extern __shared__ uint32_t s_mt[];
     uint32_t *key = s_mt, *key2 = s_mt + kMtN, *out = s_mt + 2 * kMtN;
     int *perm = reinterpret_cast<int *>(out + (ASG_MT_TEMPER_ON_READ ? 0 : 2 * kMtN));
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     const int lane = threadIdx.x;
     const int n = st.n, m = st.m, T = st.T;
     uint32_t *g = mtstate + e * (kMtN + 1);
@@ -836,12 +852,15 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
 }
 
 // the reset's table B[e][t][i][j] = mt_par_value(draw, t) (the reference's zeros + bumps, mock
-// :276-299) rounded to float32, the rows' dtype.  Per chunk of `rows` agents (rows * m <= 1024):
-// the draws staged transposed in LDS and the chunk's bumps listed (about one pair in four);
-// then per group of kTableTG times the bumps' values are evaluated into a zeroed LDS tile, one
-// bump per thread (the float64 exp / division run for bumps only, not for every element), and
-// the tile is written as whole rows.  The float64 values are not stored: their readers evaluate
-// them from the draws (ParSrc).
+// :276-299) rounded to float32, the rows' dtype, stored COMPACT: per (env, t) slice only the
+// bump pairs (about one in four; every other value is exactly 0), in (agent, task) order, with
+// their masks tmask [E][n][W] and each mask word's first compact index toff [E][n][W] -- the
+// episode kernel then reads ~1/4 of a dense slice per lookahead block.  Per chunk of `rows`
+// agents (rows * m <= 1024): the draws staged transposed in LDS, the chunk's pair masks built
+// (LDS 64-bit OR), the compact order listed, then per group of kTableTG times each bump's values
+// evaluated by one thread (the float64 exp / division for bumps only) into an LDS tile written
+// out as contiguous compact runs.  The float64 values are not stored: their readers evaluate them
+// from the draws (ParSrc).
 #ifndef ASG_TABLE_TG
 #define ASG_TABLE_TG 4
 #endif
@@ -854,61 +873,77 @@ static int mt_table_rows(int m) {
     return m >= 1024 ? 1 : (1024 / m < ASG_TABLE_ROWS ? 1024 / m : ASG_TABLE_ROWS);
 }
 static size_t mt_table_lds(int R, int m) {
-    return (sizeof(double2) + sizeof(int) + sizeof(float) * kTableTG) * (size_t)R * m;
+    const size_t W = (m + 63) / 64;
+    return (sizeof(double2) + sizeof(int) + sizeof(float) * kTableTG) * (size_t)R * m +
+           (sizeof(uint64_t) + sizeof(int)) * (size_t)R * W;
 }
-__global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, int R) {
+__global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, int R, int64_t e0 = 0) {
     extern __shared__ double2 s_par[];                               // [R agents][m tasks]
-    int *s_list = reinterpret_cast<int *>(s_par + R * st.m);         // the chunk's bumps
-    float *s_tile = reinterpret_cast<float *>(s_list + R * st.m);    // [kTableTG][R * m]
+    int *s_list = reinterpret_cast<int *>(s_par + R * st.m);         // the chunk's bumps, compact order
+    float *s_tile = reinterpret_cast<float *>(s_list + R * st.m);    // [kTableTG][chunk's bumps]
+    const int W = (st.m + 63) >> 6;
+    unsigned long long *s_mask = reinterpret_cast<unsigned long long *>(s_tile + kTableTG * R * st.m);  // [R][W]
+    int *s_off = reinterpret_cast<int *>(s_mask + R * W);           // [R][W] compact index (chunk-relative)
     __shared__ int s_cnt;
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     const int n = st.n, m = st.m, T = st.T;
     const int64_t nm = (int64_t)n * m;
     const double2 *pe = par + e * nm;
     float *te = st.table32 + e * T * nm;
-    for (int x = threadIdx.x; x < kTableTG * R * m; x += blockDim.x) s_tile[x] = 0.f;
+    uint64_t *gm = st.tmask + e * n * W;
+    int *go = st.toff + e * n * W;
+    int base = 0;  // the env's compact index of the chunk's first bump
     for (int i0 = 0; i0 < n; i0 += R) {
         const int rows = min(R, n - i0), ne = rows * m;
         __syncthreads();
-        if (threadIdx.x == 0) s_cnt = 0;
         // par is [task][agent]: `rows` consecutive agents of a task are contiguous
         for (int idx = threadIdx.x; idx < ne; idx += blockDim.x) {
             const int ii = idx % rows, j = idx / rows;
             s_par[ii * m + j] = pe[(int64_t)j * n + i0 + ii];
         }
+        for (int x = threadIdx.x; x < rows * W; x += blockDim.x) s_mask[x] = 0ull;
         __syncthreads();
         for (int idx = threadIdx.x; idx < ne; idx += blockDim.x)
-            if (s_par[idx].y != 0.0) s_list[atomicAdd(&s_cnt, 1)] = idx;
+            if (s_par[idx].y != 0.0) {
+                const int ii = idx / m, j = idx - ii * m;
+                atomicOr(&s_mask[ii * W + (j >> 6)], 1ull << (j & 63));
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // exclusive prefix over the chunk's mask words, (agent, word) order
+            int c = 0;
+            for (int x = 0; x < rows * W; ++x) {
+                s_off[x] = c;
+                c += __popcll(s_mask[x]);
+            }
+            s_cnt = c;
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < rows * W; x += blockDim.x) {
+            gm[(int64_t)i0 * W + x] = s_mask[x];
+            go[(int64_t)i0 * W + x] = base + s_off[x];
+        }
+        // each bump's slot in the compact order
+        for (int idx = threadIdx.x; idx < ne; idx += blockDim.x)
+            if (s_par[idx].y != 0.0) {
+                const int ii = idx / m, j = idx - ii * m, w = ii * W + (j >> 6);
+                s_list[s_off[w] + __popcll(s_mask[w] & ((1ull << (j & 63)) - 1ull))] = idx;
+            }
         __syncthreads();
         const int cnt = s_cnt;
-        float *o = te + (int64_t)i0 * m;
         for (int t0 = 0; t0 < T; t0 += kTableTG) {
             const int tg = min(kTableTG, T - t0);
             for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
-                const int id = s_list[k];
-                const double2 p = s_par[id];
-                for (int tt = 0; tt < tg; ++tt) s_tile[tt * ne + id] = (float)mt_par_value(p, t0 + tt);
+                const double2 p = s_par[s_list[k]];
+                for (int tt = 0; tt < tg; ++tt) s_tile[tt * cnt + k] = (float)mt_par_value(p, t0 + tt);
             }
             __syncthreads();
-            // whole rows out (16 B per lane when the rows allow), the tile left zeroed for the next group
-            if ((ne & 3) == 0 && (nm & 3) == 0 && ((R * m) & 3) == 0) {  // (the tile sits at 20 R m bytes)
-                for (int tt = 0; tt < tg; ++tt) {
-                    float4 *o4 = reinterpret_cast<float4 *>(o + (int64_t)(t0 + tt) * nm);
-                    float4 *s4 = reinterpret_cast<float4 *>(s_tile + tt * ne);
-                    for (int id = threadIdx.x; id < (ne >> 2); id += blockDim.x) {
-                        o4[id] = s4[id];
-                        s4[id] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-            } else {
-                for (int tt = 0; tt < tg; ++tt)
-                    for (int id = threadIdx.x; id < ne; id += blockDim.x) {
-                        o[(int64_t)(t0 + tt) * nm + id] = s_tile[tt * ne + id];
-                        s_tile[tt * ne + id] = 0.f;
-                    }
+            for (int tt = 0; tt < tg; ++tt) {  // one contiguous run of `cnt` floats per slice
+                float *o = te + (int64_t)(t0 + tt) * nm + base;
+                for (int k = threadIdx.x; k < cnt; k += blockDim.x) o[k] = s_tile[tt * cnt + k];
             }
             __syncthreads();
         }
+        base += cnt;
     }
 }
 
@@ -1003,7 +1038,7 @@ static BumpSrc bump_src(const EnvState &st) {
                    st.benefit_mode == ASG_BENEFIT_DENSE};
 }
 static TableSrc table_src(const EnvState &st) { return TableSrc{st.table, st.n, st.m, st.T}; }
-static ParSrc par_src(const EnvState &st) { return ParSrc{st.table32, st.mtpar, st.n, st.m, st.T}; }
+static ParSrc par_src(const EnvState &st) { return ParSrc{st.table32, st.mtpar, st.tmask, st.toff, st.n, st.m, st.T}; }
 
 static bool uses_table(const EnvState &st) {
     return st.rng_mode == ASG_RNG_MT19937 || st.benefit_mode == ASG_BENEFIT_INJECTED;
@@ -1014,21 +1049,13 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
         // the two raw MT19937 blocks + the permutation: 5,248 B at m = 64 (29 workgroups in a
         // CU's 160 KiB, LDS in 512-byte granules); with the tempered copies kept
         // (ASG_MT_TEMPER_ON_READ=0) 10,240 B, exactly 16 workgroups
-        const size_t lds = sizeof(uint32_t) * (ASG_MT_TEMPER_ON_READ ? 2 : 4) * kMtN + sizeof(int) * st.m;
-        const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
         // with an injected table (sat_prox_mat=) neither __init__ nor reset draw a
         // table: only the permutation consumes the stream (mock :32-37, :99-105)
-        hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen,
-                           gen);
-        hipError_t err = hipGetLastError();
+        const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
+        hipError_t err = launch_reset_draws(st, construct, s);
         if (err != hipSuccess) return err;
-        if (gen) {
-            const int R = mt_table_rows(st.m);
-            hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), mt_table_lds(R, st.m), s, st.mtpar, st, R);
-            if ((err = hipGetLastError()) != hipSuccess) return err;
-            return launch_reset_src(par_src(st), bv, st, ts, false, s);
-        }
-        return launch_reset_src(table_src(st), bv, st, ts, false, s);
+        return gen ? launch_reset_src(par_src(st), bv, st, ts, false, s)
+                   : launch_reset_src(table_src(st), bv, st, ts, false, s);
     }
     if (uses_table(st)) return launch_reset_src(table_src(st), bv, st, ts, true, s);
     return launch_reset_src(bump_src(st), bv, st, ts, true, s);
@@ -1036,16 +1063,71 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
 
 // The MT19937 mode's reset without its row write: the draws (and the float32 table) only --
 // the episode launch that follows writes the reset row (asg_reset_rollout in the same-seed mode)
+// The draws (one wave per env, latency-bound: the sequential MT19937 consumption) and the table
+// writer (float64 bump evaluations, compute-bound) are pipelined over env chunks on two streams:
+// chunk c's table kernel runs on an auxiliary stream beside chunk c + 1's draws (disjoint envs),
+// each table chunk after its own draws (an event) and after everything before the reset on the
+// caller's stream (so the previous episode's table readers are done), the caller's stream waiting
+// for the last table chunk.  One auxiliary stream and event set per device (handles of one device
+// used from several host threads at once would share them).
+#ifndef ASG_RESET_CHUNKS
+#define ASG_RESET_CHUNKS 8
+#endif
+namespace {
+struct ResetAux {
+    hipStream_t s = nullptr;
+    hipEvent_t ev[ASG_RESET_CHUNKS + 1] = {};
+};
+hipError_t reset_aux(ResetAux **out) {
+    static std::mutex mu;
+    static ResetAux aux[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(mu);
+    ResetAux &a = aux[dev];
+    if (!a.s) {
+        if ((e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        for (auto &ev : a.ev)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    *out = &a;
+    return hipSuccess;
+}
+}  // namespace
+
 hipError_t launch_reset_draws(const EnvState &st, bool construct, hipStream_t s) {
     if (st.rng_mode != ASG_RNG_MT19937) return hipErrorInvalidValue;
     const size_t lds = sizeof(uint32_t) * (ASG_MT_TEMPER_ON_READ ? 2 : 4) * kMtN + sizeof(int) * st.m;
     const bool gen = st.benefit_mode != ASG_BENEFIT_INJECTED;
-    hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen, gen);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess || !gen) return err;
     const int R = mt_table_rows(st.m);
-    hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), mt_table_lds(R, st.m), s, st.mtpar, st, R);
-    return hipGetLastError();
+    const int K = (gen && st.E >= 1024) ? ASG_RESET_CHUNKS : 1;
+    if (K == 1) {
+        hipLaunchKernelGGL(mt_reset_kernel, dim3(st.E), dim3(64), lds, s, st.mt, st, st.mtpar, construct && gen, gen,
+                           (int64_t)0);
+        hipError_t err = hipGetLastError();
+        if (err != hipSuccess || !gen) return err;
+        hipLaunchKernelGGL(mt_table_kernel, dim3(st.E), dim3(256), mt_table_lds(R, st.m), s, st.mtpar, st, R,
+                           (int64_t)0);
+        return hipGetLastError();
+    }
+    ResetAux *ax = nullptr;
+    hipError_t err = reset_aux(&ax);
+    if (err != hipSuccess) return err;
+    for (int c = 0; c < K; ++c) {
+        const int64_t e0 = st.E * c / K, e1 = st.E * (c + 1) / K;
+        hipLaunchKernelGGL(mt_reset_kernel, dim3((unsigned)(e1 - e0)), dim3(64), lds, s, st.mt, st, st.mtpar,
+                           construct, true, e0);
+        if ((err = hipGetLastError()) != hipSuccess) return err;
+        if ((err = hipEventRecord(ax->ev[c], s)) != hipSuccess) return err;
+        if ((err = hipStreamWaitEvent(ax->s, ax->ev[c], 0)) != hipSuccess) return err;
+        hipLaunchKernelGGL(mt_table_kernel, dim3((unsigned)(e1 - e0)), dim3(256), mt_table_lds(R, st.m), ax->s,
+                           st.mtpar, st, R, e0);
+        if ((err = hipGetLastError()) != hipSuccess) return err;
+    }
+    if ((err = hipEventRecord(ax->ev[K], ax->s)) != hipSuccess) return err;
+    return hipStreamWaitEvent(s, ax->ev[K], 0);
 }
 
 hipError_t launch_step(const asg_batch_view &bv, const EnvState &st, int ts, int k, hipStream_t s, bool assign_ready) {

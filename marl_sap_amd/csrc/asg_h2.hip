@@ -1045,6 +1045,10 @@ struct RolloutArgs {
     const double *table;   // injected float64 benefits (rewards), or
     const double2 *par;    // the MT19937 reset's draws: rewards evaluated from them (mt_par_value)
     const float *table32;  // the benefits rounded to float32: the lookahead rows' reads
+    // MT19937 draws: table32 is COMPACT (per (env, t) slice the bump pairs only, (agent, task)
+    // order; asg_env.hip:mt_table_kernel): their masks [E][n][W] and each word's first index
+    const uint64_t *tmask;
+    const int *toff;
     // QOUT instances: the agent's Q rows [E n][m] f32 (the forward of asg_rnn_agent_forward)
     // instead of the epsilon-greedy selection -- a selector outside the kernel (SAP) acts on them
     float *Q;
@@ -1182,7 +1186,7 @@ __device__ __forceinline__ void rollout_actions_from_batch(RA &ra, int64_t e, in
 // one transition (mock_constellation_env.py:116-162 + the runner's rows): rewards, returns,
 // terminated / filled / prev_assigns rows; the tasks come from the LDS (selected in this
 // launch, or read from the batch by the env prologue)
-template <bool TAB, int SQ, class RA>
+template <int TAB, int SQ, class RA>
 __device__ __forceinline__ void rollout_transition(RA &ra, int64_t e, int k, int ts, const EnvKey &key,
                                                    const uint64_t *s_scl, int *s_cnt, uint16_t *s_act,
                                                    uint16_t *s_prev, double *s_ret) {
@@ -1265,6 +1269,32 @@ __device__ __forceinline__ void st_i64x2(int64_t *p, long long a, long long b) {
 // store of the tile: gfx9's vmcnt retires memory operations in order).  After the recurrent
 // layer the tile issues the NEXT agent tile's h_t loads into hN (nsrc: its source rows, row
 // nrow0 on, stride nhs; NULL source = zeros; nmode 0 = no next agent tile in this env).
+// The compact same-seed table (RolloutArgs::tmask): the 4 tasks j0 .. j0 + 3 of a row (j0 % 4 == 0,
+// one mask word) are the set bits `nib` of the row's mask word at sh = j0 % 64, and their values
+// sit at consecutive compact indices from pos = the word's first index + the bumps below sh.  One
+// 16-byte load at pos (4-byte aligned; nib == 0: no load) then the expansion below
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ f32x4 compact_quad_load(const float *slice, uint64_t mw, int off, int sh, bool okrow,
+                                                   uint32_t *nib_out) {
+    const uint32_t nib = okrow ? (uint32_t)(mw >> sh) & 15u : 0u;
+    *nib_out = nib;
+    if (nib == 0u) return f32x4{0.f, 0.f, 0.f, 0.f};
+    const int pos = off + (int)__popcll(mw & ((1ull << sh) - 1ull));
+    const f32x4u x = *reinterpret_cast<const f32x4u *>(slice + pos);
+    return f32x4{x.x, x.y, x.z, x.w};
+}
+__device__ __forceinline__ uint32_t compact_nib(uint64_t mw, int sh, bool okrow) {
+    return okrow ? (uint32_t)(mw >> sh) & 15u : 0u;
+}
+// the quad's 4 values from its packed bumps x (value v = the (rank of v)-th packed one, 0 off the mask)
+__device__ __forceinline__ float4 compact_expand(f32x4 x, uint32_t nib) {
+    const bool b0 = nib & 1u, b1 = nib & 2u, b2 = nib & 4u, b3 = nib & 8u;
+    const float a01 = b0 ? x.y : x.x, a12 = b0 ? x.z : x.y, a23 = b0 ? x.w : x.z;  // rank shifted by b0
+    const float r2 = b1 ? a12 : a01;                                               // rank b0 + b1
+    const float r3 = b2 ? (b1 ? a23 : a12) : (b1 ? a12 : a01);                     // rank b0 + b1 + b2
+    return make_float4(b0 ? x.x : 0.f, b1 ? a01 : 0.f, b2 ? r2 : 0.f, b3 ? r3 : 0.f);
+}
+
 struct HNext {
     const float *src;
     int64_t stride, row0;
@@ -1285,11 +1315,16 @@ struct HNext {
 #ifndef ASG_TAB_PRE
 #define ASG_TAB_PRE 2
 #endif
-constexpr int kTabPre = ASG_TAB_PRE;  // lookahead blocks preloaded per chunk
+constexpr int kTabPre = ASG_TAB_PRE;  // lookahead blocks preloaded per chunk (the dense table)
+// the compact table (MT19937 draws): 1 block (SQ64 GRU instance: 0 VGPRs spilled, 51 with 2, 84
+// with 3; the dense instance: 36 / 19 / 36)
+#ifndef ASG_TAB_PRE_CMP
+#define ASG_TAB_PRE_CMP 1
+#endif
 #ifndef ASG_ROLLOUT_LATE
 #define ASG_ROLLOUT_LATE 1
 #endif
-template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, bool AGENT, int SQ, class RA>
+template <bool RNN, bool W2L, bool GEN, int TAB, bool QOUT, bool AGENT, int SQ, class RA>
 __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk, int tsr, bool stores,
                                              bool have_act, int pass, const EnvKey &key, const uint64_t *s_scl,
                                              uint16_t *s_act, const u32x4v *Wl, const int (&sw)[4],
@@ -1316,6 +1351,22 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
         rows[nt] = e * n + ia[nt];
         act[nt] = (have_act && ok[nt]) ? (int)s_act[ia[nt]] : -1;
     }
+    // the compact same-seed table's mask words / offsets of the lane's rows (chunk u's word is
+    // u / 2): loaded here, with the gather, before the tile's stores -- once per tile when the
+    // shape is compile-time 64 tasks (one word), per chunk otherwise
+    constexpr bool cmp = TAB == 2;  // the compact same-seed table (MT19937 draws)
+    uint64_t cmw[NT];
+    int cof[NT];
+    auto load_cm = [&](int w) {
+        const int W = (m + 63) >> 6;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int64_t r = (e * n + (ok[nt] ? ia[nt] : 0)) * W + w;
+            cmw[nt] = cmp ? ra.tmask[r] : 0ull;
+            cof[nt] = cmp ? ra.toff[r] : 0;
+        }
+    };
+    if (cmp && SQ == 64) load_cm(0);
     // row stores: batch row tsr (timing variant 32: row 1, env e & 7)
     const int tss = (ASG_ROLLOUT_XSKIP & 32) ? 1 : tsr;
     const int64_t sro = (ASG_ROLLOUT_XSKIP & 32) ? ((e & 7) - e) * n : 0;
@@ -1433,10 +1484,12 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
             // table modes: the chunk's lookahead values of the first kTabPre blocks, loaded at
             // once at the chunk start (in place of the Philox parameters): one wait behind the
             // tile's stores per chunk instead of one per block (gfx9's in-order vmcnt)
-            float4 tv[kTabPre][2][NT];
+            constexpr int kPre = TAB == 2 ? ASG_TAB_PRE_CMP : kTabPre;
+            float4 tv[kPre][2][NT];
+            if (cmp && SQ != 64) load_cm(u >> 1);
             if constexpr (TAB && ASG_TAB_PRELOAD) {
 #pragma unroll
-                for (int l = 1; l <= kTabPre; ++l) {
+                for (int l = 1; l <= kPre; ++l) {
                     const int t = kk + l - 1;
                     if (l > L || t >= T) continue;
                     const float *trow = ra.table32 + ((int64_t)e * T + t) * n * m;
@@ -1446,7 +1499,11 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                         for (int nt = 0; nt < NT; ++nt) {
                             const int j0 = 32 * u + 16 * c + 4 * q;
                             const float *tp = trow + (int64_t)ia[nt] * m + j0;
-                            if (!GEN) {
+                            if constexpr (cmp) {  // the packed bumps: expanded at their use
+                                uint32_t nb;
+                                const f32x4 x = compact_quad_load(trow, cmw[nt], cof[nt], j0 & 63, ok[nt] && j0 < m, &nb);
+                                tv[l - 1][c][nt] = make_float4(x.x, x.y, x.z, x.w);
+                            } else if (!GEN) {
                                 tv[l - 1][c][nt] = *reinterpret_cast<const float4 *>(tp);
                             } else {
                                 float v4[4];
@@ -1503,7 +1560,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                 // the 2 x NT x 4 bump values, straight-line (one uniform branch per block: rows
                 // past T are zeros)
                 float4 xv[2][NT];
-                if (TAB && ASG_TAB_PRELOAD && t < T && l <= kTabPre) {
+                if (TAB && ASG_TAB_PRELOAD && t < T && l <= kPre) {
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -1511,7 +1568,12 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                             // l is a loop variable: the preloaded block by a uniform select
                             float4 x = tv[0][c][nt];
 #pragma unroll
-                            for (int ll = 2; ll <= kTabPre; ++ll) x = l == ll ? tv[ll - 1][c][nt] : x;
+                            for (int ll = 2; ll <= kPre; ++ll) x = l == ll ? tv[ll - 1][c][nt] : x;
+                            if constexpr (cmp) {
+                                const int j0 = 32 * u + 16 * c + 4 * q;
+                                x = compact_expand(f32x4{x.x, x.y, x.z, x.w},
+                                                   compact_nib(cmw[nt], j0 & 63, ok[nt] && j0 < m));
+                            }
                             xv[c][nt] = x;
                         }
                 } else if (TAB && t < T) {
@@ -1525,7 +1587,11 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
                         for (int nt = 0; nt < NT; ++nt) {
                             const int j0 = 32 * u + 16 * c + 4 * q;
                             const float *tp = trow + (int64_t)ia[nt] * m + j0;
-                            if (!GEN) {
+                            if constexpr (cmp) {
+                                uint32_t nb;
+                                const f32x4 x = compact_quad_load(trow, cmw[nt], cof[nt], j0 & 63, ok[nt] && j0 < m, &nb);
+                                xv[c][nt] = compact_expand(x, nb);
+                            } else if (!GEN) {
                                 xv[c][nt] = *reinterpret_cast<const float4 *>(tp);
                             } else {
                                 float v4[4];
@@ -1665,7 +1731,7 @@ __device__ __forceinline__ void rollout_tile(RA &ra, int64_t e, int sub, int kk,
     }
 }
 
-template <bool RNN, bool W2L, bool GEN, bool TAB, bool QOUT, int SQ>
+template <bool RNN, bool W2L, bool GEN, int TAB, bool QOUT, int SQ>
 __global__ void __launch_bounds__(64 * kH2Waves) __attribute__((amdgpu_waves_per_eu(kH2WavesPerSimd)))
 rollout_kernel(RolloutArgs ra) {
     extern __shared__ u32x4v s_h2[];
@@ -1804,7 +1870,9 @@ struct RolloutLaunch {
     bool rnn, w2l, gen;
     bool sq64;  // n = m = 64 (W2 in LDS, no ragged tiles): the compile-time-shape instances
 };
-template <bool TAB, bool QOUT>
+// TAB: 0 = Philox bumps, 1 = the dense float32 table (injected sat_prox_mat), 2 = the compact
+// one (MT19937 draws: RolloutArgs::tmask)
+template <int TAB, bool QOUT>
 static hipError_t launch_rollout_inst(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
 #define LR_(RNN, W2L, GEN, SQ) \
     hipLaunchKernelGGL((rollout_kernel<RNN, W2L, GEN, TAB, QOUT, SQ>), dim3(lc.grid), dim3(64 * kH2Waves), lc.lds, s, ra)
@@ -1828,11 +1896,12 @@ hipError_t launch_rollout_q(const RolloutArgs &ra, const RolloutLaunch &lc, hipS
 
 #if ASG_H2_TU == 1
 hipError_t launch_rollout_tab(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
-    return launch_rollout_inst<true, false>(ra, lc, s);
+    return ra.tmask ? launch_rollout_inst<2, false>(ra, lc, s) : launch_rollout_inst<1, false>(ra, lc, s);
 }
 #elif ASG_H2_TU == 2
 hipError_t launch_rollout_q(const RolloutArgs &ra, const RolloutLaunch &lc, hipStream_t s) {
-    return ra.table32 ? launch_rollout_inst<true, true>(ra, lc, s) : launch_rollout_inst<false, true>(ra, lc, s);
+    if (!ra.table32) return launch_rollout_inst<0, true>(ra, lc, s);
+    return ra.tmask ? launch_rollout_inst<2, true>(ra, lc, s) : launch_rollout_inst<1, true>(ra, lc, s);
 }
 #else
 // shapes the rollout kernel takes: the split-f16 agent with the mock env's obs layout
@@ -1893,6 +1962,8 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     ra.table = tab ? st.table : nullptr;
     ra.par = tab ? st.mtpar : nullptr;
     ra.table32 = tab ? st.table32 : nullptr;
+    ra.tmask = tab ? st.tmask : nullptr;  // set only in the MT19937 draws mode (compact table)
+    ra.toff = tab ? st.toff : nullptr;
     // the table modes' reset in this launch: the MT19937 draws ran before it (asg_reset_rollout)
     // Q output: one transition and the forward of the row after it (asg_step_forward)
     // or (asg_reset_forward) the envs' reset and the forward on the reset row, no transition
@@ -1937,7 +2008,7 @@ hipError_t launch_rollout(const RolloutSlabs &sl, const EnvState &st, int ts, in
     if (lc.sq64 && ASG_ROLLOUT_L2FIRST && plan.l2_slices >= 1) ra.w1_off = 1;
     if (Q) return launch_rollout_q(ra, lc, s);
     if (tab) return launch_rollout_tab(ra, lc, s);
-    return launch_rollout_inst<false, false>(ra, lc, s);
+    return launch_rollout_inst<0, false>(ra, lc, s);
 }
 #endif  // ASG_H2_TU
 

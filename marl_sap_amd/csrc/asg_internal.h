@@ -30,7 +30,11 @@ struct EnvState {
     int *prev;             // [E][n] previous assignment (state for beta_hat)
     double *returns;       // [E] float64 episode returns
     double *table;         // [E][T][n][m] float64 (injected mode only)
-    float *table32;        // [E][T][n][m] the benefits rounded to float32 (the rows' dtype; MT19937 / injected)
+    float *table32;        // [E][T][n][m] the benefits rounded to float32 (the rows' dtype; MT19937 / injected);
+                           // MT19937 draws: COMPACT -- per (env, t) slice only the env's bump pairs, in
+                           // (agent, task) order (the other pairs are exactly 0), see tmask / toff
+    uint64_t *tmask;       // [E][n][W] (W = ceil(m / 64)) bump pairs of the compact table (MT19937 draws)
+    int *toff;             // [E][n][W] compact index of each mask word's first pair
     uint32_t *mt;          // [E][625] MT19937 key + pos (compat mode)
     double2 *mtpar;        // [E][m][n] the reset's bump draws (center, +-spread; 0: no bump) (compat mode):
                            // the float64 benefits are mt_par_value() of these, no float64 table is kept
