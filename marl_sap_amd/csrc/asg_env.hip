@@ -857,15 +857,10 @@ __global__ void __launch_bounds__(64) mt_reset_kernel(uint32_t *mtstate, EnvStat
 // their masks tmask [E][n][W] and each mask word's first compact index toff [E][n][W] -- the
 // episode kernel then reads ~1/4 of a dense slice per lookahead block.  Per chunk of `rows`
 // agents (rows * m <= 1024): the draws staged transposed in LDS, the chunk's pair masks built
-// (LDS 64-bit OR), the compact order listed, then per group of kTableTG times each bump's values
-// evaluated by one thread (the float64 exp / division for bumps only) into an LDS tile written
-// out as contiguous compact runs.  The float64 values are not stored: their readers evaluate them
-// from the draws (ParSrc).
-#ifndef ASG_TABLE_TG
-#define ASG_TABLE_TG 4
-#endif
-constexpr int kTableTG = ASG_TABLE_TG;
-// agents per chunk of the table kernel (rows * m <= 1024 floats per time slice of the tile)
+// (LDS 64-bit OR) and the compact order listed; then one thread per bump evaluates its T values
+// (the float64 sigma_2 once, the exp / division per value: for bumps only) and stores them
+// straight into the T slices -- consecutive threads, consecutive compact indices.  The float64
+// values are not stored: their readers evaluate them from the draws (ParSrc).
 #ifndef ASG_TABLE_ROWS
 #define ASG_TABLE_ROWS 16
 #endif
@@ -874,15 +869,13 @@ static int mt_table_rows(int m) {
 }
 static size_t mt_table_lds(int R, int m) {
     const size_t W = (m + 63) / 64;
-    return (sizeof(double2) + sizeof(int) + sizeof(float) * kTableTG) * (size_t)R * m +
-           (sizeof(uint64_t) + sizeof(int)) * (size_t)R * W;
+    return (sizeof(double2) + sizeof(int)) * (size_t)R * m + 8 + (sizeof(uint64_t) + sizeof(int)) * (size_t)R * W;
 }
 __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvState st, int R, int64_t e0 = 0) {
     extern __shared__ double2 s_par[];                               // [R agents][m tasks]
     int *s_list = reinterpret_cast<int *>(s_par + R * st.m);         // the chunk's bumps, compact order
-    float *s_tile = reinterpret_cast<float *>(s_list + R * st.m);    // [kTableTG][chunk's bumps]
     const int W = (st.m + 63) >> 6;
-    unsigned long long *s_mask = reinterpret_cast<unsigned long long *>(s_tile + kTableTG * R * st.m);  // [R][W]
+    unsigned long long *s_mask = reinterpret_cast<unsigned long long *>(s_list + R * st.m + ((R * st.m) & 1));
     int *s_off = reinterpret_cast<int *>(s_mask + R * W);           // [R][W] compact index (chunk-relative)
     __shared__ int s_cnt;
     const int64_t e = e0 + blockIdx.x;
@@ -930,18 +923,12 @@ __global__ void __launch_bounds__(256) mt_table_kernel(const double2 *par, EnvSt
             }
         __syncthreads();
         const int cnt = s_cnt;
-        for (int t0 = 0; t0 < T; t0 += kTableTG) {
-            const int tg = min(kTableTG, T - t0);
-            for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
-                const double2 p = s_par[s_list[k]];
-                for (int tt = 0; tt < tg; ++tt) s_tile[tt * cnt + k] = (float)mt_par_value(p, t0 + tt);
-            }
-            __syncthreads();
-            for (int tt = 0; tt < tg; ++tt) {  // one contiguous run of `cnt` floats per slice
-                float *o = te + (int64_t)(t0 + tt) * nm + base;
-                for (int k = threadIdx.x; k < cnt; k += blockDim.x) o[k] = s_tile[tt * cnt + k];
-            }
-            __syncthreads();
+        float *o = te + base;
+        for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+            const double2 p = s_par[s_list[k]];
+            // mt_par_value(p, t) for every t, sigma_2 hoisted (the same float64 operations)
+            const double scale = p.y < 0.0 ? 10.0 : 1.0, s2 = bump_s2(__builtin_fabs(p.y));
+            for (int t = 0; t < T; ++t) o[(int64_t)t * nm + k] = (float)bump_value(scale, p.x, s2, t);
         }
         base += cnt;
     }
@@ -1071,7 +1058,7 @@ hipError_t launch_reset(const asg_batch_view &bv, const EnvState &st, int ts, bo
 // for the last table chunk.  One auxiliary stream and event set per device (handles of one device
 // used from several host threads at once would share them).
 #ifndef ASG_RESET_CHUNKS
-#define ASG_RESET_CHUNKS 8
+#define ASG_RESET_CHUNKS 1  // 2 / 4 / 8 measured no faster (r6 A/B): one launch each
 #endif
 namespace {
 struct ResetAux {

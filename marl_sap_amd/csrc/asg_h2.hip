@@ -200,7 +200,8 @@ constexpr int kH2SxInit = 11;                   // fc1 input scale of the first 
 // bit 64: the tiles' bump parameters from a cheap hash instead of Philox (VALU); bit 256: no env
 // transition between the steps (rewards, returns, the transition's rows); bit 512: the return
 // not summed in agent order (one readlane); bit 1024: the transition's rewards without the bump
-// (Philox + float64 exp: beta = 0)
+// (Philox + float64 exp: beta = 0); bit 2048: the compact table's quads not loaded (a constant,
+// the mask / expansion kept); bit 4096: the compact quads loaded but not expanded
 #if defined(ASG_ROLLOUT_XSKIP) && !defined(ASG_TIMING_EXPERIMENTS)
 #error "ASG_ROLLOUT_XSKIP gives wrong results: timing experiments only (-DASG_TIMING_EXPERIMENTS)"
 #endif
@@ -1280,6 +1281,7 @@ __device__ __forceinline__ f32x4 compact_quad_load(const float *slice, uint64_t 
     *nib_out = nib;
     if (nib == 0u) return f32x4{0.f, 0.f, 0.f, 0.f};
     const int pos = off + (int)__popcll(mw & ((1ull << sh) - 1ull));
+    if (ASG_ROLLOUT_XSKIP & 2048) return f32x4{0.5f, 0.25f, 0.125f, (float)pos};
     const f32x4u x = *reinterpret_cast<const f32x4u *>(slice + pos);
     return f32x4{x.x, x.y, x.z, x.w};
 }
@@ -1288,6 +1290,7 @@ __device__ __forceinline__ uint32_t compact_nib(uint64_t mw, int sh, bool okrow)
 }
 // the quad's 4 values from its packed bumps x (value v = the (rank of v)-th packed one, 0 off the mask)
 __device__ __forceinline__ float4 compact_expand(f32x4 x, uint32_t nib) {
+    if (ASG_ROLLOUT_XSKIP & 4096) return make_float4(x.x, x.y, x.z, x.w + (float)nib);
     const bool b0 = nib & 1u, b1 = nib & 2u, b2 = nib & 4u, b3 = nib & 8u;
     const float a01 = b0 ? x.y : x.x, a12 = b0 ? x.z : x.y, a23 = b0 ? x.w : x.z;  // rank shifted by b0
     const float r2 = b1 ? a12 : a01;                                               // rank b0 + b1

@@ -10,7 +10,7 @@ B="bench.py --cpu-baseline 0 --secondary 0"
 for st in "$@"; do
   case "$st" in
     tests*)
-      K=${st#tests}; K=${K#:}
+      K=${TESTK:-}
       timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${K:+-k "$K"} > "$OUT/tests.log" 2>&1
       rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|error" "$OUT/tests.log" | tail -5; fatal $rc tests ;;
     smoke)
@@ -38,6 +38,15 @@ for st in "$@"; do
       python3 tools/pmc_real_summary.py "$OUT/pmc_real_FETCH_SIZE" "$OUT/pmc_real_WRITE_SIZE" "$OUT/pmc_real_step.json" --E $RE
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_real" -o run -- python3 tools/bench_real_env.py --envs $RE --steps 20 --cpu 0 > "$OUT/kt_real.log" 2>&1
       rc=$?; echo "kt real rc=$rc"; fatal $rc kt_real ;;
+    real_sq)
+      RE=${REAL_ENVS:-512}
+      SQ1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+      SQ2="SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_COUNT"
+      i=1
+      for set in "$SQ1" "$SQ2"; do
+        timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d "$OUT/sq_real$i" -o run -- python3 tools/bench_real_env.py --envs $RE --steps 3 --cpu 0 > "$OUT/sq_real$i.log" 2>&1
+        rc=$?; echo "sq real $i rc=$rc"; fatal $rc sq_real$i; i=$((i+1))
+      done ;;
     *) echo "unknown step $st" ;;
   esac
 done
