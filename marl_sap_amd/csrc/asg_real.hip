@@ -396,8 +396,27 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
     return (size_t)S * m * 8 + (size_t)S * ((m + 3) & ~3);
 }
 
+// the strip's grouped-load path: kStripJG task iterations (of 64) per load group, L <= kStripLM
+#ifndef ASG_STRIP_JG
+#define ASG_STRIP_JG 2
+#endif
+#ifndef ASG_STRIP_GROUPED
+#define ASG_STRIP_GROUPED 1
+#endif
+#ifndef ASG_OBS_TWOPHASE
+#define ASG_OBS_TWOPHASE 1
+#endif
+constexpr int kStripJG = ASG_STRIP_JG, kStripLM = 3;
+// ASG_STRIP_WAVES: waves per SIMD the strip kernel is compiled for (0: the allocator's choice)
+#ifndef ASG_STRIP_WAVES
+#define ASG_STRIP_WAVES 0
+#endif
 template <int CAP>
-__global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
+__global__ void __launch_bounds__(1024)
+#if ASG_STRIP_WAVES
+__attribute__((amdgpu_waves_per_eu(ASG_STRIP_WAVES)))
+#endif
+real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
                                                           int knew, int step, int S) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, M = st.M, MD = st.M + st.M / 2;
@@ -425,7 +444,46 @@ __global__ void __launch_bounds__(1024) real_strip_kernel(asg_batch_view bv, asg
         eff = eff < 0 ? 0 : eff;
         const int pa = prev[i];
         double *trow = tl + (int64_t)r * m;
-        if (fast) {
+        if (ASG_STRIP_GROUPED && fast && L <= kStripLM) {
+            // the row's table values in groups of kStripJG task iterations: every load of a group
+            // (the L slices and the priorities) is issued before the group's stores -- gfx9 retires
+            // loads and stores in order, so a load issued behind a store waits for its acknowledgement
+            __half *bb = reinterpret_cast<__half *>(bv.beta.ptr) + foff(bv.beta, e, row, i, 0);
+            uint8_t *ab = reinterpret_cast<uint8_t *>(bv.avail_actions.ptr) + foff(bv.avail_actions, e, row, i, 0);
+            int16_t *ob = step && bv.actions_onehot.ptr
+                              ? reinterpret_cast<int16_t *>(bv.actions_onehot.ptr) + foff(bv.actions_onehot, e, ts, i, 0)
+                              : nullptr;
+            const int64_t bs3 = bv.beta.stride[3], as3 = bv.avail_actions.stride[3];
+            const int64_t os3 = ob ? bv.actions_onehot.stride[3] : 0;
+            for (int jb = 0; jb < m; jb += 64 * kStripJG) {
+                double v[kStripJG][kStripLM], pr[kStripJG];
+#pragma unroll
+                for (int g = 0; g < kStripJG; ++g) {
+                    const int j = jb + 64 * g + lane;
+                    pr[g] = j < m ? st.prios[j] : 0.0;
+#pragma unroll
+                    for (int l = 0; l < kStripLM; ++l) v[g][l] = (j < m && l < eff) ? t0[l * slice + j] : 0.0;
+                }
+#pragma unroll
+                for (int g = 0; g < kStripJG; ++g) {
+                    const int j = jb + 64 * g + lane;
+                    if (j >= m) continue;
+                    double sum = 0.0;
+#pragma unroll
+                    for (int l = 0; l < kStripLM; ++l) {
+                        if (l >= L) break;
+                        const double b = v[g][l] * pr[g];
+                        sum = l == 0 ? b : sum + b;
+                        if (!(ASG_REAL_PROF_SKIP & 2)) bb[j * bs3 + l] = __float2half((float)b);
+                    }
+                    trow[j] = sum;
+                    if (!(ASG_REAL_PROF_SKIP & 2)) {
+                        ab[j * as3] = 1;
+                        if (ob) ob[j * os3] = (int16_t)(pa == j);
+                    }
+                }
+            }
+        } else if (fast) {
             __half *bb = reinterpret_cast<__half *>(bv.beta.ptr) + foff(bv.beta, e, row, i, 0);
             uint8_t *ab = reinterpret_cast<uint8_t *>(bv.avail_actions.ptr) + foff(bv.avail_actions, e, row, i, 0);
             int16_t *ob = step && bv.actions_onehot.ptr
@@ -505,6 +563,7 @@ __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, i
 // XCD-aware grid: workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD
 // b % 8), so block b serves env 8 * ((b / 8) / G) + b % 8: all G workgroups of an env
 // land on one XCD and its [m][n] totals are fetched into one L2, not eight.
+constexpr int kObsG = 16;  // observation entries per lane of the two-phase copy (obs_size <= 1024)
 template <int CAP>
 __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     extern __shared__ unsigned char s_raw[];
@@ -590,6 +649,40 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
         }
         store_real(bv.obs, o0 + p, real_beta(st, tab, knew, a, j, l));
     };
+    if (ASG_OBS_TWOPHASE && copy && bv.obs.dtype == ASG_F16 && osz <= 64 * kObsG && !(ASG_REAL_PROF_SKIP & 16)) {
+        // the row's benefit entries gathered from the beta row first, then stored: a load issued
+        // behind a store waits for its acknowledgement (gfx9's in-order vmcnt)
+        const uint16_t *bsrc = reinterpret_cast<const uint16_t *>(bv.beta.ptr) + b0;
+        uint16_t *odst = reinterpret_cast<uint16_t *>(bv.obs.ptr) + o0;
+        uint16_t val[kObsG];
+#pragma unroll
+        for (int g = 0; g < kObsG; ++g) {
+            const int p = lane + 64 * g;
+            int a = -1, j = 0, l = 0;
+            if (p < r1) {
+                a = i, j = top[p / L], l = p % L;
+            } else if (p < r2) {
+                const int x = p - r1, q = x / (M * L), y = x - q * M * L;
+                a = topn[q], j = top[y / L], l = y % L;
+            } else if (p < r3) {
+                const int x = p - r2, q = x / (M2 * L), y = x - q * M2 * L;
+                a = topn[q], j = oth[q * M2 + y / L], l = y % L;
+            }
+            val[g] = (p < r3) ? bsrc[a * bv.beta.stride[2] + j * bv.beta.stride[3] + l] : (uint16_t)0;
+        }
+#pragma unroll
+        for (int g = 0; g < kObsG; ++g) {
+            const int p = lane + 64 * g;
+            if (p < r3) {
+                odst[p] = val[g];
+            } else if (p < r4) {
+                store_real(bv.obs, o0 + p, top[p - r3] == pi ? 1.0 : 0.0);
+            } else if (p < osz) {  // [power_i, power[top_n]] (real_power_constellation_env.py:226-229)
+                store_real(bv.obs, o0 + p, p == r4 ? pw[i] : pw[topn[p - r4 - 1]]);
+            }
+        }
+        return;
+    }
     for (int p = lane; p < ((ASG_REAL_PROF_SKIP & 16) ? 0 : osz); p += 64) {
         if (p < r1) {
             bval(i, top[p / L], p % L, p);
