@@ -398,7 +398,7 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
 
 // the strip's grouped-load path: kStripJG task iterations (of 64) per load group, L <= kStripLM
 #ifndef ASG_STRIP_JG
-#define ASG_STRIP_JG 2
+#define ASG_STRIP_JG 1
 #endif
 #ifndef ASG_STRIP_GROUPED
 #define ASG_STRIP_GROUPED 1
@@ -407,9 +407,11 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
 #define ASG_OBS_TWOPHASE 1
 #endif
 constexpr int kStripJG = ASG_STRIP_JG, kStripLM = 3;
-// ASG_STRIP_WAVES: waves per SIMD the strip kernel is compiled for (0: the allocator's choice)
+// ASG_STRIP_WAVES: waves per SIMD the strip kernel is compiled for (0: the allocator's choice).
+// 8 (64 VGPRs, a few spills outside the row loop) measured 1.69 ms per real step at E = 512 against
+// 1.83 at 7 waves and 1.90 at the allocator's 80 VGPRs (profiles/r6_real_ab_s8.txt)
 #ifndef ASG_STRIP_WAVES
-#define ASG_STRIP_WAVES 0
+#define ASG_STRIP_WAVES 8
 #endif
 template <int CAP>
 __global__ void __launch_bounds__(1024)
