@@ -48,7 +48,7 @@ struct RealState {
     const double *T_trans;  // [m][m]
     int *prev;              // [E][n]
     double *returns;        // [E]
-    double *totT;           // [E][m][n] L-summed totals of the current beta, task-major
+    float *totT;            // [E][m][n] L-summed totals of the current beta rounded to float32, task-major
     int *topA;              // [E][n][M]        each agent's top-M tasks, ties -> lower index
     int *topD;              // [E][n][M + M/2]  its top tasks, ties -> higher index
     int *err;
@@ -105,21 +105,21 @@ __device__ __forceinline__ double real_beta(const RealState &st, const double *t
 // wave-wide selection of the best remaining candidate: value order descending, ties to the
 // lower index (HIGHER_TIES = false, np.argsort(-x) stable) or to the higher index
 // (HIGHER_TIES = true: the tail of an ascending stable argsort)
-template <bool HIGHER_TIES>
-__device__ __forceinline__ int wave_select(const double *vals, unsigned char *taken, int len) {
+template <bool HIGHER_TIES, class V = double>
+__device__ __forceinline__ int wave_select(const V *vals, unsigned char *taken, int len) {
     const int lane = threadIdx.x & 63;
-    double bv = -INFINITY;
+    V bv = -INFINITY;
     int bj = -1;
     for (int j = lane; j < len; j += 64) {
         if (taken[j]) continue;
-        const double v = vals[j];
+        const V v = vals[j];
         const bool better = bj < 0 || v > bv || (v == bv && (HIGHER_TIES ? j > bj : j < bj));
         if (better) {
             bv = v;
             bj = j;
         }
     }
-    const double vmax = wave_allreduce(bj >= 0 ? bv : -INFINITY, [](double a, double b) { return a > b ? a : b; });
+    const V vmax = wave_allreduce(bj >= 0 ? bv : (V)-INFINITY, [](V a, V b) { return a > b ? a : b; });
     int key;
     if (HIGHER_TIES) {
         key = wave_max_i32(bj >= 0 && bv == vmax ? bj : -1);
@@ -135,20 +135,20 @@ __device__ __forceinline__ int wave_select(const double *vals, unsigned char *ta
 // heads back from LDS and reduces float32-rounded keys (one DPP-fused max): rounding is
 // monotone, so a unique maximal key is the unique float64 maximum; equal keys take the
 // exact path (float64 compare against the first candidate, then the index rule).  The
-// winning lane shifts its index list -- no rescans.
-template <int CAP, bool HIGHER_TIES>
-__device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int K, int *out) {
+// winning lane shifts its index list -- no rescans.  (V = float: the keys are the values.)
+template <int CAP, bool HIGHER_TIES, class V = double>
+__device__ __forceinline__ void wave_topk_heads(const V *vals, int len, int K, int *out) {
     const int lane = threadIdx.x & 63;
     int id[CAP];
     {
-        double v[CAP];
+        V v[CAP];
 #pragma unroll
         for (int c = 0; c < CAP; ++c) {
             const int j = lane + 64 * c;
             v[c] = j < len ? vals[j] : -INFINITY;
             id[c] = j < len ? j : -1;  // -1: no candidate (sorts last, never wins)
         }
-        auto before = [](double va, int ia, double vb, int ib) {
+        auto before = [](V va, int ia, V vb, int ib) {
             if (ia < 0) return false;
             if (ib < 0) return true;
             return va > vb || (va == vb && (HIGHER_TIES ? ia > ib : ia < ib));
@@ -158,7 +158,7 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
 #pragma unroll
             for (int c = pass & 1; c + 1 < CAP; c += 2)
                 if (before(v[c + 1], id[c + 1], v[c], id[c])) {
-                    const double tv = v[c];
+                    const V tv = v[c];
                     v[c] = v[c + 1];
                     v[c + 1] = tv;
                     const int ti = id[c];
@@ -168,7 +168,7 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
     }
     for (int k = 0; k < K; ++k) {
         const bool has = id[0] >= 0;
-        const double x = has ? vals[id[0]] : -INFINITY;
+        const V x = has ? vals[id[0]] : (V)-INFINITY;
         const float key = has ? (float)x : -INFINITY;
         const float kmax = wave_max_f32_nonan(key);
         uint64_t cm = __ballot(has && key == kmax);
@@ -178,14 +178,19 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
         int wl = (int)__builtin_ctzll(cm);  // winning lane
         if (__popcll(cm) != 1) {
             // equal keys: exact float64 maximum among them, then the index rule
-            const uint64_t xb = __builtin_bit_cast(uint64_t, x);
-            const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)xb, wl);
-            const uint32_t hi0 = __builtin_amdgcn_readlane((int)(uint32_t)(xb >> 32), wl);
-            double vmax = __builtin_bit_cast(double, (uint64_t)lo0 | ((uint64_t)hi0 << 32));
+            V vmax;
+            if constexpr (sizeof(V) == 8) {
+                const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+                const uint32_t lo0 = __builtin_amdgcn_readlane((int)(uint32_t)xb, wl);
+                const uint32_t hi0 = __builtin_amdgcn_readlane((int)(uint32_t)(xb >> 32), wl);
+                vmax = __builtin_bit_cast(V, (uint64_t)lo0 | ((uint64_t)hi0 << 32));
+            } else {
+                vmax = __builtin_bit_cast(V, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), wl));
+            }
             uint64_t cand = cm;
             if ((__ballot(x != vmax) & cm) != 0) {
                 const bool in = __builtin_amdgcn_inverse_ballot_w64(cm);
-                vmax = wave_allreduce(in ? x : -INFINITY, [](double a, double b) { return a > b ? a : b; });
+                vmax = wave_allreduce(in ? x : (V)-INFINITY, [](V a, V b) { return a > b ? a : b; });
                 cand = __ballot(x == vmax) & cm;
             }
             if (cand == 0) cand = cm;  // NaN maximum: the index rule over all candidates
@@ -205,16 +210,16 @@ __device__ __forceinline__ void wave_topk_heads(const double *vals, int len, int
 
 // top-K: register heads when len <= 64 * CAP (CAP > 0, chosen per kernel instance so each
 // gets its own register budget), else K rescans (CAP = 0; taken: [len] scratch)
-template <int CAP, bool HIGHER_TIES>
-__device__ __forceinline__ void wave_topk(const double *vals, int len, int K, int *out, unsigned char *taken) {
+template <int CAP, bool HIGHER_TIES, class V = double>
+__device__ __forceinline__ void wave_topk(const V *vals, int len, int K, int *out, unsigned char *taken) {
     if constexpr (CAP > 0) {
-        wave_topk_heads<CAP, HIGHER_TIES>(vals, len, K, out);
+        wave_topk_heads<CAP, HIGHER_TIES, V>(vals, len, K, out);
     } else {
         const int lane = threadIdx.x & 63;
         for (int j = lane; j < len; j += 64) taken[j] = 0;
         wave_sync();
         for (int c = 0; c < K; ++c) {
-            const int j = wave_select<HIGHER_TIES>(vals, taken, len);
+            const int j = wave_select<HIGHER_TIES, V>(vals, taken, len);
             if (lane == 0) {
                 out[c] = j;
                 taken[j] = 1;
@@ -386,7 +391,8 @@ __global__ void __launch_bounds__(256) real_reset_kernel(RealState st) {
 // strip of S agents of one env --------------------------------------------------------
 // Writes beta (float16 [n][m][L]), avail, prev_assigns, filled (and, after a step, the
 // one-hot of the actions at row ts); keeps the strip's L-summed totals in LDS, writes
-// them task-major (totT, coalesced per task across the strip) and ranks each agent's row:
+// them task-major rounded to float32 (totT, coalesced per task across the strip; the
+// observation pass's competitor prefilter) and ranks each agent's row:
 //   topA[a] = the M best tasks, ties to the lower index      (np.argsort(-total)[:M], :192)
 //   topD[a] = the M + M/2 best tasks, ties to the higher index (the order of the tail of
 //             np.argsort(row)[:, -M//2:], :212-214); an agent's M/2 best tasks outside
@@ -531,10 +537,10 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
     if (blockIdx.x == 0 && threadIdx.x == 0 && bv.filled.ptr) store_int(bv.filled, foff(bv.filled, e, row, 0, 0), 1);
     __syncthreads();
     if (knew >= st.T) return;  // done: no observation pass follows
-    double *totT = st.totT + e * (int64_t)n * m;
+    float *totT = st.totT + e * (int64_t)n * m;
     for (int64_t p = threadIdx.x; p < (int64_t)rows * m; p += blockDim.x) {
         const int j = (int)(p / rows), r = (int)(p - (int64_t)j * rows);
-        totT[(int64_t)j * n + i0 + r] = tl[(int64_t)r * m + j];
+        totT[(int64_t)j * n + i0 + r] = (float)tl[(int64_t)r * m + j];
     }
     // rank each agent row of the strip, one wave per row
     unsigned char *taken = taken_all + (size_t)wave * ((m + 3) & ~3);
@@ -554,10 +560,11 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
 }
 
 // ---- kernel 3: observation rows, one wave per agent ---------------------------------------
-// per-wave LDS of the observation pass: best[n] f64, taken[n], top[M], topn[N], oth[N][M/2]
+// per-wave LDS of the observation pass: best[n] f64, best32[n] f32, taken[n], top[max(M, 10)]
+// (padded with top[0]), topn[N], oth[N][M/2], tmask[ceil(m / 32)] (agent i's top-M tasks as a bit set)
 __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, int N, int M) {
-    (void)m;
-    return ((size_t)n * 9 + 3 + 4 * (size_t)(M + N + N * (M / 2)) + 15) & ~(size_t)15;
+    const int Mp = M > 10 ? M : 10;
+    return ((size_t)n * 13 + 3 + 4 * (size_t)(Mp + N + N * (M / 2) + (m + 31) / 32) + 15) & ~(size_t)15;
 }
 
 // Observation pass, one wave per (env, agent i): competitors from the task-major totals,
@@ -566,8 +573,14 @@ __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, i
 // b % 8), so block b serves env 8 * ((b / 8) / G) + b % 8: all G workgroups of an env
 // land on one XCD and its [m][n] totals are fetched into one L2, not eight.
 constexpr int kObsG = 16;  // observation entries per lane of the two-phase copy (obs_size <= 1024)
+constexpr int kObsMD = 24; // topD list entries per competitor loaded at once (M + M/2 <= 24)
+constexpr int kObsMB = 10; // top tasks per agent held in registers by the competitor scan (M <= 10)
+#ifndef ASG_OBS_PIPE
+#define ASG_OBS_PIPE 1
+#endif
 template <int CAP>
-__global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, N = st.N, M = st.M, M2 = st.M / 2, MD = st.M + st.M / 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
@@ -582,48 +595,151 @@ __global__ void __launch_bounds__(256) real_obs_kernel(asg_batch_view bv, RealSt
     }
     const size_t per_wave = real_obs_lds_per_wave(n, m, N, M);
     unsigned char *base = s_raw + per_wave * wave;
-    double *best = reinterpret_cast<double *>(base);             // [n]
-    unsigned char *taken = base + 8 * (size_t)n;                 // [n]
+    double *best = reinterpret_cast<double *>(base);                // [n]
+    float *best32 = reinterpret_cast<float *>(base + 8 * (size_t)n);  // [n]
+    unsigned char *taken = base + 12 * (size_t)n;                   // [n]
     int *top = reinterpret_cast<int *>(taken + ((n + 3) & ~3));  // [M]
-    int *topn = top + M;                                         // [N]
+    int *topn = top + (M > kObsMB ? M : kObsMB);                 // [N]
     int *oth = topn + N;                                         // [N][M2], ascending
+    uint32_t *tmask = reinterpret_cast<uint32_t *>(oth + N * M2);  // [ceil(m / 32)]
     const int *myA = st.topA + (e * n + i) * (int64_t)M;
-    for (int c = lane; c < M; c += 64) top[c] = myA[c];
+    for (int c = lane; c < M || c < kObsMB; c += 64) top[c] = myA[c < M ? c : 0];
     wave_sync();
-    // (b) each agent's best total over agent i's top-M tasks, agent i excluded (:196-198)
-    const double *totT = st.totT + e * (int64_t)n * m;
-    for (int a = lane; a < n; a += 64) {
-        double b = totT[(int64_t)top[0] * n + a];
-        for (int c = 1; c < ((ASG_REAL_PROF_SKIP & 4) ? 1 : M); ++c) {
-            const double v = totT[(int64_t)top[c] * n + a];
+    // (b) each agent's best total over agent i's top-M tasks, agent i excluded (:196-198), from
+    //     the float32-rounded totals: rounding is monotone, so f32(x) < f32(y) implies x < y
+    const float *totT = st.totT + e * (int64_t)n * m;
+    const int Mb = (ASG_REAL_PROF_SKIP & 4) ? 1 : M;
+    bool nan_seen = false;
+    int a_done = 0;
+    if (ASG_OBS_PIPE && Mb <= kObsMB) {
+        // the rows of agent i's top tasks as wave-uniform (scalar) bases, lanes along the agents,
+        // two 64-agent groups in flight: group t + 1's loads are issued before group t is reduced
+        const float *rowp[kObsMB];
+#pragma unroll
+        for (int c = 0; c < kObsMB; ++c)
+            rowp[c] = totT + (int64_t)__builtin_amdgcn_readfirstlane(top[c]) * n;  // (c >= M: the padding)
+        // (every load unconditional -- rows past M repeat row top[0], groups past the last repeat
+        // it -- so each reduce waits on a fixed count of the loads in flight)
+        const int groups = (n + 63) >> 6;
+        float va[kObsMB], vb[kObsMB];
+        auto issue = [&](float (&v)[kObsMB], int g) {
+            const int a = min(lane + 64 * min(g, groups - 1), n - 1);
+#pragma unroll
+            for (int c = 0; c < kObsMB; ++c) v[c] = rowp[c][a];
+        };
+        auto reduce = [&](const float (&v)[kObsMB], int g) {
+            const int a = lane + 64 * g;
+            float b = v[0];
+            bool bad = b != b;
+#pragma unroll
+            for (int c = 1; c < kObsMB; ++c) {
+                const bool on = c < Mb;
+                bad |= on && v[c] != v[c];
+                b = on && v[c] > b ? v[c] : b;
+            }
+            if (g < groups && a < n) {
+                nan_seen |= bad;
+                best32[a] = a == i ? -INFINITY : b;
+                taken[a] = 0;
+            }
+        };
+        issue(va, 0);
+        for (int g = 0; g < groups; g += 2) {
+            issue(vb, g + 1);
+            reduce(va, g);
+            issue(va, g + 2);
+            reduce(vb, g + 1);
+        }
+        a_done = n;
+    }
+    for (int a = a_done + lane; a < n; a += 64) {
+        float b = totT[(int64_t)top[0] * n + a];
+        nan_seen |= b != b;
+        for (int c = 1; c < Mb; ++c) {
+            const float v = totT[(int64_t)top[c] * n + a];
+            nan_seen |= v != v;
             b = v > b ? v : b;
         }
-        best[a] = a == i ? -INFINITY : b;
+        best32[a] = a == i ? -INFINITY : b;
         taken[a] = 0;
     }
     wave_sync();
-    // (c) the N strongest competitors (np.argsort(-best)[:N])
+    const double *tab = st.table + e * st.table_env_stride;
+    // (c) the N strongest competitors (np.argsort(-best)[:N]): ranked by the float32 keys; the
+    //     float64 order is the same unless keys tie (among the N picks, or with the N-th) or are
+    //     NaN -- then the exact float64 best of every agent whose key reaches the N-th pick's
+    //     (any agent outside that set has N keys strictly above it) is recomputed from the table
+    //     the way the strip summed it, the others are -inf, and the float64 ranking decides
     if (!(ASG_REAL_PROF_SKIP & 8)) {
-        wave_topk<CAP, false>(best, n, N, topn, taken);
+        const bool anynan = __ballot(nan_seen) != 0;
+        bool exact = anynan;
+        float tau = -INFINITY;
+        if (!exact) {
+            wave_topk<CAP, false, float>(best32, n, N, topn, taken);
+            tau = best32[topn[N - 1]];
+            int ties = 0;
+            for (int a = lane; a < n; a += 64) ties += best32[a] == tau;
+            for (int q = lane; q + 1 < N; q += 64) ties += 2 * (best32[topn[q]] == best32[topn[q + 1]]);
+            exact = wave_allreduce(ties, [](int x, int y) { return x + y; }) > 1;
+        }
+        if (exact) {
+            auto total = [&](int a, int j) {  // the strip's L-sum of beta[a, j, :]
+                double sum = 0.0;
+                for (int l = 0; l < L; ++l) {
+                    const double b = real_beta(st, tab, knew, a, j, l);
+                    sum = l == 0 ? b : sum + b;
+                }
+                return sum;
+            };
+            for (int a = lane; a < n; a += 64) {
+                double b = -INFINITY;
+                if (a != i && (anynan || !(best32[a] < tau))) {
+                    b = total(a, top[0]);
+                    for (int c = 1; c < Mb; ++c) {
+                        const double v = total(a, top[c]);
+                        b = v > b ? v : b;
+                    }
+                }
+                best[a] = b;
+            }
+            wave_sync();
+            wave_topk<CAP, false>(best, n, N, topn, taken);
+        }
     } else {  // profiling: valid placeholder competitors (agents 0..)
         for (int c = lane; c < N; c += 64) topn[c] = c;
         wave_sync();
     }
     // (d) competitor q's M/2 best tasks outside agent i's top M: the first M/2 entries of
     //     its topD list not in top[], stored ascending (largest picked first)
+    const int mw = (m + 31) / 32;
+    for (int w = lane; w < mw; w += 64) tmask[w] = 0u;
+    wave_sync();
+    for (int c = lane; c < M; c += 64) atomicOr(&tmask[top[c] >> 5], 1u << (top[c] & 31));
+    wave_sync();
+    auto in_top = [&](int j) { return ((tmask[j >> 5] >> (j & 31)) & 1u) != 0u; };
     for (int q = lane; q < N; q += 64) {
         const int *d = st.topD + (e * n + topn[q]) * (int64_t)MD;
         int got = 0;
-        for (int c = 0; c < MD && got < M2; ++c) {
-            const int j = d[c];
-            bool in_top = false;
-            for (int k = 0; k < M; ++k) in_top |= top[k] == j;
-            if (!in_top) oth[q * M2 + (M2 - 1 - got++)] = j;
+        if (MD <= kObsMD) {  // the whole list in one round trip
+            int dj[kObsMD];
+#pragma unroll
+            for (int c = 0; c < kObsMD; ++c) dj[c] = c < MD ? d[c] : 0;
+#pragma unroll
+            for (int c = 0; c < kObsMD; ++c) {
+                if (c < MD && got < M2 && !in_top(dj[c])) {
+                    oth[q * M2 + (M2 - 1 - got)] = dj[c];
+                    ++got;
+                }
+            }
+        } else {
+            for (int c = 0; c < MD && got < M2; ++c) {
+                const int j = d[c];
+                if (!in_top(j)) oth[q * M2 + (M2 - 1 - got++)] = j;
+            }
         }
     }
     wave_sync();
     // (e) the observation row: local, neighbouring, neighbouring-other benefits, assigns
-    const double *tab = st.table + e * st.table_env_stride;
     const int pi = st.prev[e * n + i];
     const int64_t o0 = foff(bv.obs, e, row, i, 0);
     const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L, r4 = r3 + M;
@@ -1099,7 +1215,7 @@ int asg_real_create(const asg_real_config *cfg, int device, void *hip_stream, as
     if (e == hipSuccess) e = hipMalloc(&st.prev, sizeof(int) * (size_t)st.E * n);
     if (e == hipSuccess) e = hipMalloc(&st.power, sizeof(double) * (size_t)st.E * n);
     if (e == hipSuccess) e = hipMalloc(&st.returns, sizeof(double) * (size_t)st.E);
-    if (e == hipSuccess) e = hipMalloc(&st.totT, sizeof(double) * (size_t)st.E * n * m);
+    if (e == hipSuccess) e = hipMalloc(&st.totT, sizeof(float) * (size_t)st.E * n * m);
     if (e == hipSuccess) e = hipMalloc(&st.topA, sizeof(int) * (size_t)st.E * n * cfg->M);
     if (e == hipSuccess) e = hipMalloc(&st.topD, sizeof(int) * (size_t)st.E * n * (cfg->M + cfg->M / 2));
     if (e == hipSuccess) e = hipMalloc(&st.err, sizeof(int));
