@@ -413,12 +413,27 @@ __host__ __device__ __forceinline__ size_t strip_lds(int S, int m) {
 #define ASG_OBS_TWOPHASE 1
 #endif
 constexpr int kStripJG = ASG_STRIP_JG, kStripLM = 3;
+// the deferred-store path (m <= 64 kStripIt, L <= kStripLM): the whole row is loaded (two task
+// iterations in flight) and reduced into registers -- float16 beta packed, the totals in LDS --
+// before any of its global stores, so no load waits behind a store's acknowledgement
+#ifndef ASG_STRIP_DEFER
+#define ASG_STRIP_DEFER 1
+#endif
+constexpr int kStripIt = 8;
 // ASG_STRIP_WAVES: waves per SIMD the strip kernel is compiled for (0: the allocator's choice).
 // 8 (64 VGPRs, a few spills outside the row loop) measured 1.69 ms per real step at E = 512 against
 // 1.83 at 7 waves and 1.90 at the allocator's 80 VGPRs (profiles/r6_real_ab_s8.txt)
 #ifndef ASG_STRIP_WAVES
 #define ASG_STRIP_WAVES 8
 #endif
+// a buffer descriptor the compiler can prove wave-uniform (base and size through readfirstlane)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uint64_t)lo | ((uint64_t)hi << 32)), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 template <int CAP>
 __global__ void __launch_bounds__(1024)
 #if ASG_STRIP_WAVES
@@ -439,7 +454,7 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
     // one wave per agent row of the strip, lanes along the tasks: per row the field bases
     // are computed once; the scheme's own dtypes (f16 beta, bool avail, i16 one-hot) take
     // typed stores, anything else the generic ones
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, waves = blockDim.x >> 6;
     // (bids_as_actions: no actions_onehot field -- the scheme has no preprocess, :110-112)
     const bool fast = bv.beta.dtype == ASG_F16 && bv.avail_actions.dtype == ASG_BOOL &&
                       (!step || !bv.actions_onehot.ptr || bv.actions_onehot.dtype == ASG_I16) && bv.beta.ptr &&
@@ -452,7 +467,78 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
         eff = eff < 0 ? 0 : eff;
         const int pa = prev[i];
         double *trow = tl + (int64_t)r * m;
-        if (ASG_STRIP_GROUPED && fast && L <= kStripLM) {
+        if (ASG_STRIP_DEFER && fast && L == 3 && m <= 64 * kStripIt && bv.beta.stride[3] == 3 &&
+            bv.avail_actions.stride[3] == 1 && (!step || !bv.actions_onehot.ptr || bv.actions_onehot.stride[3] == 1)) {
+            // buffer descriptors over the row's slices and fields: 32-bit lane offsets, and the
+            // range check zeroes the loads (and drops the stores) of tasks past m and of slices
+            // past the episode end -- every memory instruction below is unconditional
+            const bool oh = step && bv.actions_onehot.ptr;
+            __amdgpu_buffer_rsrc_t rs[kStripLM];
+#pragma unroll
+            for (int l = 0; l < kStripLM; ++l) rs[l] = uniform_rsrc(t0 + l * slice, l < eff ? (uint32_t)m * 8u : 0u);
+            const __amdgpu_buffer_rsrc_t rp = uniform_rsrc(st.prios, (uint32_t)m * 8u);
+            double va[kStripLM], vb[kStripLM], pra, prb;
+            const uint32_t off = 8u * (uint32_t)lane;
+            auto issue = [&](double (&v)[kStripLM], double &pr, int it) {  // iteration it: + 512 it bytes
+                pr = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rp, off, 512 * it, 0));
+#pragma unroll
+                for (int l = 0; l < kStripLM; ++l)
+                    v[l] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs[l], off, 512 * it, 0));
+            };
+            uint32_t pk0[kStripIt], pk1[kStripIt];  // float16 beta: l0 | l1 << 16, l2
+            auto reduce = [&](const double (&v)[kStripLM], double pr, int it) {
+                const int j = 64 * it + lane;
+                double sum = 0.0;
+                uint32_t h[kStripLM];
+#pragma unroll
+                for (int l = 0; l < kStripLM; ++l) {
+                    const double b = v[l] * pr;  // (a zeroed slice: 0 * pr, as l >= eff reads 0)
+                    if (l < L) sum = l == 0 ? b : sum + b;
+                    h[l] = __half_as_ushort(__float2half((float)b));
+                }
+                if (j < m) trow[j] = sum;
+                pk0[it] = h[0] | (h[1] << 16);
+                pk1[it] = h[2];
+                // materialise the packed halves here: otherwise the conversions sink to the stores
+                // and the three float64 products of every iteration stay live until then
+                asm volatile("" : "+v"(pk0[it]), "+v"(pk1[it]));
+            };
+            issue(va, pra, 0);
+#pragma unroll
+            for (int it = 0; it < kStripIt; it += 2) {
+                issue(vb, prb, it + 1);
+                reduce(va, pra, it);
+                if (it + 2 < kStripIt) issue(va, pra, it + 2);
+                reduce(vb, prb, it + 1);
+            }
+            if (!(ASG_REAL_PROF_SKIP & 2)) {
+                const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(
+                    reinterpret_cast<__half *>(bv.beta.ptr) + foff(bv.beta, e, row, i, 0), 6u * (uint32_t)m);
+                const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(
+                    reinterpret_cast<uint8_t *>(bv.avail_actions.ptr) + foff(bv.avail_actions, e, row, i, 0), (uint32_t)m);
+                const __amdgpu_buffer_rsrc_t ro = uniform_rsrc(
+                    oh ? reinterpret_cast<int16_t *>(bv.actions_onehot.ptr) + foff(bv.actions_onehot, e, ts, i, 0)
+                       : nullptr,
+                    oh ? 2u * (uint32_t)m : 0u);
+                // beta: 6 bytes per task at 2-byte alignment -> one dword + one short; task j = 64 it
+                // + lane starts at byte 384 it + 6 lane, so the alignment is the lane's for every
+                // iteration and the iteration is an immediate offset
+                const uint32_t base_odd = (uint32_t)(reinterpret_cast<uintptr_t>(bv.beta.ptr) +
+                                                     2 * foff(bv.beta, e, row, i, 0)) & 2u;
+                const bool al = ((6u * (uint32_t)lane + base_odd) & 3u) == 0u;
+                const uint32_t odw = 6u * (uint32_t)lane + (al ? 0u : 2u), osh = 6u * (uint32_t)lane + (al ? 4u : 0u);
+#pragma unroll
+                for (int it = 0; it < kStripIt; ++it) {
+                    const uint32_t h0 = pk0[it] & 0xffffu, h1 = pk0[it] >> 16, h2 = pk1[it];
+                    __builtin_amdgcn_raw_buffer_store_b32(al ? pk0[it] : (h1 | (h2 << 16)), rb, odw, 384 * it, 0);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(al ? h2 : h0), rb, osh, 384 * it, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)1, ra, (uint32_t)lane, 64 * it, 0);
+                    if (oh)
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(pa == 64 * it + lane), ro, 2u * (uint32_t)lane,
+                                                              128 * it, 0);
+                }
+            }
+        } else if (ASG_STRIP_GROUPED && fast && L <= kStripLM) {
             // the row's table values in groups of kStripJG task iterations: every load of a group
             // (the L slices and the priorities) is issued before the group's stores -- gfx9 retires
             // loads and stores in order, so a load issued behind a store waits for its acknowledgement
@@ -583,7 +669,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, N = st.N, M = st.M, M2 = st.M / 2, MD = st.M + st.M / 2;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = blockDim.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, waves = blockDim.x >> 6;
     const int64_t k = blockIdx.x / 8;
     const int64_t e = (int64_t)(blockIdx.x % 8) + 8 * (k / G);
     const int i = (int)(k % G) * waves + wave;

@@ -65,12 +65,15 @@ def test_real_env_matches_reference_fixture(golden):
 
 @pytest.mark.parametrize("n,m,T,L,N,M,sparse", [(16, 24, 6, 3, 4, 6, True), (20, 20, 5, 2, 19, 4, False),
                                                 (33, 70, 4, 3, 5, 10, True), (8, 9, 3, 5, 2, 2, True),
-                                                (20, 30, 4, 3, 6, 6, "near"), (33, 70, 5, 3, 5, 10, "near")])
+                                                (20, 30, 4, 3, 6, 6, "near"), (33, 70, 5, 3, 5, 10, "near"),
+                                                (15, 27, 5, 3, 4, 6, True)])
 def test_real_env_matches_oracle_per_env_tables(oracle, n, m, T, L, N, M, sparse):
     """Per-env tables, random actions; sparse tables make many equal totals, so this
     checks the stable tie rule the GPU and the oracle share.  "near": quarter-step values
     plus offsets of a few 2**-36 -- the competitors' best totals tie as float32 keys but not
-    as float64, so the observation pass must take its exact float64 re-ranking."""
+    as float64, so the observation pass must take its exact float64 re-ranking.  Odd m with
+    L = 3: agent rows of beta start at both 4-byte alignments (the strip's dword + short
+    stores)."""
     E = 5
     rng = np.random.RandomState(n * 100 + m)
     tables = rng.uniform(0.0, 1.0, size=(E, n, m, T))
