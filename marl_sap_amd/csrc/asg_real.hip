@@ -136,8 +136,10 @@ __device__ __forceinline__ int wave_select(const V *vals, unsigned char *taken, 
 // monotone, so a unique maximal key is the unique float64 maximum; equal keys take the
 // exact path (float64 compare against the first candidate, then the index rule).  The
 // winning lane shifts its index list -- no rescans.  (V = float: the keys are the values.)
+// The picks go out 64 at a time, lane k holding pick k (one store instead of one per pick);
+// the return value is lane k's pick k for k < min(K, 64) (-1 past K).
 template <int CAP, bool HIGHER_TIES, class V = double>
-__device__ __forceinline__ void wave_topk_heads(const V *vals, int len, int K, int *out) {
+__device__ __forceinline__ int wave_topk_heads(const V *vals, int len, int K, int *out) {
     const int lane = threadIdx.x & 63;
     int id[CAP];
     {
@@ -166,6 +168,7 @@ __device__ __forceinline__ void wave_topk_heads(const V *vals, int len, int K, i
                     id[c + 1] = ti;
                 }
     }
+    int mine = -1, first = -1;
     for (int k = 0; k < K; ++k) {
         const bool has = id[0] >= 0;
         const V x = has ? vals[id[0]] : (V)-INFINITY;
@@ -199,13 +202,18 @@ __device__ __forceinline__ void wave_topk_heads(const V *vals, int len, int K, i
             wl = (int)__builtin_ctzll(__ballot(has && id[0] == win));
         }
         const int win = __builtin_amdgcn_readlane(id[0], wl);
-        if (lane == 0) out[k] = win;
+        if (lane == (k & 63)) mine = win;
+        if ((k & 63) == 63 || k == K - 1) {
+            if (lane <= (k & 63)) out[(k & ~63) + lane] = mine;
+            if (k < 64) first = mine;
+        }
         if (lane == wl) {
 #pragma unroll
             for (int c = 0; c + 1 < CAP; ++c) id[c] = id[c + 1];
             id[CAP - 1] = -1;
         }
     }
+    return K > 0 ? first : -1;
 }
 
 // top-K: register heads when len <= 64 * CAP (CAP > 0, chosen per kernel instance so each
@@ -213,7 +221,7 @@ __device__ __forceinline__ void wave_topk_heads(const V *vals, int len, int K, i
 template <int CAP, bool HIGHER_TIES, class V = double>
 __device__ __forceinline__ void wave_topk(const V *vals, int len, int K, int *out, unsigned char *taken) {
     if constexpr (CAP > 0) {
-        wave_topk_heads<CAP, HIGHER_TIES, V>(vals, len, K, out);
+        (void)wave_topk_heads<CAP, HIGHER_TIES, V>(vals, len, K, out);
     } else {
         const int lane = threadIdx.x & 63;
         for (int j = lane; j < len; j += 64) taken[j] = 0;
@@ -640,17 +648,36 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
             }
             continue;
         }
-        wave_topk<CAP, false>(vals, m, M, st.topA + (e * n + a) * (int64_t)M, taken);
-        wave_topk<CAP, true>(vals, m, MD, st.topD + (e * n + a) * (int64_t)MD, taken);
+        int *outA = st.topA + (e * n + a) * (int64_t)M, *outD = st.topD + (e * n + a) * (int64_t)MD;
+        if constexpr (CAP > 0) {
+            // topD first; when its first M + 1 totals are strictly decreasing (no tie can reorder
+            // or swap the M best: every other task is <= the (M+1)-th), topA is its first M
+            if (MD <= 64) {
+                const int d = wave_topk_heads<CAP, true>(vals, m, MD, outD);
+                const double v = lane <= M && d >= 0 ? vals[d] : 0.0;
+                const double vn = __shfl_down(v, 1);
+                if (__ballot(lane < M && !(v > vn)) == 0) {
+                    if (lane < M) outA[lane] = d;
+                } else {
+                    (void)wave_topk_heads<CAP, false>(vals, m, M, outA);
+                }
+                wave_sync();
+                continue;
+            }
+        }
+        wave_topk<CAP, false>(vals, m, M, outA, taken);
+        wave_topk<CAP, true>(vals, m, MD, outD, taken);
     }
 }
 
 // ---- kernel 3: observation rows, one wave per agent ---------------------------------------
 // per-wave LDS of the observation pass: best[n] f64, best32[n] f32, taken[n], top[max(M, 10)]
-// (padded with top[0]), topn[N], oth[N][M/2], tmask[ceil(m / 32)] (agent i's top-M tasks as a bit set)
+// (padded with top[0]), topn[N], oth[N][M/2], tmask[ceil(m / 32)] (agent i's top-M tasks as a bit
+// set), slot[M + N M + N M/2] (the (agent, task) of each L-run of the row's benefit entries)
 __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, int N, int M) {
     const int Mp = M > 10 ? M : 10;
-    return ((size_t)n * 13 + 3 + 4 * (size_t)(Mp + N + N * (M / 2) + (m + 31) / 32) + 15) & ~(size_t)15;
+    return ((size_t)n * 13 + 3 + 4 * (size_t)(Mp + N + N * (M / 2) + (m + 31) / 32 + M + N * M + N * (M / 2)) + 15) &
+           ~(size_t)15;
 }
 
 // Observation pass, one wave per (env, agent i): competitors from the task-major totals,
@@ -688,6 +715,7 @@ real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     int *topn = top + (M > kObsMB ? M : kObsMB);                 // [N]
     int *oth = topn + N;                                         // [N][M2], ascending
     uint32_t *tmask = reinterpret_cast<uint32_t *>(oth + N * M2);  // [ceil(m / 32)]
+    uint32_t *slot = tmask + (m + 31) / 32;                         // [M + N M + N M2]
     const int *myA = st.topA + (e * n + i) * (int64_t)M;
     for (int c = lane; c < M || c < kObsMB; c += 64) top[c] = myA[c < M ? c : 0];
     wave_sync();
@@ -853,29 +881,58 @@ real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
         }
         store_real(bv.obs, o0 + p, real_beta(st, tab, knew, a, j, l));
     };
-    if (ASG_OBS_TWOPHASE && copy && bv.obs.dtype == ASG_F16 && osz <= 64 * kObsG && !(ASG_REAL_PROF_SKIP & 16)) {
+    if (ASG_OBS_TWOPHASE && copy && bv.obs.dtype == ASG_F16 && osz <= 64 * kObsG && n < 65536 && m < 65536 &&
+        !(ASG_REAL_PROF_SKIP & 16)) {
         // the row's benefit entries gathered from the beta row first, then stored: a load issued
-        // behind a store waits for its acknowledgement (gfx9's in-order vmcnt)
+        // behind a store waits for its acknowledgement (gfx9's in-order vmcnt).  Entry p is
+        // element p % L of L-run p / L, whose (agent, task) the slot table holds
+        const int nsl = M + N * M + N * M2;
+        for (int sx = lane; sx < nsl; sx += 64) {
+            int a, j;
+            if (sx < M) {
+                a = i, j = top[sx];
+            } else if (sx < M + N * M) {
+                const int x = sx - M, q = x / M;
+                a = topn[q], j = top[x - q * M];
+            } else {
+                const int x = sx - M - N * M, q = x / M2;
+                a = topn[q], j = oth[x];  // oth is [N][M2]: entry q * M2 + (x - q * M2) = x
+            }
+            slot[sx] = ((uint32_t)a << 16) | (uint32_t)j;
+        }
+        wave_sync();
         const uint16_t *bsrc = reinterpret_cast<const uint16_t *>(bv.beta.ptr) + b0;
         uint16_t *odst = reinterpret_cast<uint16_t *>(bv.obs.ptr) + o0;
-        uint16_t val[kObsG];
+        const int64_t bs2 = bv.beta.stride[2], bs3 = bv.beta.stride[3];
+        const int sq = 64 / L, sr = 64 - sq * L;  // +64 entries = +sq runs, +sr elements
+        uint32_t sv[kObsG];
+        const int sl0 = lane / L, l0 = lane - sl0 * L;
+        {
+            int sl = sl0, l = l0;
 #pragma unroll
-        for (int g = 0; g < kObsG; ++g) {
-            const int p = lane + 64 * g;
-            int a = -1, j = 0, l = 0;
-            if (p < r1) {
-                a = i, j = top[p / L], l = p % L;
-            } else if (p < r2) {
-                const int x = p - r1, q = x / (M * L), y = x - q * M * L;
-                a = topn[q], j = top[y / L], l = y % L;
-            } else if (p < r3) {
-                const int x = p - r2, q = x / (M2 * L), y = x - q * M2 * L;
-                a = topn[q], j = oth[q * M2 + y / L], l = y % L;
+            for (int g = 0; g < kObsG; ++g) {
+                if (64 * g >= r3) break;
+                sv[g] = lane + 64 * g < r3 ? slot[sl] : 0u;
+                l += sr;
+                sl += sq + (l >= L ? 1 : 0);
+                l -= l >= L ? L : 0;
             }
-            val[g] = (p < r3) ? bsrc[a * bv.beta.stride[2] + j * bv.beta.stride[3] + l] : (uint16_t)0;
+        }
+        uint16_t val[kObsG];
+        {
+            int l = l0;
+#pragma unroll
+            for (int g = 0; g < kObsG; ++g) {
+                if (64 * g >= r3) break;
+                const uint32_t t = sv[g];
+                val[g] = lane + 64 * g < r3 ? bsrc[(int64_t)(t >> 16) * bs2 + (int64_t)(t & 0xffffu) * bs3 + l] : (uint16_t)0;
+                l += sr;
+                l -= l >= L ? L : 0;
+            }
         }
 #pragma unroll
         for (int g = 0; g < kObsG; ++g) {
+            if (64 * g >= osz) break;
             const int p = lane + 64 * g;
             if (p < r3) {
                 odst[p] = val[g];
