@@ -673,10 +673,13 @@ real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
 // ---- kernel 3: observation rows, one wave per agent ---------------------------------------
 // per-wave LDS of the observation pass: best[n] f64, best32[n] f32, taken[n], top[max(M, 10)]
 // (padded with top[0]), topn[N], oth[N][M/2], tmask[ceil(m / 32)] (agent i's top-M tasks as a bit
-// set), slot[M + N M + N M/2] (the (agent, task) of each L-run of the row's benefit entries)
+// set), slot[M + N M + N M/2] (the (agent, task) of each L-run of the row's benefit entries; in
+// best32's place once the ranking is done, when it fits there -- at 324 x 450 that keeps a
+// 4-wave workgroup under 20 KB, 8 per CU)
 __host__ __device__ __forceinline__ size_t real_obs_lds_per_wave(int n, int m, int N, int M) {
     const int Mp = M > 10 ? M : 10;
-    return ((size_t)n * 13 + 3 + 4 * (size_t)(Mp + N + N * (M / 2) + (m + 31) / 32 + M + N * M + N * (M / 2)) + 15) &
+    const int nsl = M + N * M + N * (M / 2);
+    return ((size_t)n * 13 + 3 + 4 * (size_t)(Mp + N + N * (M / 2) + (m + 31) / 32 + (nsl > n ? nsl : 0)) + 15) &
            ~(size_t)15;
 }
 
@@ -715,8 +718,10 @@ real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     int *topn = top + (M > kObsMB ? M : kObsMB);                 // [N]
     int *oth = topn + N;                                         // [N][M2], ascending
     uint32_t *tmask = reinterpret_cast<uint32_t *>(oth + N * M2);  // [ceil(m / 32)]
-    uint32_t *slot = tmask + (m + 31) / 32;                         // [M + N M + N M2]
+    uint32_t *slot = M + N * M + N * M2 <= n ? reinterpret_cast<uint32_t *>(best32)  // [M + N M + N M2]
+                                             : tmask + (m + 31) / 32;
     const int *myA = st.topA + (e * n + i) * (int64_t)M;
+    const int pi = st.prev[e * n + i];  // (issued with the first load, used by the row's one-hot)
     for (int c = lane; c < M || c < kObsMB; c += 64) top[c] = myA[c < M ? c : 0];
     wave_sync();
     // (b) each agent's best total over agent i's top-M tasks, agent i excluded (:196-198), from
@@ -854,7 +859,6 @@ real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     }
     wave_sync();
     // (e) the observation row: local, neighbouring, neighbouring-other benefits, assigns
-    const int pi = st.prev[e * n + i];
     const int64_t o0 = foff(bv.obs, e, row, i, 0);
     const int r1 = M * L, r2 = r1 + N * M * L, r3 = r2 + N * M2 * L, r4 = r3 + M;
     const double *pw = st.power + e * n;
