@@ -137,7 +137,8 @@ __device__ __forceinline__ int wave_select(const V *vals, unsigned char *taken, 
 // exact path (float64 compare against the first candidate, then the index rule).  The
 // winning lane shifts its index list -- no rescans.  (V = float: the keys are the values.)
 // The picks go out 64 at a time, lane k holding pick k (one store instead of one per pick);
-// the return value is lane k's pick k for k < min(K, 64) (-1 past K).
+// the return value is lane k's pick k for k < min(K, 64) (-1 past K).  (Keeping float32
+// values in registers beside the indices instead of re-reading them measured no faster.)
 template <int CAP, bool HIGHER_TIES, class V = double>
 __device__ __forceinline__ int wave_topk_heads(const V *vals, int len, int K, int *out) {
     const int lane = threadIdx.x & 63;
@@ -445,7 +446,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *p, ui
 template <int CAP>
 __global__ void __launch_bounds__(1024)
 #if ASG_STRIP_WAVES
-__attribute__((amdgpu_waves_per_eu(ASG_STRIP_WAVES)))
+__attribute__((amdgpu_waves_per_eu(CAP >= 16 ? 4 : ASG_STRIP_WAVES)))  // (CAP 16: m > 512, registers first)
 #endif
 real_strip_kernel(asg_batch_view bv, asg_field pfield, RealState st, int ts,
                                                           int knew, int step, int S) {
@@ -695,7 +696,7 @@ constexpr int kObsMB = 10; // top tasks per agent held in registers by the compe
 #define ASG_OBS_PIPE 1
 #endif
 template <int CAP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAP >= 16 ? 4 : 8)))
 real_obs_kernel(asg_batch_view bv, RealState st, int row, int knew, int G) {
     extern __shared__ unsigned char s_raw[];
     const int n = st.n, m = st.m, L = st.L, N = st.N, M = st.M, M2 = st.M / 2, MD = st.M + st.M / 2;
