@@ -546,11 +546,13 @@ def run_leg(a, dev, world, E, steps, warmup, selector=None, agent=None, count_ls
                 state["mode"] = "random_episode" if fused_sched else None
             else:
                 state["mode"] = mac.fused_mode(env, runner.batch, runner.t_env)
-        # (the random policy's launch folds the reset in the Philox mode only: the MT19937 reset
-        # is its draw kernels, run by random_rollout itself before the launch)
-        state["fuse_reset"] = bool(a.fuse_reset) and (
-            state["mode"] == "episode" or (state["mode"] == "random_episode" and env.rng == "philox")
-            or (state["mode"] == "step_q" and mac.fused_reset_ok(env)))  # asg_reset_forward
+            # (the random policy's launch folds the reset in the Philox mode only: the MT19937 reset
+            # is its draw kernels, run by random_rollout itself before the launch); asg_reset_forward
+            # for step_q -- asked under no_grad, as the runner's rollout() asks it (the fused
+            # paths require inference mode)
+            state["fuse_reset"] = bool(a.fuse_reset) and (
+                state["mode"] == "episode" or (state["mode"] == "random_episode" and env.rng == "philox")
+                or (state["mode"] == "step_q" and mac.fused_reset_ok(env)))
         if not state["fuse_reset"]:
             env.reset(runner.batch, ts=0)
 
@@ -966,15 +968,19 @@ def main():
             for name, sel_, yaml in (("iql", "eps", "mock_constellation_iql.yaml"),
                                      ("reda", "sap", "mock_constellation_reda.yaml")):
                 eps_over = dict(epsilon_start=1.0, epsilon_finish=0.0, epsilon_anneal_time=20000)
-                rj = run_leg(a, dev, world, E, sk, a.T, selector=sel_, agent="rnn", count_lsa=sel_ == "sap", **js,
+                # two warmup episodes: the jumpstart (HAA) one at t_env = 0, then one RL episode, so the
+                # timed episodes are the steady state (the RL path's first-use allocations -- the Q
+                # buffer, the warm-start duals -- happen in the warmup, as in any longer run)
+                rj = run_leg(a, dev, world, E, sk, 2 * a.T, selector=sel_, agent="rnn", count_lsa=sel_ == "sap", **js,
                              **eps_over)
                 extra[name] = {
                     **leg_base(rj, sk, a.T),
                     "what": f"{yaml}: jumpstart_mac (haa_selector jumpstart) + "
                             f"{'epsilon_greedy' if sel_ == 'eps' else 'sap'} selector, RNNAgent use_rnn False "
                             f"(Linear + ReLU, fused split-f16 kernel), both epsilons 1 -> 0 over 20,000 env steps; "
-                            f"timed after one warmup episode (the jumpstart/HAA phase, t_env = 0)",
-                    "jumpstart_phase_value": round(rj["global_envs"] * a.T / rj["warmup_elapsed"], 1),
+                            f"timed after two warmup episodes (the jumpstart/HAA phase at t_env = 0, then one RL "
+                            f"episode)",
+                    "warmup_value": round(rj["global_envs"] * 2 * a.T / rj["warmup_elapsed"], 1),
                     "kernels_ms": sap_kernels(rj) if sel_ == "sap" else {
                         "fused_rollout_per_step": round(rj["fused_ms"], 4) if rj["fused_ms"] else None,
                         "env_step": round(rj["kern_ms"], 4) if rj["kern_ms"] else None,

@@ -44,6 +44,16 @@ class SequentialAssignmentProblemSelector:
         # Assignments do not depend on it (certified or solved by scipy's algorithm).
         self.warm_start = bool(getattr(args, "sap_warm_start", True))
         self._duals = None
+        # an episode's first selection solves a new env's Q: by default it still starts from the
+        # previous episode's last duals (measured faster than a cold start: 1.20 vs 1.43 ms for
+        # the reset + forward + first selection at configs[2], profiles/r6_reda_cold_warm_s23.txt);
+        # args.sap_warm_across_episodes = False starts it cold
+        self.warm_across_episodes = bool(getattr(args, "sap_warm_across_episodes", True))
+        self._cold_next = False
+
+    def episode_start(self):
+        """The next selection is the first of an episode (called by the MAC at t_ep = 0)."""
+        self._cold_next = not self.warm_across_episodes
 
     def _env_index_base(self):
         return env_index_base(self)
@@ -71,8 +81,9 @@ class SequentialAssignmentProblemSelector:
                     status = self.status.sticky(B, q.device)  # min-accumulated by the kernel
                     if self.warm_start and n == m:
                         d = self._duals
-                        warm = int(d is not None and d.shape[0] == B and d.device == q.device)
-                        if not warm:
+                        warm = int(d is not None and d.shape[0] == B and d.device == q.device and not self._cold_next)
+                        self._cold_next = False
+                        if d is None or d.shape[0] != B or d.device != q.device:
                             d = self._duals = torch.empty((B, 64), dtype=torch.float64, device=q.device)
                         _lib.check(_lib.lib().asg_sap_select_warm(
                             *common, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(status.data_ptr()), steps,

@@ -49,6 +49,8 @@ class BasicMAC:
                 out, status, env_index_base=base)
             return out
         agent_outputs = self.forward(ep_batch, t_ep, test_mode=test_mode, action_selection_mode=True)
+        if t_ep == 0 and hasattr(self.action_selector, "episode_start"):
+            self.action_selector.episode_start()
         kw = {"out": out} if out is not None and _accepts_out(self.action_selector) else {}
         return self.action_selector.select_action(agent_outputs[bs], avail_actions[bs], t_env,
                                                   test_mode=test_mode, beta=ep_batch["beta"][bs, t_ep], **kw)
@@ -146,6 +148,8 @@ class BasicMAC:
         asg_bids_select (the bids row and its LSA)."""
         self._q_buf = q
         B = ep_batch.batch_size
+        if t == 0 and hasattr(self.action_selector, "episode_start"):
+            self.action_selector.episode_start()
         if self._fused_bids_ok():
             self.action_selector.fused_bids(q.view(B, self.n, -1), ep_batch["actions"][:, t], t_env, test_mode,
                                             row_softmax=self.agent_output_type == "pi_logits")

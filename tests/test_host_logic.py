@@ -317,3 +317,18 @@ def test_runner_flush_clears_env_error_when_selector_raises():
     assert r._pending == [] and r._pending_steps == []
     r.flush_pending()  # nothing stale left: no error, nothing logged twice
     assert r.env.syncs == 2
+
+
+def test_sap_selector_episode_start_warm_or_cold():
+    """The SAP selector's warm start carries duals from one selection to the next; the MAC's
+    episode_start() (t_ep = 0) makes the next call cold when args.sap_warm_across_episodes is
+    False (by default the previous episode's duals stay the start)."""
+    from marl_sap_amd.action_selectors.sap_selectors import SequentialAssignmentProblemSelector
+    base = dict(epsilon_start=0.1, epsilon_finish=0.1, epsilon_anneal_time=1, evaluation_epsilon=0.0)
+    keep = SequentialAssignmentProblemSelector(SimpleNamespace(**base))
+    keep.episode_start()
+    assert not keep._cold_next
+    cold = SequentialAssignmentProblemSelector(SimpleNamespace(**base, sap_warm_across_episodes=False))
+    assert not cold._cold_next
+    cold.episode_start()
+    assert cold._cold_next
