@@ -294,6 +294,51 @@ hipError_t launch_sap_select(const float *q, const int64_t qs[3], int64_t B, int
 #ifndef ASG_BIDS_WAVES
 #define ASG_BIDS_WAVES 5
 #endif
+// The row softmax's per-row max and sum over the 64 lanes, 16 rows at a time: rows 8g + j (a[j])
+// and 8g + j + 32 (b[j]), j < 8, folded by a transposing butterfly -- v_permlane32_swap /
+// v_permlane16_swap hand each lane its partner's copy of the rows it keeps (one instruction per
+// pair), then row_mirror / row_half_mirror DPP, then a quad reduction -- 17 cross-lane steps for
+// 16 rows instead of 16 wave reductions of 6 DPP steps and a broadcast each (one row-softmax pass
+// priced at 0.076 ms of the kernel's 0.497, profiles/r6_bids_rowsm_s25.txt).  Lane l ends with
+// row 8g + (l >> 2 & 7) + 32 (l >> 5) reduced over all lanes: row_lane16(r) is where row r is.
+#ifndef ASG_BIDS_ROW_GROUPS
+#define ASG_BIDS_ROW_GROUPS 1
+#endif
+__device__ __forceinline__ float f_of(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint32_t u_of(float f) { return __builtin_bit_cast(uint32_t, f); }
+template <class Op>
+__device__ __forceinline__ float rows16_reduce(const float (&a)[8], const float (&b)[8], Op op) {
+    const int lane = threadIdx.x & 63;
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // lanes < 32 keep row 8g + j, lanes >= 32 row 8g + j + 32
+        const auto r = __builtin_amdgcn_permlane32_swap(u_of(a[j]), u_of(b[j]), false, false);
+        t[j] = op(f_of(r[0]), f_of(r[1]));
+    }
+    float u[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // + 4 (lane bit 4)
+        const auto r = __builtin_amdgcn_permlane16_swap(u_of(t[j]), u_of(t[j + 4]), false, false);
+        u[j] = op(f_of(r[0]), f_of(r[1]));
+    }
+    const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+    float w[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // + 2 (lane bit 3): partner 15 - i in the 16-lane row
+        const float keep = b3 ? u[j + 2] : u[j], send = b3 ? u[j] : u[j + 2];
+        w[j] = op(keep, f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(send), 0x140, 0xf, 0xf, false)));
+    }
+    // + 1 (lane bit 2): partner 7 - i in the 8-lane half row
+    const float keep = b2 ? w[1] : w[0], send = b2 ? w[0] : w[1];
+    float v = op(keep, f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(send), 0x141, 0xf, 0xf, false)));
+    // the quad holds four disjoint 16-lane partials of the same row
+    v = op(v, f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(v), 0x4e, 0xf, 0xf, false)));
+    v = op(v, f_of((uint32_t)__builtin_amdgcn_update_dpp(0, (int)u_of(v), 0xb1, 0xf, 0xf, false)));
+    return v;
+}
+// the lane holding row r (r mod 32 in [8g, 8g + 8)) after rows16_reduce of its group
+__device__ __forceinline__ constexpr int row_lane16(int r) { return 32 * (r >> 5) + 4 * (r & 7); }
+
 // kCount: the instrumented instance (bench.py's efficiency figure): steps_out[b] = the env's
 // augmenting-path steps, fast path in bits 0..15, scipy-exact solver above (as asg_sap_select)
 template <bool kCount>
@@ -330,7 +375,45 @@ bids_select_kernel(const float *q, int64_t q0, int64_t q1, int64_t q2, int n, in
     };
     // exp as v_exp_f32 of x log2(e) (x = y - max <= 0: relative error <= |x| 2^-24 + 1 ulp; torch's
     // expf is within 1 ulp): the accurate expf unrolled over the 64 rows spilled at any budget
-    if (row_sm) {  // softmax(dim = -1) of each agent's row: exp(x - max) / sum, as torch
+#ifdef ASG_BIDS_TIMING_RS2  // timing only: one extra row-softmax pass, its results discarded
+    if (row_sm) {
+        each_row([&](float x, int) {
+            const float mx = wave_allreduce(lv ? x : -__builtin_inff(), [](float a, float c) { return fmaxf(a, c); });
+            const float ex = lv ? __expf(x - mx) : 0.0f;
+            const float sum = wave_allreduce(ex, [](float a, float c) { return a + c; });
+            const float r = ex / sum;
+            asm volatile("" ::"v"(r));
+            return x;
+        });
+    }
+#endif
+    if (row_sm && ASG_BIDS_ROW_GROUPS) {  // softmax(dim = -1) of each agent's row: exp(x - max) / sum
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float a[8], bb[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                a[j] = lv ? rc.lo[8 * g + j] : -__builtin_inff();
+                bb[j] = lv ? rc.hi[8 * g + j] : -__builtin_inff();
+            }
+            const float mx = rows16_reduce(a, bb, [](float x, float y) { return fmaxf(x, y); });
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float ma = f_of((uint32_t)__builtin_amdgcn_readlane((int)u_of(mx), row_lane16(8 * g + j)));
+                const float mb = f_of((uint32_t)__builtin_amdgcn_readlane((int)u_of(mx), row_lane16(8 * g + j + 32)));
+                a[j] = lv ? __expf(rc.lo[8 * g + j] - ma) : 0.0f;
+                bb[j] = lv ? __expf(rc.hi[8 * g + j] - mb) : 0.0f;
+            }
+            const float sm = rows16_reduce(a, bb, [](float x, float y) { return x + y; });
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sa = f_of((uint32_t)__builtin_amdgcn_readlane((int)u_of(sm), row_lane16(8 * g + j)));
+                const float sb = f_of((uint32_t)__builtin_amdgcn_readlane((int)u_of(sm), row_lane16(8 * g + j + 32)));
+                if (8 * g + j < n) rc.lo[8 * g + j] = a[j] / sa;
+                if (8 * g + j + 32 < n) rc.hi[8 * g + j] = bb[j] / sb;
+            }
+        }
+    } else if (row_sm) {  // softmax(dim = -1) of each agent's row: exp(x - max) / sum, as torch
         each_row([&](float x, int) {
             const float mx = wave_allreduce(lv ? x : -__builtin_inff(), [](float a, float c) { return fmaxf(a, c); });
             const float ex = lv ? __expf(x - mx) : 0.0f;
