@@ -1186,6 +1186,8 @@ def main():
                         "per-episode all-gather of the float64 returns) per episode inside the timed window"}
         if a.selector == "sap":
             line["roofline_lsa"] = lsa_roofline(a, E, res)
+        elif a.selector == "bids":
+            line["roofline_lsa"] = lsa_roofline(a, E, res, kernel="asg::bids_select_kernel", pmc="*pmc_bids_kernel*.json")
         if extra:
             line["secondary"] = extra
         print(json.dumps(line), flush=True)

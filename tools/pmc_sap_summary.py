@@ -22,17 +22,19 @@ def main():
     p.add_argument("--n", type=int, default=64)
     p.add_argument("--m", type=int, default=64)
     p.add_argument("--E", type=int, default=16384)
+    p.add_argument("--kernel", default="sap_select_kernel<false",
+                   help="kernel-name substring (bids: bids_select_kernel<false)")
     a = p.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(os.path.join(a.sq_dir, "run_counter_collection.csv"))):
-        if "sap_select_kernel<false" in r["Kernel_Name"]:
+        if a.kernel in r["Kernel_Name"]:
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
     n = len(per)
     avg = {c: sum(d[c] for d in per.values()) / n for c in next(iter(per.values()))}
     line = json.loads([x for x in open(a.bench_log).read().splitlines() if x.startswith("{")][-1])
     lsa = line.get("roofline_lsa") or line["secondary"]["sap"]["roofline_lsa"]
     steps = lsa["path_steps_per_launch"]
-    out = {"n": a.n, "m": a.m, "E": a.E, "kernel": "asg::sap_select_kernel<false, *>", "dispatches_averaged": n,
+    out = {"n": a.n, "m": a.m, "E": a.E, "kernel": "asg::" + a.kernel + ", *>", "dispatches_averaged": n,
            "counters": avg, "path_steps_per_launch": steps,
            "valu_insts_per_path_step": avg["SQ_INSTS_VALU"] / steps,
            "salu_insts_per_path_step": avg.get("SQ_INSTS_SALU", 0.0) / steps,
