@@ -139,6 +139,9 @@ __device__ __forceinline__ int wave_select(const V *vals, unsigned char *taken, 
 // The picks go out 64 at a time, lane k holding pick k (one store instead of one per pick);
 // the return value is lane k's pick k for k < min(K, 64) (-1 past K).  (Keeping float32
 // values in registers beside the indices instead of re-reading them measured no faster.)
+#ifndef ASG_TOPK_NET8
+#define ASG_TOPK_NET8 1
+#endif
 template <int CAP, bool HIGHER_TIES, class V = double>
 __device__ __forceinline__ int wave_topk_heads(const V *vals, int len, int K, int *out) {
     const int lane = threadIdx.x & 63;
@@ -156,18 +159,29 @@ __device__ __forceinline__ int wave_topk_heads(const V *vals, int len, int K, in
             if (ib < 0) return true;
             return va > vb || (va == vb && (HIGHER_TIES ? ia > ib : ia < ib));
         };
+        auto cswap = [&](int a, int b) {  // a < b: a gets the one that comes first
+            if (before(v[b], id[b], v[a], id[a])) {
+                const V tv = v[a];
+                v[a] = v[b];
+                v[b] = tv;
+                const int ti = id[a];
+                id[a] = id[b];
+                id[b] = ti;
+            }
+        };
+        if constexpr (CAP == 8 && ASG_TOPK_NET8) {
+            // the 19-comparator sorting network for 8 inputs (depth 6) in place of the
+            // 28-comparator odd-even transposition sort: same order (a total order on (value, index))
+            constexpr int kNet[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
+                                         {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
 #pragma unroll
-        for (int pass = 0; pass < CAP; ++pass)  // odd-even transposition sort, fully unrolled
+            for (int q = 0; q < 19; ++q) cswap(kNet[q][0], kNet[q][1]);
+        } else {
 #pragma unroll
-            for (int c = pass & 1; c + 1 < CAP; c += 2)
-                if (before(v[c + 1], id[c + 1], v[c], id[c])) {
-                    const V tv = v[c];
-                    v[c] = v[c + 1];
-                    v[c + 1] = tv;
-                    const int ti = id[c];
-                    id[c] = id[c + 1];
-                    id[c + 1] = ti;
-                }
+            for (int pass = 0; pass < CAP; ++pass)  // odd-even transposition sort, fully unrolled
+#pragma unroll
+                for (int c = pass & 1; c + 1 < CAP; c += 2) cswap(c, c + 1);
+        }
     }
     int mine = -1, first = -1;
     for (int k = 0; k < K; ++k) {
