@@ -169,7 +169,12 @@ __device__ __forceinline__ int wave_topk_heads(const V *vals, int len, int K, in
                 id[b] = ti;
             }
         };
-        if constexpr (CAP == 8 && ASG_TOPK_NET8) {
+        if constexpr (CAP == 6 && ASG_TOPK_NET8) {  // the 12-comparator network for 6 inputs
+            constexpr int kNet6[12][2] = {{0, 5}, {1, 3}, {2, 4}, {1, 2}, {3, 4}, {0, 3},
+                                          {2, 5}, {0, 1}, {2, 3}, {4, 5}, {1, 2}, {3, 4}};
+#pragma unroll
+            for (int q = 0; q < 12; ++q) cswap(kNet6[q][0], kNet6[q][1]);
+        } else if constexpr (CAP == 8 && ASG_TOPK_NET8) {
             // the 19-comparator sorting network for 8 inputs (depth 6) in place of the
             // 28-comparator odd-even transposition sort: same order (a total order on (value, index))
             constexpr int kNet[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
@@ -1238,10 +1243,11 @@ int rcheck_view(asg_real_handle *h, const asg_batch_view *b, bool step) {
     return ASG_OK;
 }
 
-// candidates per lane of a top-K over `len` values: 1, 2, 4, 8, 16, or 0 (> 1024: rescans)
+// candidates per lane of a top-K over `len` values: 1, 2, 4, 6, 8, 16, or 0 (> 1024: rescans);
+// 6 (257..384, e.g. the 324 satellites) sorts its lanes with a 12-comparator network
 int cap_of(int len) {
     const int c = (len + 63) / 64;
-    return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : c <= 8 ? 8 : c <= 16 ? 16 : 0;
+    return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : c <= 6 ? 6 : c <= 8 ? 8 : c <= 16 ? 16 : 0;
 }
 
 int strip_height(const RealState &st) {
@@ -1288,6 +1294,7 @@ hipError_t launch_real(asg_real_handle *h, const asg_real_batch_view &v, int ts,
         case 2: STRIP_(2); break;
         case 4: STRIP_(4); break;
         case 8: STRIP_(8); break;
+        case 6: STRIP_(6); break;
         case 16: STRIP_(16); break;
         default: STRIP_(0); break;
     }
@@ -1307,6 +1314,7 @@ hipError_t launch_real(asg_real_handle *h, const asg_real_batch_view &v, int ts,
         case 2: OBS_(2); break;
         case 4: OBS_(4); break;
         case 8: OBS_(8); break;
+        case 6: OBS_(6); break;
         case 16: OBS_(16); break;
         default: OBS_(0); break;
     }
